@@ -1,0 +1,146 @@
+#!/usr/bin/env python3
+"""Headline benchmark: cell-updates/sec (whole node) on a 32768^2 board per GPU.
+
+    python bench.py --gpus N --steps K --warmup W
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
+        --master-port P bench.py --gpus N --steps K --warmup W
+
+A *step* is one Game of Life generation (B3/S23) over the whole board.  Each rank owns one GPU and a
+32768 x 32768 tile (weak scaling, the reference's per-rank semantics: gol-main.c:76) — the global
+board is (N*32768) x 32768, a torus, with RCCL halo exchange over xGMI between ranks.  ``--scaling
+strong`` instead splits one 32768^2 board over the N GPUs.  The board is random (pattern 5,
+synthetic), the timed region runs every generation in full: W untimed warmup generations, barrier +
+device sync, K timed generations, device sync + barrier; the max over ranks is reported.  Metric =
+global cells x K / elapsed.  Without a GPU it falls back to the CPU backend on BASELINE config 1
+(256^2).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+
+METRIC = "cell-updates/sec (whole node) on 32768^2 board; 1/2/4/8-GPU weak+strong scaling"
+
+
+def main() -> int:
+    ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=4000, help="timed generations")
+    ap.add_argument("--warmup", type=int, default=400, help="untimed generations")
+    ap.add_argument("--size", type=int, default=32768, help="tile side per GPU (weak) / board side (strong)")
+    ap.add_argument("--scaling", choices=["weak", "strong"], default="weak")
+    ap.add_argument("--decomp", default="1d", help="1d | 2d | auto")
+    ap.add_argument("--halo-depth", type=int, default=int(os.environ.get("GOL_HALO_DEPTH", "8")))
+    ap.add_argument("--kernel", default=os.environ.get("GOL_KERNEL", "temporal"))
+    ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--no-overlap", action="store_true")
+    ap.add_argument("--yardstick", action="store_true", help="also time the naive byte-per-cell kernel (rank 0)")
+    ap.add_argument("--seed", type=int, default=0x5EED)
+    args = ap.parse_args()
+
+    import gol_amd
+    from gol_amd.parallel import init_distributed, rccl_transport, torch_transport
+
+    native = gol_amd.native
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus and world > 1:
+        print(f"[bench] warning: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+    have_gpu = native.hip_device_count() > 0
+    backend = "hip" if have_gpu else "cpu"
+    size, steps, warmup = args.size, args.steps, args.warmup
+    if not have_gpu:
+        size, steps, warmup = 256, min(steps, 100), min(warmup, 10)
+
+    rank, P, local, cpu_group = init_distributed()
+    if P > 1:
+        control = torch_transport(cpu_group)
+        transport = rccl_transport(control, group=cpu_group) if backend == "hip" else control
+    else:
+        transport = native.SelfTransport()
+
+    sim = gol_amd.Simulation(
+        size,
+        transport,
+        backend=backend,
+        global_mode=(args.scaling == "strong"),
+        decomp=args.decomp,
+        halo_depth=args.halo_depth,
+        graph=not args.no_graph,
+        overlap=not args.no_overlap,
+        kernel=args.kernel,
+        device=local if backend == "hip" else None,
+    )
+    sim.init(pattern=5, seed=args.seed)
+    dec = sim.decomposition
+    cells = dec.H * dec.W
+
+    sim.step(warmup)
+    sim.synchronize()
+    transport.barrier()
+    t0 = time.perf_counter()
+    sim.step(steps)
+    sim.synchronize()
+    t1 = time.perf_counter()
+    transport.barrier()
+    elapsed = transport.allreduce_max(t1 - t0)
+    pop = sim.population()
+
+    yard = None
+    if args.yardstick and rank == 0 and have_gpu:
+        ys = min(size, 16384)
+        yg = 50
+        t, _ = native.naive_byte_run(ys, yg, 256, True, args.seed)
+        yard = {"board": ys, "generations": yg, "cell_updates_per_s": ys * ys * yg / t}
+
+    if rank == 0:
+        value = cells * steps / elapsed
+        st = sim.stats()
+        out = {
+            "metric": METRIC,
+            "value": value,
+            "unit": "cell-updates/s",
+            "n_gpus": P if have_gpu else 0,
+            "steps": steps,
+            "warmup": warmup,
+            "ms_per_step": elapsed / steps * 1e3,
+            "higher_is_better": True,
+            "scaling": args.scaling,
+            "vs_baseline": None,
+            "dtype": "u1 bit-packed (64 cells per u64)",
+            "data": "synthetic (pattern 5: seeded random board, density 1/2)",
+            "config": {
+                "model": "Conway B3/S23 torus, bit-packed temporal-blocked HIP kernel",
+                "board": [dec.H, dec.W],
+                "tile_per_rank": [sim.geometry.h, sim.geometry.w],
+                "global_batch": cells,
+                "seq_len": None,
+                "parallelism": f"{'2d' if dec.Px > 1 else '1d'}-spatial p{P} ({dec.Px}x{dec.Py})",
+                "backend": backend,
+                "halo_depth": st["depth"],
+                "kernel": args.kernel,
+                "graph_launches": st["graph_launches"],
+                "plan_waves": st["plan_waves"],
+                "lane_efficiency": round(st["lane_efficiency"], 4),
+                "population": pop,
+            },
+            "baseline_note": "reference publishes no numbers (BASELINE.md); vs_baseline is null",
+        }
+        if yard:
+            out["yardstick_naive_byte_kernel"] = yard
+            out["speedup_vs_yardstick"] = value / (yard["cell_updates_per_s"] * P)
+        print(json.dumps(out), flush=True)
+    if P > 1:
+        import torch.distributed as dist
+
+        dist.barrier()
+        dist.destroy_process_group()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -1,0 +1,130 @@
+// gol-mi355x: the generation engine (superstep scheduler) — CPU and HIP backends.
+//
+// Reference loop (gol-main.c:93-116, gol-with-cuda.cu:264-284): for every generation, 2 Irecv +
+// 2 Isend of one byte row, wait for the receives, launch gol_kernel, cudaDeviceSynchronize, swap.
+//
+// Engine loop: generations are grouped into supersteps of k <= R generations.  Per superstep:
+//   1. halo refresh — exchange k-deep halos with the neighbours (canonical order, one transport call:
+//      1-D: 2 contiguous full-pitch row blocks sent straight from / received straight into the board;
+//      2-D: 8 packed regions incl. corners).  Self-neighbour directions need nothing: the kernel
+//      wraps rows / columns by addressing.
+//   2. compute — k generations in one pass of the temporal kernel.  With overlap, the interior
+//      (rows that only need local data) runs on the compute stream while the exchange runs on the
+//      comm stream; the boundary bands follow once the halo has landed.
+//   3. swap (parity flip).
+// On the HIP backend supersteps are captured into hipGraphs (pairs, so parity is preserved) and
+// replayed; there is no host synchronisation inside run().
+#pragma once
+
+#include <memory>
+#include <string>
+#include <utility>
+#include <vector>
+
+#include "gol/geometry.hpp"
+#include "gol/pattern.hpp"
+#include "gol/plan.hpp"
+#include "gol/transport.hpp"
+
+namespace gol {
+
+struct EngineConfig {
+    std::string backend = "cpu";      // cpu | hip
+    int halo_depth = 8;               // R: max generations per superstep (clamped to the geometry)
+    bool overlap = true;              // interior/boundary split with comm-stream exchange
+    bool graph = true;                // hipGraph capture of superstep pairs
+    bool compat = false;              // reference halo quirks (Q1/Q2), 1-D only, k = 1
+    int device = -1;                  // HIP device (-1: current)
+    i64 rows_per_wave = 0;            // plan segment height override (0 = auto)
+    int waves_target = 0;             // plan wave-count target (0 = auto)
+    std::string kernel = "temporal";  // temporal | lds
+    std::string transport = "auto";   // auto | device | host  (host = stage halos through host memory)
+    bool profile = false;             // per-phase event timing
+    int graph_supersteps = 0;         // supersteps per captured graph (0 = auto, even)
+};
+
+struct EngineStats {
+    u64 generations = 0;
+    u64 supersteps = 0;
+    u64 exchanges = 0;
+    u64 halo_bytes = 0;       // bytes sent by this rank
+    u64 graph_launches = 0;
+    int depth = 0;            // R
+    i64 plan_waves = 0;       // waves of the full-tile plan
+    double lane_efficiency = 0;  // output words / (64 * input rows * waves) for the full plan
+    double t_exchange_ms = 0;  // profile only
+    double t_compute_ms = 0;   // profile only
+};
+
+class Engine {
+   public:
+    static std::unique_ptr<Engine> create(const Geometry& g, const EngineConfig& c, std::shared_ptr<Transport> t);
+    virtual ~Engine() = default;
+
+    void init(const PatternSpec& p);
+    virtual void run(u64 generations);
+    virtual void synchronize() = 0;
+
+    // Local tile as dense masked words (h * nw), and the reverse (halos are refreshed).
+    virtual std::vector<u64> tile_words() = 0;
+    virtual void set_tile_words(const std::vector<u64>& dense) = 0;
+    // (population, fingerprint) of the local tile.
+    virtual std::pair<u64, u64> local_reduce() = 0;
+    // Global values (collective over the transport).
+    u64 population();
+    u64 fingerprint();
+
+    const Geometry& geometry() const { return g_; }
+    const Layout& layout() const { return L_; }
+    const EngineConfig& config() const { return cfg_; }
+    Transport& transport() { return *t_; }
+    std::shared_ptr<Transport> transport_ptr() { return t_; }
+    const EngineStats& stats() const { return stats_; }
+    u64 generation() const { return gen_; }
+    std::string describe() const;
+    virtual std::string backend_name() const = 0;
+
+    // One halo region in tile coordinates (rows [r0, r0+rows), words [c0, c0+words); c0 may be -1).
+    struct Rect {
+        i64 r0, rows, c0, words;
+        i64 count() const { return rows * words; }
+    };
+    struct HaloItem {
+        Dir d;
+        int send_peer, recv_peer;
+        Rect send, recv;
+        bool contiguous;  // full-pitch rows: can be sent straight from the board
+    };
+    // Canonical-order halo messages of a k-deep superstep (self directions omitted).
+    std::vector<HaloItem> halo_items(int k) const;
+    bool self_x() const { return g_.nbr[DIR_W] == g_.rank && g_.nbr[DIR_E] == g_.rank; }
+    bool self_y() const { return g_.nbr[DIR_N] == g_.rank && g_.nbr[DIR_S] == g_.rank; }
+    bool xwrap_by_plan() const { return self_x() && L_.aligned(); }
+
+   protected:
+    Engine(const Geometry& g, const EngineConfig& c, std::shared_ptr<Transport> t);
+    virtual void do_init(const PatternSpec& p) = 0;
+    virtual void do_superstep(int k) = 0;
+    // Compat mode: install constant depth-1 ghost rows (both buffers); rows are full-pitch.
+    virtual void do_set_compat_halos(const std::vector<u64>& above, const std::vector<u64>& below) = 0;
+    virtual std::vector<u64> read_row(i64 r) = 0;  // full-pitch row r of the current buffer
+    void setup_compat();
+    void maybe_inject_fault();
+
+    Geometry g_;
+    EngineConfig cfg_;
+    std::shared_ptr<Transport> t_;
+    Layout L_;
+    EngineStats stats_;
+    u64 gen_ = 0;
+    i64 fault_gen_ = -1;
+};
+
+std::unique_ptr<Engine> make_cpu_engine(const Geometry& g, const EngineConfig& c, std::shared_ptr<Transport> t);
+std::unique_ptr<Engine> make_hip_engine(const Geometry& g, const EngineConfig& c, std::shared_ptr<Transport> t);
+
+// HIP runtime helpers used by the CLI / bindings (no-ops without a GPU).
+int hip_device_count(int* err = nullptr);
+void hip_set_device(int dev);
+
+}  // namespace gol

@@ -1,0 +1,83 @@
+// gol-mi355x: host API of the hand-written gfx950 kernels (implemented in src/hip/*.hip).
+//
+// Kernel inventory (reference has one kernel, gol_kernel, gol-with-cuda.cu:189-262):
+//   step_temporal<K>  — K generations of B3/S23 per pass over a bit-packed tile: wave64 column
+//                       streaming, bit-sliced v_bitop3/v_alignbit adders, DPP wave_shr/shl lane
+//                       exchange, K-deep register pipeline (temporal blocking), periodic wrap by
+//                       load addressing.  Replaces gol_kernel + the per-generation sync/swap.
+//   step_lds          — single-generation LDS-tiled variant (tile + ghost words staged in LDS);
+//                       kept as a measured alternative (GOL_KERNEL=lds).
+//   fill_ghost_cols   — x-periodic ghost words for widths that are not a multiple of 64.
+//   fill_ghost_rows   — y-periodic ghost rows for a tile shorter than the halo depth.
+//   init_fill/set_cells — device-side pattern init (reference: host loops over managed memory).
+//   copy_regions      — batched strided copies: 2-D halo pack/unpack and self-neighbour copies.
+//   reduce_board      — population + decomposition-invariant fingerprint.
+//   naive_byte_step   — byte-per-cell, thread-per-cell yardstick of the reference's algorithm class
+//                       (no printf), used only by the benchmark for comparison.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include "gol/geometry.hpp"
+#include "gol/plan.hpp"
+
+namespace gol {
+namespace hipk {
+
+enum : u32 {
+    STEP_WRAP_X = 1u << 0,  // LDS kernel: tile is its own E/W neighbour (w % 64 == 0); the temporal
+                            // kernel gets x-wrap from its plan (build_plan(..., xwrap = true))
+    STEP_WRAP_Y = 1u << 1,  // tile is its own N/S neighbour: rows are read modulo h, no ghost rows
+};
+
+struct StepParams {
+    i64 pitch;
+    i32 h;
+    i32 nw;
+    i32 R;
+    u32 flags;
+};
+
+// Supported temporal depths (template instantiations).
+bool step_depth_supported(int k);
+int max_step_depth();
+// Launch K generations: src -> dst over the waves of `plan` (n_waves * 64 LaneDescs in device memory).
+void launch_step(int k, const u64* src, u64* dst, const LaneDesc* plan, i64 n_waves, const StepParams& p,
+                 hipStream_t s);
+// Single-generation LDS-tiled kernel over output rows [r0, r1) (all words).
+void launch_step_lds(const u64* src, u64* dst, const Layout& L, i64 r0, i64 r1, u32 flags, hipStream_t s);
+
+void launch_fill_ghost_cols(u64* buf, const Layout& L, i64 r_lo, i64 r_hi, hipStream_t s);
+void launch_fill_ghost_rows(u64* buf, const Layout& L, hipStream_t s);
+
+struct InitParams {
+    i64 row0;     // global row of tile row 0
+    i64 gword0;   // global word index of tile word 0
+    i64 gwords;   // words per global row
+    u64 seed;
+    int fill;     // 0 zero, 1 ones, 2 random
+};
+void launch_init_fill(u64* buf, const Layout& L, const InitParams& ip, hipStream_t s);
+// cells: device array of (row, col) tile coordinates
+void launch_set_cells(u64* buf, const Layout& L, const i64* cells, i64 n, hipStream_t s);
+
+struct CopyDesc {
+    const u64* src;
+    u64* dst;
+    i64 src_stride;  // words between rows
+    i64 dst_stride;
+    i32 rows;
+    i32 words;
+};
+void launch_copy_regions(const CopyDesc* descs, int n, i64 max_elems, hipStream_t s);
+
+// out[0] += population, out[1] += fingerprint (wrapping sums); out must be zeroed by the caller.
+void launch_reduce_board(const u64* buf, const Layout& L, i64 grow0, i64 gword0, i64 gwords, u64* out,
+                         hipStream_t s);
+
+// Yardstick: one byte per cell, one thread per cell, x-wrap + two ghost rows (reference class).
+void launch_naive_byte_step(const u8* src, u8* dst, i64 w, i64 h, const u8* above, const u8* below, int threads,
+                            hipStream_t s);
+
+}  // namespace hipk
+}  // namespace gol

@@ -1,0 +1,64 @@
+// gol-mi355x: work plans for the temporal-blocked stencil kernel.
+//
+// The reference launches one thread per byte-cell over the whole N x N tile every generation
+// (gol-with-cuda.cu:189-198, 264-277).  Here a generation sweep is planned once on the host and
+// replayed: the output region(s) of a superstep are cut into *segments*, each a block of output
+// rows x up to 62 output words, and the segments are packed side by side into 64-lane waves.
+//
+//   lane layout of a segment of `nwords` output words starting at word c0:
+//       [halo c0-1] [c0] [c0+1] ... [c0+nwords-1] [halo c0+nwords]      (nwords + 2 lanes)
+//
+// Every lane owns one 64-cell word column and streams down the rows; horizontal neighbours come
+// from the adjacent lanes through DPP (wave_shr/wave_shl).  The two halo lanes carry the
+// neighbouring words: after k <= 64 generations only their outer bits are invalid, so the interior
+// lanes stay exact.  Several narrow segments can share one wave (the 2-D edge columns, the
+// remainder of a row), so lane utilisation stays high for any width.
+#pragma once
+
+#include <vector>
+
+#include "gol/common.hpp"
+
+namespace gol {
+
+// Per-lane descriptor, read once at kernel start (16 bytes, naturally aligned).
+struct LaneDesc {
+    i32 row0;   // first output row of this lane's segment (tile coordinates)
+    i32 col;    // word column this lane streams (-1 .. nw)
+    u32 flags;  // LANE_* bits
+    i32 nrows;  // output rows of the segment; identical for all 64 lanes of a wave (0: idle wave)
+};
+
+enum : u32 {
+    LANE_STORE = 1u << 0,  // interior lane whose word is an output word
+};
+
+// Output region of a superstep: rows [r0, r1) x words [c0, c1) of the tile.
+struct Region {
+    i64 r0, r1, c0, c1;
+};
+
+static constexpr int kWaveLanes = 64;
+static constexpr int kSegWords = kWaveLanes - 2;  // output words of a full-width segment
+static constexpr int kWavesPerBlock = 4;          // 256-thread workgroups of independent waves
+
+struct PlanStats {
+    i64 waves = 0;        // including padding waves
+    i64 active_lanes = 0; // lanes that store an output word (summed over waves, per row)
+    i64 lane_rows = 0;    // total lane x input-row slots issued
+    i64 out_words = 0;    // output words produced
+};
+
+// Build the lane descriptors for `regions` (all within a tile with `nw` words per row).
+// `rows_per_chunk` is the segment height S (rows of output per wave); `k` the generations per pass
+// (only used to account for the 2k extra input rows per segment in the stats).  With `xwrap` the
+// tile is its own E/W neighbour (w % 64 == 0): halo lanes left of word 0 stream word nw-1 and halo
+// lanes right of word nw-1 stream word 0, so no ghost words are needed.
+std::vector<LaneDesc> build_plan(const std::vector<Region>& regions, i64 nw, i64 h, i64 rows_per_chunk, int k,
+                                 bool xwrap, PlanStats* stats = nullptr);
+
+// Pick a segment height so that the sweep has enough waves to fill the GPU (about `target_waves`)
+// while keeping the 2k-row vertical halo overhead small.
+i64 choose_rows_per_chunk(const std::vector<Region>& regions, int k, i64 target_waves, i64 min_rows);
+
+}  // namespace gol

@@ -1,0 +1,121 @@
+// gol-mi355x: segment planner for the temporal-blocked stencil kernel (see plan.hpp).
+#include "gol/plan.hpp"
+
+#include <algorithm>
+#include <map>
+
+namespace gol {
+
+namespace {
+
+struct Item {
+    i64 r0, nrows, c0, nwords;
+    int lanes() const { return (int)nwords + 2; }
+};
+
+}  // namespace
+
+i64 choose_rows_per_chunk(const std::vector<Region>& regions, int k, i64 target_waves, i64 min_rows) {
+    // lane-rows of output work, expressed in waves of full segments
+    double seg_rows = 0;
+    i64 max_rows = 1;
+    for (const Region& r : regions) {
+        i64 rows = r.r1 - r.r0, words = r.c1 - r.c0;
+        if (rows <= 0 || words <= 0) continue;
+        seg_rows += (double)rows * (double)words / kSegWords;
+        max_rows = std::max(max_rows, rows);
+    }
+    if (seg_rows <= 0) return 1;
+    i64 s = (i64)(seg_rows / (double)std::max<i64>(1, target_waves));
+    s = std::max<i64>(s, std::max<i64>(min_rows, 4 * (i64)k));
+    return std::max<i64>(1, std::min(s, max_rows));
+}
+
+std::vector<LaneDesc> build_plan(const std::vector<Region>& regions, i64 nw, i64 h, i64 rows_per_chunk, int k,
+                                 bool xwrap, PlanStats* stats) {
+    if (rows_per_chunk < 1) rows_per_chunk = 1;
+    std::vector<Item> items;
+    for (const Region& rg : regions) {
+        i64 rows = rg.r1 - rg.r0, words = rg.c1 - rg.c0;
+        if (rows <= 0 || words <= 0) continue;
+        if (rg.r0 < 0 || rg.r1 > h || rg.c0 < 0 || rg.c1 > nw) throw Error("plan region outside the tile");
+        i64 nch = ceil_div(rows, rows_per_chunk);
+        i64 base = rows / nch, extra = rows % nch;
+        i64 r = rg.r0;
+        for (i64 ch = 0; ch < nch; ++ch) {
+            i64 nr = base + (ch < extra ? 1 : 0);
+            for (i64 c = rg.c0; c < rg.c1; c += kSegWords) {
+                items.push_back({r, nr, c, std::min<i64>(kSegWords, rg.c1 - c)});
+            }
+            r += nr;
+        }
+    }
+
+    // Group by height; full-width segments get a wave each, narrow ones are packed first-fit.
+    std::map<i64, std::vector<Item>> by_rows;
+    for (const Item& it : items) by_rows[it.nrows].push_back(it);
+
+    std::vector<std::vector<Item>> waves;
+    for (auto& kv : by_rows) {
+        std::vector<Item>& v = kv.second;
+        std::vector<Item> narrow;
+        for (const Item& it : v) {
+            if (it.lanes() == kWaveLanes)
+                waves.push_back({it});
+            else
+                narrow.push_back(it);
+        }
+        std::stable_sort(narrow.begin(), narrow.end(),
+                         [](const Item& a, const Item& b) { return a.lanes() > b.lanes(); });
+        std::vector<std::pair<int, std::vector<Item>>> open;  // used lanes, items
+        for (const Item& it : narrow) {
+            bool placed = false;
+            for (auto& w : open) {
+                if (w.first + it.lanes() <= kWaveLanes) {
+                    w.first += it.lanes();
+                    w.second.push_back(it);
+                    placed = true;
+                    break;
+                }
+            }
+            if (!placed) open.push_back({it.lanes(), {it}});
+        }
+        for (auto& w : open) waves.push_back(std::move(w.second));
+    }
+
+    i64 nwaves = round_up(std::max<i64>(1, (i64)waves.size()), kWavesPerBlock);
+    std::vector<LaneDesc> lanes((size_t)(nwaves * kWaveLanes));
+    PlanStats st;
+    st.waves = nwaves;
+    for (size_t wi = 0; wi < (size_t)nwaves; ++wi) {
+        LaneDesc* L = &lanes[wi * kWaveLanes];
+        if (wi >= waves.size()) {
+            for (int l = 0; l < kWaveLanes; ++l) L[l] = {0, 0, 0u, 0};
+            continue;
+        }
+        const std::vector<Item>& w = waves[wi];
+        int l = 0;
+        i64 nrows = w[0].nrows;
+        for (const Item& it : w) {
+            for (int j = 0; j < it.lanes(); ++j, ++l) {
+                i64 col = it.c0 - 1 + j;
+                u32 f = 0;
+                if (j >= 1 && j <= it.nwords) {
+                    f |= LANE_STORE;
+                    st.active_lanes += 1;
+                    st.out_words += it.nrows;
+                }
+                if (xwrap && col == -1) col = nw - 1;
+                if (xwrap && col == nw) col = 0;
+                L[l] = {(i32)it.r0, (i32)col, f, (i32)nrows};
+            }
+        }
+        // idle lanes: stream a valid in-bounds column (the first item's first column), never store
+        for (; l < kWaveLanes; ++l) L[l] = {(i32)w[0].r0, (i32)w[0].c0, 0u, (i32)nrows};
+        st.lane_rows += (i64)kWaveLanes * (nrows + 2 * (i64)k);
+    }
+    if (stats) *stats = st;
+    return lanes;
+}
+
+}  // namespace gol

@@ -1,0 +1,548 @@
+// gol-mi355x: HIP backend of the engine.
+//
+// Board memory: two bit-packed tiles in HBM (hipMalloc, never managed memory — the reference
+// migrates managed pages host<->device every generation, gol-with-cuda.cu:35-51 + gol-main.c:97-100).
+// Streams: s_comp (kernels) and s_comm (halo exchange).  Per superstep with neighbours:
+//     s_comm:  wait(ev_ready) -> pack (2-D) -> RCCL group send/recv (or host staging) -> unpack -> ev_halo
+//     s_comp:  interior kernel -> wait(ev_halo) -> boundary kernel -> ev_ready
+// With graphs on, G/(m*k) captures of m supersteps (m even => parity preserved) are replayed.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstring>
+#include <map>
+
+#include "gol/engine.hpp"
+#include "gol/hip_kernels.hpp"
+
+#define HIP_CHECK(x)                                                                                    \
+    do {                                                                                                \
+        hipError_t e_ = (x);                                                                            \
+        if (e_ != hipSuccess)                                                                           \
+            throw ::gol::Error(::gol::strprintf("%s failed: %s (%s:%d)", #x, hipGetErrorString(e_), __FILE__, \
+                                                __LINE__));                                             \
+    } while (0)
+
+namespace gol {
+
+int hip_device_count(int* err) {
+    int n = 0;
+    hipError_t e = hipGetDeviceCount(&n);
+    if (err) *err = (int)e;
+    return e == hipSuccess ? n : 0;
+}
+
+void hip_set_device(int dev) { HIP_CHECK(hipSetDevice(dev)); }
+
+namespace {
+
+struct DevPlan {
+    LaneDesc* d = nullptr;
+    i64 waves = 0;
+    PlanStats st;
+};
+
+struct DevCopies {
+    hipk::CopyDesc* pack = nullptr;
+    hipk::CopyDesc* unpack = nullptr;
+    int npack = 0, nunpack = 0;
+    i64 max_pack = 0, max_unpack = 0;
+};
+
+class HipEngine : public Engine {
+   public:
+    HipEngine(const Geometry& g, const EngineConfig& c, std::shared_ptr<Transport> t) : Engine(g, c, std::move(t)) {
+        if (cfg_.device >= 0) HIP_CHECK(hipSetDevice(cfg_.device));
+        HIP_CHECK(hipGetDevice(&dev_));
+        hipDeviceProp_t prop;
+        HIP_CHECK(hipGetDeviceProperties(&prop, dev_));
+        cus_ = prop.multiProcessorCount;
+        int R = L_.R;
+        if (cfg_.kernel == "lds") {
+            R = 1;
+        } else if (cfg_.kernel != "temporal") {
+            throw Error("GOL_KERNEL must be temporal or lds");
+        }
+        R = std::min(R, hipk::max_step_depth());
+        while (!hipk::step_depth_supported(R)) --R;
+        if (R != L_.R) L_ = Layout(L_.h, L_.w, R);
+        stats_.depth = R;
+        // slack rows: the temporal kernel prefetches 3 rows past a segment's last input row
+        const size_t bytes = (size_t)(L_.words() + 4 * L_.pitch) * 8;
+        for (int i = 0; i < 2; ++i) {
+            HIP_CHECK(hipMalloc(&buf_[i], bytes));
+            HIP_CHECK(hipMemset(buf_[i], 0, bytes));
+        }
+        alloc_bytes_ = bytes;
+        HIP_CHECK(hipStreamCreateWithFlags(&s_comp_, hipStreamNonBlocking));
+        HIP_CHECK(hipStreamCreateWithFlags(&s_comm_, hipStreamNonBlocking));
+        HIP_CHECK(hipEventCreateWithFlags(&ev_ready_, hipEventDisableTiming));
+        HIP_CHECK(hipEventCreateWithFlags(&ev_halo_, hipEventDisableTiming));
+        if (cfg_.profile) {
+            for (auto* e : {&ev_t0_, &ev_t1_, &ev_t2_, &ev_t3_}) HIP_CHECK(hipEventCreate(e));
+        }
+        HIP_CHECK(hipMalloc(&d_red_, 2 * sizeof(u64)));
+        HIP_CHECK(hipHostMalloc(&h_red_, 2 * sizeof(u64), hipHostMallocDefault));
+        device_transport_ = t_->device_buffers() && cfg_.transport != "host";
+        if (cfg_.transport == "device" && !t_->device_buffers())
+            throw Error("GOL_TRANSPORT=device needs a device transport (RCCL)");
+    }
+
+    ~HipEngine() override {
+        hipStreamSynchronize(s_comp_);
+        hipStreamSynchronize(s_comm_);
+        for (auto& kv : graphs_) hipGraphExecDestroy(kv.second);
+        for (auto& kv : plans_) hipFree(kv.second.d);
+        for (auto& kv : copies_) {
+            hipFree(kv.second.pack);
+            hipFree(kv.second.unpack);
+        }
+        for (auto& v : {&dstage_s_, &dstage_r_})
+            for (u64* p : *v) hipFree(p);
+        for (auto& v : {&hstage_s_, &hstage_r_})
+            for (u64* p : *v) hipHostFree(p);
+        for (int i = 0; i < 2; ++i) hipFree(buf_[i]);
+        hipFree(d_red_);
+        hipHostFree(h_red_);
+        hipEventDestroy(ev_ready_);
+        hipEventDestroy(ev_halo_);
+        if (cfg_.profile)
+            for (auto e : {ev_t0_, ev_t1_, ev_t2_, ev_t3_}) hipEventDestroy(e);
+        hipStreamDestroy(s_comp_);
+        hipStreamDestroy(s_comm_);
+    }
+
+    std::string backend_name() const override { return "hip"; }
+
+    void synchronize() override {
+        HIP_CHECK(hipStreamSynchronize(s_comm_));
+        HIP_CHECK(hipStreamSynchronize(s_comp_));
+    }
+
+    std::vector<u64> tile_words() override {
+        synchronize();
+        std::vector<u64> d((size_t)(L_.h * L_.nw));
+        HIP_CHECK(hipMemcpy2D(d.data(), (size_t)L_.nw * 8, buf_[cur_] + L_.index(0, 0), (size_t)L_.pitch * 8,
+                              (size_t)L_.nw * 8, (size_t)L_.h, hipMemcpyDeviceToHost));
+        if (L_.w % 64)
+            for (i64 r = 0; r < L_.h; ++r) d[(size_t)(r * L_.nw + L_.nw - 1)] &= L_.mask(L_.nw - 1);
+        return d;
+    }
+
+    void set_tile_words(const std::vector<u64>& dense) override {
+        if ((i64)dense.size() != L_.h * L_.nw) throw Error("set_tile_words: wrong size");
+        synchronize();
+        std::vector<u64> m = dense;
+        for (i64 r = 0; r < L_.h; ++r)
+            for (i64 c = 0; c < L_.nw; ++c) m[(size_t)(r * L_.nw + c)] &= L_.mask(c);
+        HIP_CHECK(hipMemcpy2D(buf_[cur_] + L_.index(0, 0), (size_t)L_.pitch * 8, m.data(), (size_t)L_.nw * 8,
+                              (size_t)L_.nw * 8, (size_t)L_.h, hipMemcpyHostToDevice));
+        post(buf_[cur_], s_comp_);
+        HIP_CHECK(hipEventRecord(ev_ready_, s_comp_));
+        synchronize();
+    }
+
+    std::pair<u64, u64> local_reduce() override {
+        HIP_CHECK(hipMemsetAsync(d_red_, 0, 2 * sizeof(u64), s_comp_));
+        hipk::launch_reduce_board(buf_[cur_], L_, g_.row0, g_.word0(), g_.global_words(), d_red_, s_comp_);
+        HIP_CHECK(hipGetLastError());
+        HIP_CHECK(hipMemcpyAsync(h_red_, d_red_, 2 * sizeof(u64), hipMemcpyDeviceToHost, s_comp_));
+        HIP_CHECK(hipStreamSynchronize(s_comp_));
+        return {h_red_[0], h_red_[1]};
+    }
+
+    void run_graphed(u64& generations) {
+        const int k = cfg_.compat ? 1 : L_.R;
+        int m = cfg_.graph_supersteps;
+        if (m <= 0) m = k >= 8 ? 16 : 32;
+        m += m & 1;  // even: the graph returns to the same buffer parity
+        const u64 per = (u64)m * (u64)k;
+        bool local = cfg_.compat || halo_items(k).empty();
+        if (!local && !device_transport_) return;  // host-staged exchange cannot be captured
+        while (generations >= per && graph_ok_) {
+            hipGraphExec_t exec = graph_for(k, m);
+            if (!exec) break;
+            maybe_inject_fault();
+            HIP_CHECK(hipGraphLaunch(exec, s_comp_));
+            gen_ += per;
+            generations -= per;
+            stats_.generations += per;
+            stats_.supersteps += (u64)m;
+            stats_.graph_launches += 1;
+        }
+    }
+
+    void run(u64 generations) override {
+        if (cfg_.graph && !cfg_.profile) run_graphed(generations);
+        Engine::run(generations);
+    }
+
+    const DevPlan& full_plan_stats() { return plan(0, L_.R); }
+
+   protected:
+    void do_init(const PatternSpec& p) override {
+        synchronize();
+        for (int i = 0; i < 2; ++i) HIP_CHECK(hipMemsetAsync(buf_[i], 0, alloc_bytes_, s_comp_));
+        hipk::InitParams ip{g_.row0, g_.word0(), g_.global_words(), p.seed,
+                            p.fill == Fill::Ones ? 1 : (p.fill == Fill::Random ? 2 : 0)};
+        cur_ = 0;
+        if (p.fill != Fill::Zero) hipk::launch_init_fill(buf_[cur_], L_, ip, s_comp_);
+        std::vector<i64> cells;
+        for (const auto& rc : p.cells) {
+            i64 r = rc.first - g_.row0, c = rc.second - g_.col0;
+            if (r < 0 || r >= L_.h || c < 0 || c >= L_.w) continue;
+            cells.push_back(r);
+            cells.push_back(c);
+        }
+        i64* dcells = nullptr;
+        if (!cells.empty()) {
+            HIP_CHECK(hipMalloc(&dcells, cells.size() * sizeof(i64)));
+            HIP_CHECK(hipMemcpyAsync(dcells, cells.data(), cells.size() * sizeof(i64), hipMemcpyHostToDevice, s_comp_));
+            hipk::launch_set_cells(buf_[cur_], L_, dcells, (i64)cells.size() / 2, s_comp_);
+        }
+        post(buf_[cur_], s_comp_);
+        HIP_CHECK(hipGetLastError());
+        HIP_CHECK(hipEventRecord(ev_ready_, s_comp_));
+        synchronize();
+        if (dcells) HIP_CHECK(hipFree(dcells));
+        // Build the plans for the common depths now, so graph capture never allocates.
+        prepare(cfg_.compat ? 1 : L_.R);
+        const DevPlan& fp = plan(0, cfg_.compat ? 1 : L_.R);
+        stats_.plan_waves = fp.waves;
+        stats_.lane_efficiency =
+            fp.st.lane_rows ? (double)fp.st.out_words / (double)fp.st.lane_rows : 0.0;
+    }
+
+    void do_superstep(int k) override {
+        prepare(k);
+        u64* src = buf_[cur_];
+        u64* dst = buf_[cur_ ^ 1];
+        const std::vector<HaloItem>& items = items_for(k);
+        const bool prof = cfg_.profile;
+        if (cfg_.compat || items.empty()) {
+            if (prof) HIP_CHECK(hipEventRecord(ev_t2_, s_comp_));
+            launch(0, k, src, dst, s_comp_);
+            post(dst, s_comp_);
+            if (prof) {
+                HIP_CHECK(hipEventRecord(ev_t3_, s_comp_));
+                HIP_CHECK(hipEventSynchronize(ev_t3_));
+                float ms = 0;
+                HIP_CHECK(hipEventElapsedTime(&ms, ev_t2_, ev_t3_));
+                stats_.t_compute_ms += ms;
+            }
+        } else if (cfg_.overlap && can_overlap()) {
+            if (device_transport_) {
+                HIP_CHECK(hipStreamWaitEvent(s_comm_, ev_ready_, 0));
+                if (prof) HIP_CHECK(hipEventRecord(ev_t0_, s_comm_));
+                exchange_device(k, items, cur_, s_comm_);
+                if (prof) HIP_CHECK(hipEventRecord(ev_t1_, s_comm_));
+                HIP_CHECK(hipEventRecord(ev_halo_, s_comm_));
+                if (prof) HIP_CHECK(hipEventRecord(ev_t2_, s_comp_));
+                launch(1, k, src, dst, s_comp_);
+            } else {
+                if (prof) HIP_CHECK(hipEventRecord(ev_t2_, s_comp_));
+                launch(1, k, src, dst, s_comp_);  // interior first: runs while the host exchanges
+                HIP_CHECK(hipStreamWaitEvent(s_comm_, ev_ready_, 0));
+                if (prof) HIP_CHECK(hipEventRecord(ev_t0_, s_comm_));
+                exchange_staged(k, items, cur_, s_comm_);
+                if (prof) HIP_CHECK(hipEventRecord(ev_t1_, s_comm_));
+                HIP_CHECK(hipEventRecord(ev_halo_, s_comm_));
+            }
+            HIP_CHECK(hipStreamWaitEvent(s_comp_, ev_halo_, 0));
+            launch(2, k, src, dst, s_comp_);
+            post(dst, s_comp_);
+            if (prof) record_profile(true);
+        } else {
+            if (prof) HIP_CHECK(hipEventRecord(ev_t0_, s_comp_));
+            if (device_transport_)
+                exchange_device(k, items, cur_, s_comp_);
+            else
+                exchange_staged(k, items, cur_, s_comp_);
+            if (prof) {
+                HIP_CHECK(hipEventRecord(ev_t1_, s_comp_));
+                HIP_CHECK(hipEventRecord(ev_t2_, s_comp_));
+            }
+            launch(0, k, src, dst, s_comp_);
+            post(dst, s_comp_);
+            if (prof) record_profile(true);
+        }
+        HIP_CHECK(hipEventRecord(ev_ready_, s_comp_));
+        cur_ ^= 1;
+    }
+
+    void do_set_compat_halos(const std::vector<u64>& above, const std::vector<u64>& below) override {
+        synchronize();
+        for (int i = 0; i < 2; ++i) {
+            HIP_CHECK(hipMemcpy(buf_[i] + L_.index(-1, -1), above.data(), (size_t)L_.pitch * 8, hipMemcpyHostToDevice));
+            HIP_CHECK(hipMemcpy(buf_[i] + L_.index(L_.h, -1), below.data(), (size_t)L_.pitch * 8,
+                                hipMemcpyHostToDevice));
+            if (self_x() && !L_.aligned()) {
+                hipk::launch_fill_ghost_cols(buf_[i], L_, -1, 0, s_comp_);
+                hipk::launch_fill_ghost_cols(buf_[i], L_, L_.h, L_.h + 1, s_comp_);
+            }
+        }
+        HIP_CHECK(hipEventRecord(ev_ready_, s_comp_));
+        synchronize();
+    }
+
+    std::vector<u64> read_row(i64 r) override {
+        synchronize();
+        std::vector<u64> row((size_t)L_.pitch);
+        HIP_CHECK(hipMemcpy(row.data(), buf_[cur_] + L_.index(r, -1), (size_t)L_.pitch * 8, hipMemcpyDeviceToHost));
+        return row;
+    }
+
+   private:
+    // ----- plans -----
+    u32 step_flags() const {
+        u32 f = 0;
+        if (self_y() && !cfg_.compat) f |= hipk::STEP_WRAP_Y;
+        if (xwrap_by_plan()) f |= hipk::STEP_WRAP_X;
+        return f;
+    }
+
+    bool can_overlap() const {
+        // interior must exist, and the LDS kernel reads ghost words for every row (2-D needs them)
+        if (L_.h <= 2 * (i64)L_.R) return false;
+        if (cfg_.kernel == "lds" && g_.dec.Px > 1) return false;
+        return true;
+    }
+
+    std::vector<Region> regions(int kind, int k) const {
+        const i64 h = L_.h, nw = L_.nw;
+        const bool two_d = g_.dec.Px > 1;
+        if (kind == 0 || h <= 2 * (i64)k) return kind == 1 ? std::vector<Region>{} : std::vector<Region>{{0, h, 0, nw}};
+        if (kind == 1) {
+            if (two_d) return nw > 2 ? std::vector<Region>{{k, h - k, 1, nw - 1}} : std::vector<Region>{};
+            return {{k, h - k, 0, nw}};
+        }
+        std::vector<Region> r = {{0, k, 0, nw}, {h - k, h, 0, nw}};
+        if (two_d) {
+            if (nw > 2) {
+                r.push_back({k, h - k, 0, 1});
+                r.push_back({k, h - k, nw - 1, nw});
+            } else {
+                r.push_back({k, h - k, 0, nw});
+            }
+        }
+        return r;
+    }
+
+    const DevPlan& plan(int kind, int k) {
+        const int key = kind * 1000 + k;
+        auto it = plans_.find(key);
+        if (it != plans_.end()) return it->second;
+        std::vector<Region> rg = regions(kind, k);
+        DevPlan p;
+        i64 target = cfg_.waves_target > 0 ? cfg_.waves_target : (i64)cus_ * 8;
+        i64 rows = cfg_.rows_per_wave > 0 ? cfg_.rows_per_wave : choose_rows_per_chunk(rg, k, target, 4 * (i64)k);
+        std::vector<LaneDesc> lanes = build_plan(rg, L_.nw, L_.h, rows, k, xwrap_by_plan(), &p.st);
+        p.waves = (i64)lanes.size() / kWaveLanes;
+        HIP_CHECK(hipMalloc(&p.d, lanes.size() * sizeof(LaneDesc)));
+        HIP_CHECK(hipMemcpy(p.d, lanes.data(), lanes.size() * sizeof(LaneDesc), hipMemcpyHostToDevice));
+        return plans_.emplace(key, p).first->second;
+    }
+
+    void launch(int kind, int k, const u64* src, u64* dst, hipStream_t s) {
+        if (cfg_.kernel == "lds") {
+            // full-row bands only (the LDS variant is never split by columns: can_overlap)
+            for (const Region& r : regions(kind, 1))
+                if (r.c0 == 0) hipk::launch_step_lds(src, dst, L_, r.r0, r.r1, step_flags(), s);
+        } else {
+            const DevPlan& p = plan(kind, k);
+            if (p.st.out_words == 0) return;
+            hipk::StepParams sp{L_.pitch, (i32)L_.h, (i32)L_.nw, L_.R, step_flags()};
+            hipk::launch_step(k, src, dst, p.d, p.waves, sp, s);
+        }
+        HIP_CHECK(hipGetLastError());
+    }
+
+    // Ghost words for widths that are not a multiple of 64 when the tile is its own E/W neighbour.
+    void post(u64* buf, hipStream_t s) {
+        if (self_x() && !L_.aligned()) hipk::launch_fill_ghost_cols(buf, L_, 0, L_.h, s);
+    }
+
+    // ----- halo exchange -----
+    const std::vector<HaloItem>& items_for(int k) {
+        auto it = items_.find(k);
+        if (it != items_.end()) return it->second;
+        return items_.emplace(k, halo_items(k)).first->second;
+    }
+
+    void prepare(int k) {
+        plan(0, k);
+        if (can_overlap()) {
+            plan(1, k);
+            plan(2, k);
+        }
+        const std::vector<HaloItem>& items = items_for(k);
+        if (items.empty()) return;
+        // staging buffers sized for the deepest halo (k = R)
+        const std::vector<HaloItem>& deep = items_for(L_.R);
+        if (dstage_s_.empty()) {
+            for (const HaloItem& itm : deep) {
+                u64 *ds, *dr, *hs = nullptr, *hr = nullptr;
+                HIP_CHECK(hipMalloc(&ds, (size_t)itm.send.count() * 8));
+                HIP_CHECK(hipMalloc(&dr, (size_t)itm.recv.count() * 8));
+                if (!device_transport_) {
+                    HIP_CHECK(hipHostMalloc(&hs, (size_t)itm.send.count() * 8, hipHostMallocDefault));
+                    HIP_CHECK(hipHostMalloc(&hr, (size_t)itm.recv.count() * 8, hipHostMallocDefault));
+                }
+                dstage_s_.push_back(ds);
+                dstage_r_.push_back(dr);
+                hstage_s_.push_back(hs);
+                hstage_r_.push_back(hr);
+            }
+        }
+        for (int parity = 0; parity < 2; ++parity) copies(k, parity);
+    }
+
+    const DevCopies& copies(int k, int parity) {
+        const int key = k * 2 + parity;
+        auto it = copies_.find(key);
+        if (it != copies_.end()) return it->second;
+        const std::vector<HaloItem>& items = items_for(k);
+        std::vector<hipk::CopyDesc> pk, up;
+        DevCopies dc;
+        u64* b = buf_[parity];
+        for (size_t i = 0; i < items.size(); ++i) {
+            const HaloItem& itm = items[i];
+            if (itm.contiguous) continue;
+            pk.push_back({b + L_.index(itm.send.r0, itm.send.c0), dstage_s_[i], L_.pitch, itm.send.words,
+                          (i32)itm.send.rows, (i32)itm.send.words});
+            up.push_back({dstage_r_[i], b + L_.index(itm.recv.r0, itm.recv.c0), itm.recv.words, L_.pitch,
+                          (i32)itm.recv.rows, (i32)itm.recv.words});
+            dc.max_pack = std::max(dc.max_pack, itm.send.count());
+            dc.max_unpack = std::max(dc.max_unpack, itm.recv.count());
+        }
+        dc.npack = (int)pk.size();
+        dc.nunpack = (int)up.size();
+        if (!pk.empty()) {
+            HIP_CHECK(hipMalloc(&dc.pack, pk.size() * sizeof(hipk::CopyDesc)));
+            HIP_CHECK(hipMemcpy(dc.pack, pk.data(), pk.size() * sizeof(hipk::CopyDesc), hipMemcpyHostToDevice));
+            HIP_CHECK(hipMalloc(&dc.unpack, up.size() * sizeof(hipk::CopyDesc)));
+            HIP_CHECK(hipMemcpy(dc.unpack, up.data(), up.size() * sizeof(hipk::CopyDesc), hipMemcpyHostToDevice));
+        }
+        return copies_.emplace(key, dc).first->second;
+    }
+
+    void build_messages(int k, const std::vector<HaloItem>& items, int parity, std::vector<Message>& sends,
+                        std::vector<Message>& recvs) {
+        (void)k;
+        u64* b = buf_[parity];
+        for (size_t i = 0; i < items.size(); ++i) {
+            const HaloItem& itm = items[i];
+            u64* sp = itm.contiguous ? b + L_.index(itm.send.r0, itm.send.c0) : dstage_s_[i];
+            u64* rp = itm.contiguous ? b + L_.index(itm.recv.r0, itm.recv.c0) : dstage_r_[i];
+            sends.push_back({itm.send_peer, sp, (size_t)itm.send.count() * 8});
+            recvs.push_back({itm.recv_peer, rp, (size_t)itm.recv.count() * 8});
+        }
+    }
+
+    void exchange_device(int k, const std::vector<HaloItem>& items, int parity, hipStream_t s) {
+        const DevCopies& dc = copies(k, parity);
+        if (dc.npack) hipk::launch_copy_regions(dc.pack, dc.npack, dc.max_pack, s);
+        std::vector<Message> sends, recvs;
+        build_messages(k, items, parity, sends, recvs);
+        t_->exchange(sends, recvs, (void*)s);
+        if (dc.nunpack) hipk::launch_copy_regions(dc.unpack, dc.nunpack, dc.max_unpack, s);
+        HIP_CHECK(hipGetLastError());
+        account(items);
+    }
+
+    void exchange_staged(int k, const std::vector<HaloItem>& items, int parity, hipStream_t s) {
+        const DevCopies& dc = copies(k, parity);
+        if (dc.npack) hipk::launch_copy_regions(dc.pack, dc.npack, dc.max_pack, s);
+        std::vector<Message> dsends, drecvs;
+        build_messages(k, items, parity, dsends, drecvs);
+        std::vector<Message> hsends, hrecvs;
+        for (size_t i = 0; i < items.size(); ++i) {
+            HIP_CHECK(hipMemcpyAsync(hstage_s_[i], dsends[i].buf, dsends[i].bytes, hipMemcpyDeviceToHost, s));
+            hsends.push_back({dsends[i].peer, hstage_s_[i], dsends[i].bytes});
+            hrecvs.push_back({drecvs[i].peer, hstage_r_[i], drecvs[i].bytes});
+        }
+        HIP_CHECK(hipStreamSynchronize(s));
+        t_->exchange_host(hsends, hrecvs);
+        for (size_t i = 0; i < items.size(); ++i)
+            HIP_CHECK(hipMemcpyAsync(drecvs[i].buf, hstage_r_[i], drecvs[i].bytes, hipMemcpyHostToDevice, s));
+        if (dc.nunpack) hipk::launch_copy_regions(dc.unpack, dc.nunpack, dc.max_unpack, s);
+        HIP_CHECK(hipGetLastError());
+        account(items);
+    }
+
+    void account(const std::vector<HaloItem>& items) {
+        stats_.exchanges += 1;
+        for (const HaloItem& it : items) stats_.halo_bytes += (u64)it.send.count() * 8;
+    }
+
+    void record_profile(bool with_exchange) {
+        HIP_CHECK(hipEventRecord(ev_t3_, s_comp_));
+        HIP_CHECK(hipEventSynchronize(ev_t3_));
+        float ms = 0;
+        if (with_exchange) {
+            HIP_CHECK(hipEventElapsedTime(&ms, ev_t0_, ev_t1_));
+            stats_.t_exchange_ms += ms;
+        }
+        HIP_CHECK(hipEventElapsedTime(&ms, ev_t2_, ev_t3_));
+        stats_.t_compute_ms += ms;
+    }
+
+    // ----- graphs -----
+    hipGraphExec_t graph_for(int k, int m) {
+        const int key = k * 1000 + m;
+        auto it = graphs_.find(key);
+        if (it != graphs_.end()) return it->second;
+        prepare(k);
+        hipGraph_t graph = nullptr;
+        hipGraphExec_t exec = nullptr;
+        const int cur0 = cur_;
+        try {
+            HIP_CHECK(hipStreamBeginCapture(s_comp_, hipStreamCaptureModeRelaxed));
+            HIP_CHECK(hipEventRecord(ev_ready_, s_comp_));  // fork point for the comm stream
+            for (int i = 0; i < m; ++i) do_superstep(k);
+            HIP_CHECK(hipStreamEndCapture(s_comp_, &graph));
+            HIP_CHECK(hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0));
+            HIP_CHECK(hipGraphDestroy(graph));
+        } catch (const Error& e) {
+            hipGraph_t g2 = nullptr;
+            hipStreamEndCapture(s_comp_, &g2);
+            if (g2) hipGraphDestroy(g2);
+            hipGetLastError();
+            cur_ = cur0;
+            graph_ok_ = false;
+            fprintf(stderr, "[gol] hipGraph capture disabled: %s\n", e.what());
+            HIP_CHECK(hipEventRecord(ev_ready_, s_comp_));
+            return nullptr;
+        }
+        if (cur_ != cur0) throw Error("graph capture changed the buffer parity");
+        graphs_[key] = exec;
+        return exec;
+    }
+
+    int dev_ = 0, cus_ = 256;
+    u64* buf_[2] = {nullptr, nullptr};
+    size_t alloc_bytes_ = 0;
+    int cur_ = 0;
+    hipStream_t s_comp_ = nullptr, s_comm_ = nullptr;
+    hipEvent_t ev_ready_ = nullptr, ev_halo_ = nullptr;
+    hipEvent_t ev_t0_ = nullptr, ev_t1_ = nullptr, ev_t2_ = nullptr, ev_t3_ = nullptr;
+    u64* d_red_ = nullptr;
+    u64* h_red_ = nullptr;
+    bool device_transport_ = false;
+    bool graph_ok_ = true;
+    std::map<int, DevPlan> plans_;
+    std::map<int, DevCopies> copies_;
+    std::map<int, std::vector<HaloItem>> items_;
+    std::map<int, hipGraphExec_t> graphs_;
+    std::vector<u64*> dstage_s_, dstage_r_, hstage_s_, hstage_r_;
+};
+
+}  // namespace
+
+std::unique_ptr<Engine> make_hip_engine(const Geometry& g, const EngineConfig& c, std::shared_ptr<Transport> t) {
+    int err = 0;
+    if (hip_device_count(&err) <= 0) throw Error("no HIP device available");
+    return std::make_unique<HipEngine>(g, c, std::move(t));
+}
+
+}  // namespace gol

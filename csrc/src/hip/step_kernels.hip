@@ -1,0 +1,260 @@
+// gol-mi355x: the B3/S23 stencil kernels for gfx950 (CDNA4).
+//
+// step_temporal<K> — the hot kernel.  Design (MI355X-first, not a port of gol_kernel,
+// reference gol-with-cuda.cu:189-262, which reads 9 bytes per cell per generation from global memory):
+//
+//  * 1 bit per cell, 64 cells per lane: each lane owns one u64 word column of the tile (two VGPRs,
+//    lo = cells 0..31, hi = cells 32..63) and streams DOWN the rows.  A wave64 covers 64 adjacent
+//    words = 4096 cells per row; the work plan (plan.hpp) packs segments of <= 62 output words plus
+//    one halo lane on each side into the 64 lanes.
+//  * Horizontal neighbours: the previous lane's hi word (v_mov_b32_dpp wave_shr:1) and the next
+//    lane's lo word (wave_shl:1), funnel-shifted in with v_alignbit_b32 — no LDS, no barriers.
+//  * Bit-sliced counting: per row the horizontal 3-sum (xor3 / maj = 1 v_bitop3 each), then the
+//    vertical 3-sum of those 2-bit sums and the rule in 8 more v_bitop3 (bits.hpp): 13 VALU ops per
+//    32 cells per generation.
+//  * Temporal blocking: K generation levels are chained in registers.  Level l keeps a 3-row
+//    window (horizontal sums of rows r-2, r-1 and its centre row); when a row arrives at level l it
+//    emits row r-1 of generation l+1 to level l+1.  One HBM pass = K generations, so the kernel is
+//    VALU bound instead of HBM bound (0.25 B/cell/pass / K).  The window rotates by unrolling the
+//    row loop x3, so there are no register moves.
+//  * Halo semantics: a segment reads K rows above/below its output rows and the two halo words;
+//    invalid bits spread one column per generation from the halo lanes' outer edges, so the output
+//    lanes are exact for K <= 64.
+//  * Periodic wrap without ghost traffic: when the tile is its own E/W neighbour the plan points the
+//    edge segments' halo lanes at word nw-1 / word 0 (x-wrap), and when it is its own N/S neighbour
+//    the load stream addresses rows modulo h (STEP_WRAP_Y).  A single-GPU run therefore needs no
+//    ghost rows, ghost words, halo kernels or copies at all.
+//
+// step_lds — single-generation LDS-tiled variant: a 256-thread workgroup stages a (16+2) x (64+2)
+// word tile + ghost ring in LDS and computes 16 x 64 output words.  Kept as a measured alternative.
+#include "gol/bits.hpp"
+#include "gol/hip_kernels.hpp"
+
+namespace gol {
+namespace hipk {
+
+namespace {
+
+template <unsigned LUT>
+__device__ __forceinline__ u32 b3(u32 a, u32 b, u32 c) {
+    return __builtin_amdgcn_bitop3_b32(a, b, c, LUT);
+}
+
+// lane i <- lane i-1 (lane 0 gets 0: bound_ctrl)
+__device__ __forceinline__ u32 dpp_prev(u32 v) {
+    return (u32)__builtin_amdgcn_mov_dpp((int)v, 0x138 /*wave_shr:1*/, 0xF, 0xF, true);
+}
+// lane i <- lane i+1 (lane 63 gets 0: bound_ctrl)
+__device__ __forceinline__ u32 dpp_next(u32 v) {
+    return (u32)__builtin_amdgcn_mov_dpp((int)v, 0x130 /*wave_shl:1*/, 0xF, 0xF, true);
+}
+
+__device__ __forceinline__ u32 rule32(u32 a0, u32 a1, u32 b0, u32 b1, u32 c0, u32 c1, u32 x) {
+    const u32 x0 = b3<kLutXor3>(a0, b0, c0);
+    const u32 cy = b3<kLutMaj>(a0, b0, c0);
+    const u32 u0 = b3<kLutXor3>(a1, b1, c1);
+    const u32 u1 = b3<kLutMaj>(a1, b1, c1);
+    const u32 y1 = b3<kLutY1>(u1, u0, cy);
+    const u32 y2 = b3<kLutY2>(u1, u0, cy);
+    const u32 t = b3<kLutBorn4>(x0, x, y2);
+    return b3<kLutOut>(x0, y1, t);
+}
+
+template <int K>
+struct Pipe {
+    u32 s0[K][3][2];  // horizontal sum bit 0, per level, ring slot, half
+    u32 s1[K][3][2];  // horizontal sum bit 1
+    u32 x[K][3][2];   // the level's input rows (centre cells)
+};
+
+// Push one row (lo, hi) through the K levels.  Input index i (0-based within the segment's input
+// rows).  PH == i % 3 selects the ring slots at compile time.  Returns false while the pipeline is
+// still filling (GUARD instantiation only); otherwise (lo, hi) is the output row i - 2K.
+template <int K, int PH, bool GUARD>
+__device__ __forceinline__ bool advance(Pipe<K>& P, u32& lo, u32& hi, int i) {
+#pragma unroll
+    for (int l = 0; l < K; ++l) {
+        if (GUARD && i < 2 * l) return false;
+        const int s = (PH + l) % 3;     // slot of the arriving row
+        const int sp = (s + 2) % 3;     // previous row (centre of the output)
+        const int spp = (s + 1) % 3;    // two rows back
+        const u32 ph = dpp_prev(hi), nl = dpp_next(lo);
+        const u32 L0 = __builtin_amdgcn_alignbit(lo, ph, 31);
+        const u32 L1 = __builtin_amdgcn_alignbit(hi, lo, 31);
+        const u32 R0 = __builtin_amdgcn_alignbit(hi, lo, 1);
+        const u32 R1 = __builtin_amdgcn_alignbit(nl, hi, 1);
+        P.s0[l][s][0] = b3<kLutXor3>(L0, lo, R0);
+        P.s1[l][s][0] = b3<kLutMaj>(L0, lo, R0);
+        P.s0[l][s][1] = b3<kLutXor3>(L1, hi, R1);
+        P.s1[l][s][1] = b3<kLutMaj>(L1, hi, R1);
+        P.x[l][s][0] = lo;
+        P.x[l][s][1] = hi;
+        if (GUARD && i < 2 * l + 2) return false;
+        lo = rule32(P.s0[l][spp][0], P.s1[l][spp][0], P.s0[l][sp][0], P.s1[l][sp][0], P.s0[l][s][0],
+                    P.s1[l][s][0], P.x[l][sp][0]);
+        hi = rule32(P.s0[l][spp][1], P.s1[l][spp][1], P.s0[l][sp][1], P.s1[l][sp][1], P.s0[l][s][1],
+                    P.s1[l][s][1], P.x[l][sp][1]);
+    }
+    return true;
+}
+
+template <int K, bool WRAPY>
+struct WaveRunner {
+    const StepParams& p;
+    const LaneDesc& d;
+    const int n;  // input rows of the segment: nrows + 2K
+    const i64 hp;  // h * pitch
+    const uint2* ld;
+    uint2* st;
+    int lrow;     // tile row of the next load (WRAPY only)
+    uint2 pf[3];
+    Pipe<K> P;
+
+    __device__ __forceinline__ void next_row() {
+        ld += p.pitch;
+        if (WRAPY) {  // rows are periodic: row h is row 0 (branch-free select)
+            ++lrow;
+            const bool w = lrow == p.h;
+            lrow = w ? 0 : lrow;
+            ld = w ? ld - hp : ld;
+        }
+    }
+
+    __device__ __forceinline__ WaveRunner(const u64* src, u64* dst, const LaneDesc& d_, int nrows, const StepParams& p_)
+        : p(p_), d(d_), n(nrows + 2 * K), hp((i64)p_.h * p_.pitch) {
+        lrow = d.row0 - K;
+        if (WRAPY && lrow < 0) lrow += p.h;
+        ld = reinterpret_cast<const uint2*>(src + (i64)(lrow + p.R) * p.pitch + (d.col + 1));
+        st = reinterpret_cast<uint2*>(dst + (i64)(d.row0 + p.R) * p.pitch + (d.col + 1));
+        pf[0] = *ld;
+        next_row();
+        pf[1] = *ld;
+        next_row();
+        pf[2] = *ld;
+        next_row();
+    }
+
+    template <int PH, bool GUARD>
+    __device__ __forceinline__ void body(int i) {
+        if (GUARD && i >= n) return;
+        const uint2 x = pf[PH];
+        pf[PH] = *ld;  // prefetch 3 rows ahead (the allocation has slack rows past the halo)
+        next_row();
+        u32 lo = x.x, hi = x.y;
+        if (!advance<K, PH, GUARD>(P, lo, hi, i)) return;
+        if (d.flags & LANE_STORE) *st = make_uint2(lo, hi);
+        st += p.pitch;
+    }
+
+    __device__ __forceinline__ void run() {
+        constexpr int i0 = ((2 * K + 2) / 3) * 3;  // first multiple of 3 >= 2K: pipeline full
+        int i = 0;
+        for (; i < i0; i += 3) {
+            body<0, true>(i);
+            body<1, true>(i + 1);
+            body<2, true>(i + 2);
+        }
+        for (; i + 3 <= n; i += 3) {
+            body<0, false>(i);
+            body<1, false>(i + 1);
+            body<2, false>(i + 2);
+        }
+        if (i < n) body<0, false>(i);
+        if (i + 1 < n) body<1, false>(i + 1);
+    }
+};
+
+template <int K, bool WRAPY>
+__global__ __launch_bounds__(256) void step_temporal(const u64* __restrict__ src, u64* __restrict__ dst,
+                                                     const LaneDesc* __restrict__ plan, StepParams p) {
+    const i64 wave = (i64)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    const LaneDesc d = plan[wave * kWaveLanes + lane];
+    const int nrows = __builtin_amdgcn_readfirstlane(d.nrows);
+    if (nrows <= 0) return;  // padding wave (uniform)
+    WaveRunner<K, WRAPY> w(src, dst, d, nrows, p);
+    w.run();
+}
+
+// ------------------------------------------------------------------------------------------
+// LDS-tiled single-generation kernel.
+// ------------------------------------------------------------------------------------------
+constexpr int kLdsRows = 16, kLdsWords = 64;
+
+__global__ __launch_bounds__(256) void step_lds(const u64* __restrict__ src, u64* __restrict__ dst, i64 pitch,
+                                                int R, int h, int nw, int r0, int r1, u32 flags) {
+    __shared__ u64 tile[kLdsRows + 2][kLdsWords + 3];  // +1 pad word per row against bank conflicts
+    const int tr = r0 + blockIdx.y * kLdsRows;  // first output row of the tile
+    const int tc = blockIdx.x * kLdsWords;      // first output word
+    const bool wy = flags & STEP_WRAP_Y, wx = flags & STEP_WRAP_X;
+    // stage (rows tr-1 .. tr+16) x (words tc-1 .. tc+64): 18 x 66 words
+    for (int e = threadIdx.x; e < (kLdsRows + 2) * (kLdsWords + 2); e += 256) {
+        const int rr = e / (kLdsWords + 2), cc = e % (kLdsWords + 2);
+        int row = tr - 1 + rr, col = tc - 1 + cc;
+        if (wy) row = row < 0 ? row + h : (row >= h ? row - h : row);
+        if (wx) col = col < 0 ? nw - 1 : (col >= nw ? 0 : col);
+        u64 v = 0;
+        if (row <= h + R - 1 && col <= nw) v = src[(i64)(R + row) * pitch + (col + 1)];
+        tile[rr][cc] = v;
+    }
+    __syncthreads();
+    for (int e = threadIdx.x; e < kLdsRows * kLdsWords; e += 256) {
+        const int rr = e / kLdsWords, cc = e % kLdsWords;
+        const int row = tr + rr, col = tc + cc;
+        if (row >= r1 || col >= nw) continue;
+        u64 a0, a1, b0, b1, c0, c1;
+        hsum64(tile[rr][cc], tile[rr][cc + 1], tile[rr][cc + 2], a0, a1);
+        hsum64(tile[rr + 1][cc], tile[rr + 1][cc + 1], tile[rr + 1][cc + 2], b0, b1);
+        hsum64(tile[rr + 2][cc], tile[rr + 2][cc + 1], tile[rr + 2][cc + 2], c0, c1);
+        dst[(i64)(R + row) * pitch + (col + 1)] = rule64(a0, a1, b0, b1, c0, c1, tile[rr + 1][cc + 1]);
+    }
+}
+
+}  // namespace
+
+// Instantiated depths.  Larger K amortises HBM traffic over more generations at the cost of
+// registers (10 VGPRs per level per lane) and 2K halo rows per segment.
+#define GOL_FOR_EACH_DEPTH(X) X(1) X(2) X(3) X(4) X(6) X(8) X(12) X(16)
+
+bool step_depth_supported(int k) {
+    switch (k) {
+#define GOL_CASE(K) \
+    case K:         \
+        return true;
+        GOL_FOR_EACH_DEPTH(GOL_CASE)
+#undef GOL_CASE
+        default:
+            return false;
+    }
+}
+
+int max_step_depth() { return 16; }
+
+void launch_step(int k, const u64* src, u64* dst, const LaneDesc* plan, i64 n_waves, const StepParams& p,
+                 hipStream_t s) {
+    const dim3 grid((unsigned)(n_waves / kWavesPerBlock)), block(256);
+    const bool wy = p.flags & STEP_WRAP_Y;
+    switch (k) {
+#define GOL_CASE(K)                                                                          \
+    case K:                                                                                  \
+        if (wy)                                                                              \
+            hipLaunchKernelGGL((step_temporal<K, true>), grid, block, 0, s, src, dst, plan, p);  \
+        else                                                                                 \
+            hipLaunchKernelGGL((step_temporal<K, false>), grid, block, 0, s, src, dst, plan, p); \
+        break;
+        GOL_FOR_EACH_DEPTH(GOL_CASE)
+#undef GOL_CASE
+        default:
+            throw Error(strprintf("no step kernel instantiated for depth %d", k));
+    }
+}
+
+void launch_step_lds(const u64* src, u64* dst, const Layout& L, i64 r0, i64 r1, u32 flags, hipStream_t s) {
+    if (r1 <= r0) return;
+    const dim3 grid((unsigned)ceil_div(L.nw, kLdsWords), (unsigned)ceil_div(r1 - r0, kLdsRows)), block(256);
+    hipLaunchKernelGGL(step_lds, grid, block, 0, s, src, dst, L.pitch, L.R, (int)L.h, (int)L.nw, (int)r0, (int)r1,
+                       flags);
+}
+
+}  // namespace hipk
+}  // namespace gol

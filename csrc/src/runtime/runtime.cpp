@@ -1,0 +1,393 @@
+// gol-mi355x: launch/bootstrap + the reference-compatible CLI driver (see runtime.hpp).
+//
+// Reference program flow (gol-main.c:30-146): argc check -> atoi -> MPI_Init -> fopen dump file ->
+// gol_initMaster (device select + pattern) -> timer -> generation loop -> MPI_Barrier -> rank-0
+// report -> banner -> dump -> MPI_Finalize -> free.  The same order is kept here, with two
+// documented deviations: a barrier before the timer starts (fairer, never slower), and fatal errors
+// abort every rank instead of leaving the others hanging (survey Q8, Q11).
+#include "gol/runtime.hpp"
+
+#include <chrono>
+#include <cstring>
+#include <exception>
+#include <fstream>
+#include <thread>
+
+#include <unistd.h>
+
+#include "gol/io.hpp"
+#include "gol/pattern.hpp"
+
+namespace gol {
+
+namespace {
+
+double wtime() {
+    return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+int env_rank_var(const char* const* names, int dflt) {
+    for (const char* const* n = names; *n; ++n) {
+        const char* v = getenv(*n);
+        if (v && *v) return atoi(v);
+    }
+    return dflt;
+}
+
+}  // namespace
+
+LaunchInfo detect_launch(const Options& o) {
+    LaunchInfo li;
+    static const char* mpi_rank[] = {"PMI_RANK", "OMPI_COMM_WORLD_RANK", "PMIX_RANK", nullptr};
+    static const char* mpi_size[] = {"PMI_SIZE", "OMPI_COMM_WORLD_SIZE", nullptr};
+    static const char* mpi_local[] = {"MPI_LOCALRANKID", "OMPI_COMM_WORLD_LOCAL_RANK", "PMI_LOCAL_RANK", nullptr};
+    static const char* tr_rank[] = {"RANK", nullptr};
+    static const char* tr_size[] = {"WORLD_SIZE", nullptr};
+    static const char* tr_local[] = {"LOCAL_RANK", nullptr};
+    if (o.nranks > 1) {
+        li.mode = "threads";
+        li.size = o.nranks;
+        return li;
+    }
+    if (mpi_launched()) {
+        li.mode = "mpi";
+        li.rank = env_rank_var(mpi_rank, 0);
+        li.size = env_rank_var(mpi_size, 1);
+        li.local_rank = env_rank_var(mpi_local, li.rank);
+        return li;
+    }
+    if (getenv("WORLD_SIZE") && atoi(getenv("WORLD_SIZE")) > 1) {
+        li.mode = "tcp";
+        li.rank = env_rank_var(tr_rank, 0);
+        li.size = env_rank_var(tr_size, 1);
+        li.local_rank = env_rank_var(tr_local, li.rank);
+        return li;
+    }
+    return li;
+}
+
+std::shared_ptr<Transport> make_control_transport(const LaunchInfo& li, int* argc, char*** argv) {
+    if (li.mode == "mpi") {
+        auto t = make_mpi_transport(argc, argv);
+        if (!t) throw Error("launched under mpirun but this build has no MPI support (GOL_WITH_MPI)");
+        return t;
+    }
+    if (li.mode == "tcp") {
+        std::string addr = env_str("MASTER_ADDR", "127.0.0.1");
+        int port = (int)env_int("MASTER_PORT", 29500);
+        return make_tcp_transport(li.rank, li.size, addr, port);
+    }
+    return std::make_shared<SelfTransport>();
+}
+
+std::string select_backend(const Options& o, int rank, int local_rank) {
+    std::string b = o.backend;
+    if (b == "cpu") return b;
+    int err = 0;
+    int n = hip_device_count(&err);
+    if (b == "auto") {
+        if (n <= 0) return "cpu";
+        b = "hip";
+    }
+    if (b != "hip") throw Error("GOL_BACKEND must be auto, hip or cpu (got " + b + ")");
+    if (n <= 0)
+        throw ContractError(strprintf(" Unable to determine cuda device count, error is %d, count is %d\n", err, n), 255);
+    int dev = (local_rank >= 0 ? local_rank : rank) % n;
+    try {
+        hip_set_device(dev);
+    } catch (const Error&) {
+        throw ContractError(strprintf(" Unable to have rank %d set to cuda device %d, error is %d \n", rank, dev, 1),
+                            255);
+    }
+    return b;
+}
+
+std::shared_ptr<Transport> make_data_transport(std::shared_ptr<Transport> control, const std::string& backend,
+                                               const Options& o) {
+    if (backend == "hip" && control->size() > 1 && o.transport != "host") return make_rccl_transport(control);
+    return control;
+}
+
+EngineConfig engine_config(const Options& o, const std::string& backend, int device) {
+    EngineConfig c;
+    c.backend = backend;
+    c.halo_depth = o.halo_depth;
+    c.overlap = o.overlap;
+    c.graph = o.graph;
+    c.compat = o.compat;
+    c.device = device;
+    c.rows_per_wave = o.rows_per_wave;
+    c.waves_target = o.waves_target;
+    c.kernel = env_str("GOL_KERNEL", "temporal");
+    c.transport = o.transport == "rccl" ? "device" : o.transport;
+    c.profile = o.profile;
+    c.graph_supersteps = (int)env_int("GOL_GRAPH_SUPERSTEPS", 0);
+    return c;
+}
+
+// ---------------------------------------------------------------------------------------------
+// Dumps
+// ---------------------------------------------------------------------------------------------
+
+void write_dumps(Engine& eng, FILE* fp) {
+    const Geometry& g = eng.geometry();
+    const Decomposition& d = g.dec;
+    Transport& t = eng.transport();
+    const int r = g.rank;
+    io::write_header(fp, r);
+    std::vector<u64> words = eng.tile_words();
+    const bool tile_is_strip = d.Px == 1 && d.strip_starts[r] == g.row0 && d.strip_starts[r + 1] == g.row0 + g.h;
+    bool all_strips = t.allreduce_min(tile_is_strip ? 1.0 : 0.0) > 0.5;
+    if (all_strips) {
+        io::write_rows(fp, words.data(), g.h, g.w, eng.layout().nw, g.row0);
+        return;
+    }
+    // General case (2-D blocks): gather packed tiles to rank 0, assemble, send each rank its strip.
+    const i64 gw = g.global_words();
+    std::vector<std::vector<u8>> tiles;
+    t.gatherv(words.data(), words.size() * 8, &tiles, 0);
+    if (r == 0) {
+        std::vector<u64> board((size_t)(d.H * gw), 0);
+        for (int q = 0; q < d.P; ++q) {
+            Geometry gq = make_geometry(d, q);
+            const i64 nwq = ceil_div(gq.w, 64);
+            const u64* src = (const u64*)tiles[q].data();
+            for (i64 rr = 0; rr < gq.h; ++rr)
+                memcpy(&board[(size_t)((gq.row0 + rr) * gw + gq.word0())], src + rr * nwq, (size_t)nwq * 8);
+        }
+        for (int q = 0; q < d.P; ++q) {
+            const u64* strip = &board[(size_t)(d.strip_starts[q] * gw)];
+            const i64 rows = d.strip_starts[q + 1] - d.strip_starts[q];
+            if (q == 0)
+                io::write_rows(fp, strip, rows, d.W, gw, d.strip_starts[0]);
+            else
+                t.send_bytes(q, strip, (size_t)(rows * gw) * 8);
+        }
+    } else {
+        const i64 rows = d.strip_starts[r + 1] - d.strip_starts[r];
+        std::vector<u64> strip((size_t)(rows * gw));
+        t.recv_bytes(0, strip.data(), strip.size() * 8);
+        io::write_rows(fp, strip.data(), rows, d.W, gw, d.strip_starts[r]);
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Checkpoints
+// ---------------------------------------------------------------------------------------------
+
+namespace {
+struct CkptHeader {
+    char magic[8];
+    u64 version, H, W, P, Px, Py, rank, row0, col0, h, w, generation, seed;
+};
+std::string ckpt_name(const std::string& prefix, int rank, int P) {
+    return strprintf("%s.rank%d.of%d.gol", prefix.c_str(), rank, P);
+}
+}  // namespace
+
+void save_checkpoint(Engine& eng, const std::string& prefix, u64 seed) {
+    const Geometry& g = eng.geometry();
+    std::vector<u64> words = eng.tile_words();
+    CkptHeader hd{};
+    memcpy(hd.magic, "GOLCKPT1", 8);
+    hd = CkptHeader{{'G', 'O', 'L', 'C', 'K', 'P', 'T', '1'}, 1, (u64)g.dec.H, (u64)g.dec.W, (u64)g.dec.P,
+                    (u64)g.dec.Px, (u64)g.dec.Py, (u64)g.rank, (u64)g.row0, (u64)g.col0, (u64)g.h, (u64)g.w,
+                    eng.generation(), seed};
+    std::string name = ckpt_name(prefix, g.rank, g.dec.P), tmp = name + ".tmp";
+    FILE* f = fopen(tmp.c_str(), "wb");
+    if (!f) throw Error("cannot write checkpoint " + tmp);
+    fwrite(&hd, sizeof(hd), 1, f);
+    fwrite(words.data(), 8, words.size(), f);
+    fclose(f);
+    if (rename(tmp.c_str(), name.c_str()) != 0) throw Error("cannot rename checkpoint " + tmp);
+    eng.transport().barrier();
+}
+
+u64 load_checkpoint(Engine& eng, const std::string& prefix) {
+    const Geometry& g = eng.geometry();
+    std::string name = ckpt_name(prefix, g.rank, g.dec.P);
+    FILE* f = fopen(name.c_str(), "rb");
+    if (!f) throw Error("cannot open checkpoint " + name);
+    CkptHeader hd{};
+    if (fread(&hd, sizeof(hd), 1, f) != 1 || memcmp(hd.magic, "GOLCKPT1", 8) != 0) {
+        fclose(f);
+        throw Error("bad checkpoint header in " + name);
+    }
+    if (hd.H != (u64)g.dec.H || hd.W != (u64)g.dec.W || hd.P != (u64)g.dec.P || hd.row0 != (u64)g.row0 ||
+        hd.col0 != (u64)g.col0 || hd.h != (u64)g.h || hd.w != (u64)g.w) {
+        fclose(f);
+        throw Error("checkpoint " + name + " was written for a different board or decomposition");
+    }
+    std::vector<u64> words((size_t)(g.h * ceil_div(g.w, 64)));
+    size_t got = fread(words.data(), 8, words.size(), f);
+    fclose(f);
+    if (got != words.size()) throw Error("truncated checkpoint " + name);
+    eng.set_tile_words(words);
+    return hd.generation;
+}
+
+// ---------------------------------------------------------------------------------------------
+// CLI
+// ---------------------------------------------------------------------------------------------
+
+namespace {
+
+struct RankResult {
+    int status = 0;
+};
+
+void write_metrics(const Options& o, Engine& eng, const CliArgs& a, double duration, u64 gens, long updates,
+                   const LaunchInfo& li) {
+    if (o.metrics_json.empty() || eng.geometry().rank != 0) return;
+    const EngineStats& s = eng.stats();
+    const Decomposition& d = eng.geometry().dec;
+    std::ofstream f(o.metrics_json);
+    f << "{\n";
+    f << "  \"metric\": \"cell-updates/sec\",\n";
+    f << "  \"cell_updates_per_sec\": " << (duration > 0 ? (double)updates / duration : 0.0) << ",\n";
+    f << "  \"duration_s\": " << duration << ",\n";
+    f << "  \"cell_updates\": " << updates << ",\n";
+    f << "  \"generations\": " << gens << ",\n";
+    f << "  \"pattern\": " << a.pattern << ",\n  \"world_size\": " << a.world_size << ",\n";
+    f << "  \"ranks\": " << d.P << ",\n  \"grid\": \"" << d.Px << "x" << d.Py << "\",\n";
+    f << "  \"board\": [" << d.H << ", " << d.W << "],\n";
+    f << "  \"mode\": \"" << (d.per_rank ? "per-rank" : "global") << "\",\n";
+    f << "  \"launch\": \"" << li.mode << "\",\n";
+    f << "  \"backend\": \"" << eng.backend_name() << "\",\n";
+    f << "  \"transport\": \"" << eng.transport().name() << "\",\n";
+    f << "  \"halo_depth\": " << s.depth << ",\n";
+    f << "  \"supersteps\": " << s.supersteps << ",\n  \"exchanges\": " << s.exchanges << ",\n";
+    f << "  \"halo_bytes_rank0\": " << s.halo_bytes << ",\n";
+    f << "  \"graph_launches\": " << s.graph_launches << ",\n";
+    f << "  \"plan_waves\": " << s.plan_waves << ",\n  \"lane_efficiency\": " << s.lane_efficiency << ",\n";
+    f << "  \"t_exchange_ms\": " << s.t_exchange_ms << ",\n  \"t_compute_ms\": " << s.t_compute_ms << "\n";
+    f << "}\n";
+}
+
+int run_rank(const CliArgs& a, const Options& o, const LaunchInfo& li, std::shared_ptr<Transport> control) {
+    const int rank = control->rank(), P = control->size();
+    FILE* fp = nullptr;
+    if (a.on_off == 1) {
+        std::string fname = io::dump_filename(rank, P);
+        fp = fopen(fname.c_str(), "w");
+        if (!fp) {
+            printf("ERROR IN RANK %d", rank);
+            fflush(stdout);
+            control->abort(255);
+        }
+    }
+    try {
+        const int local = li.mode == "threads" ? rank : li.local_rank;
+        std::string backend = select_backend(o, rank, local);
+        int device = -1;
+        if (backend == "hip") {
+            int n = hip_device_count();
+            device = local % n;
+        }
+        Decomposition dec = make_decomposition((i64)a.world_size, P, o.global_mode, o.decomp, o.grid);
+        Geometry g = make_geometry(dec, rank);
+        PatternSpec pat = make_pattern(a.pattern, dec, o.seed);
+        std::shared_ptr<Transport> t = make_data_transport(control, backend, o);
+        std::unique_ptr<Engine> eng = Engine::create(g, engine_config(o, backend, device), t);
+        if (o.verbose && rank == 0) fprintf(stderr, "[gol] %s\n", eng->describe().c_str());
+        eng->init(pat);
+        u64 done = 0;
+        if (!o.restart.empty()) done = load_checkpoint(*eng, o.restart);
+        const u64 total = a.iterations;
+        const u64 todo = done >= total ? 0 : total - done;
+
+        t->barrier();
+        const double t0 = wtime();
+        if (o.checkpoint_every > 0) {
+            u64 left = todo;
+            while (left > 0) {
+                u64 chunk = std::min<u64>(left, (u64)o.checkpoint_every);
+                eng->run(chunk);
+                left -= chunk;
+                save_checkpoint(*eng, o.checkpoint_path, o.seed);
+            }
+        } else {
+            eng->run(todo);
+        }
+        eng->synchronize();
+        t->barrier();
+        const double duration = wtime() - t0;
+        const long updates = (long)P * (long)g.h * (long)g.w * (long)todo;
+        // Reference formula counts P * N * N * iterations (gol-main.c:124-125): in per-rank mode and
+        // 1-D that is exactly sum over ranks of h*w*iterations; use the global count in general.
+        const long count = (long)dec.H * (long)dec.W * (long)todo;
+        (void)updates;
+        if (rank == 0) {
+            std::string line = io::timing_line(duration, count);
+            fwrite(line.data(), 1, line.size(), stdout);
+            fputs(io::kBanner, stdout);
+            fflush(stdout);
+        }
+        write_metrics(o, *eng, a, duration, todo, count, li);
+        if (fp) {
+            write_dumps(*eng, fp);
+            fclose(fp);
+            fp = nullptr;
+        }
+        t->barrier();
+        return 0;
+    } catch (const ContractError& e) {
+        fputs(e.what(), stdout);
+        fflush(stdout);
+        if (fp) fclose(fp);
+        if (P > 1) control->abort(e.exit_status);
+        return e.exit_status;
+    }
+}
+
+}  // namespace
+
+int run_cli(int argc, char** argv) {
+    CliArgs a;
+    if (!parse_cli(argc, argv, a)) {
+        printf("%s", kUsage);
+        fflush(stdout);
+        return 255;  // exit(-1), before any communicator (gol-main.c:43-47)
+    }
+    try {
+        Options o = options_from_env();
+        LaunchInfo li = detect_launch(o);
+        if (li.mode == "threads") {
+            auto group = make_thread_group(li.size);
+            std::vector<int> status((size_t)li.size, 0);
+            std::vector<std::thread> th;
+            for (int r = 0; r < li.size; ++r) {
+                th.emplace_back([&, r] {
+                    try {
+                        auto t = std::make_shared<ThreadTransport>(group, r);
+                        status[(size_t)r] = run_rank(a, o, li, t);
+                    } catch (const std::exception& e) {
+                        fprintf(stderr, "[gol] rank %d: %s\n", r, e.what());
+                        fflush(stderr);
+                        _exit(1);
+                    }
+                });
+            }
+            for (auto& x : th) x.join();
+            for (int s : status)
+                if (s) return s;
+            return 0;
+        }
+        auto control = make_control_transport(li, &argc, &argv);
+        int st = 0;
+        try {
+            st = run_rank(a, o, li, control);
+        } catch (const std::exception& e) {
+            fprintf(stderr, "[gol] rank %d: %s\n", control->rank(), e.what());
+            fflush(stderr);
+            if (control->size() > 1) control->abort(1);
+            return 1;
+        }
+        return st;
+    } catch (const std::exception& e) {
+        fprintf(stderr, "[gol] %s\n", e.what());
+        return 1;
+    }
+}
+
+}  // namespace gol

@@ -1,0 +1,284 @@
+// gol-mi355x: host-side C++ unit tests (no GPU needed).  Run: build/gol_unit
+//
+// Covers: CLI parsing, decomposition geometry, pattern placement (survey §2.9), planner coverage,
+// the bit-sliced CPU stepper vs a byte-per-cell oracle (any width, incl. N % 64 != 0), temporal
+// supersteps vs single generations, dump formatting, and multi-rank engines over ThreadTransport
+// (1-D and 2-D, P <= 2 canonical ordering) against the single-rank result.
+#include <cstring>
+#include <functional>
+#include <random>
+#include <thread>
+
+#include "gol/bits.hpp"
+#include "gol/config.hpp"
+#include "gol/cpu.hpp"
+#include "gol/engine.hpp"
+#include "gol/io.hpp"
+#include "gol/pattern.hpp"
+#include "gol/plan.hpp"
+
+using namespace gol;
+
+static int g_fail = 0, g_pass = 0;
+#define CHECK(c)                                                              \
+    do {                                                                      \
+        if (!(c)) {                                                           \
+            if (g_fail < 20) fprintf(stderr, "FAIL %s:%d: %s\n", __FILE__, __LINE__, #c); \
+            ++g_fail;                                                         \
+        } else {                                                              \
+            ++g_pass;                                                         \
+        }                                                                     \
+    } while (0)
+
+// ---------- byte oracle ----------
+static std::vector<u8> byte_step(const std::vector<u8>& b, i64 H, i64 W) {
+    std::vector<u8> o(b.size());
+    for (i64 y = 0; y < H; ++y)
+        for (i64 x = 0; x < W; ++x) {
+            int n = 0;
+            for (int dy = -1; dy <= 1; ++dy)
+                for (int dx = -1; dx <= 1; ++dx)
+                    if (dy || dx) n += b[(size_t)(pmod(y + dy, H) * W + pmod(x + dx, W))];
+            u8 c = b[(size_t)(y * W + x)];
+            o[(size_t)(y * W + x)] = (u8)(n == 3 || (c && n == 2));
+        }
+    return o;
+}
+
+static std::vector<u64> pack(const std::vector<u8>& b, i64 H, i64 W) {
+    i64 nw = ceil_div(W, 64);
+    std::vector<u64> w((size_t)(H * nw), 0);
+    for (i64 y = 0; y < H; ++y)
+        for (i64 x = 0; x < W; ++x)
+            if (b[(size_t)(y * W + x)]) w[(size_t)(y * nw + x / 64)] |= 1ull << (x % 64);
+    return w;
+}
+
+static std::vector<u8> random_board(i64 H, i64 W, unsigned seed) {
+    std::mt19937 rng(seed);
+    std::vector<u8> b((size_t)(H * W));
+    for (auto& v : b) v = (u8)(rng() & 1);
+    return b;
+}
+
+static void test_cli() {
+    CliArgs a;
+    const char* bad[] = {"gol", "1", "2"};
+    CHECK(!parse_cli(3, bad, a));
+    const char* ok[] = {"gol", "4", "32", "2", "66000", "1"};
+    CHECK(parse_cli(6, ok, a));
+    CHECK(a.pattern == 4 && a.world_size == 32 && a.iterations == 2 && a.on_off == 1);
+    CHECK(a.threads == (unsigned short)66000);  // ushort truncation like the reference
+    CHECK(std::string(kUsage).find("GOL requires 5 arguments") == 0);
+}
+
+static void test_geometry() {
+    Decomposition d = make_decomposition(32, 4, false, "1d", "");
+    CHECK(d.H == 128 && d.W == 32 && d.Px == 1 && d.Py == 4);
+    Geometry g = make_geometry(d, 0);
+    CHECK(g.nbr[DIR_N] == 3 && g.nbr[DIR_S] == 1 && g.h == 32);
+    Decomposition d2 = make_decomposition(256, 8, true, "2d", "4x2");
+    CHECK(d2.Px == 4 && d2.Py == 2 && d2.col_starts[1] == 64);
+    Geometry g5 = make_geometry(d2, 5);  // cx=1, cy=1
+    CHECK(g5.cx == 1 && g5.cy == 1 && g5.nbr[DIR_NW] == 0 && g5.nbr[DIR_SE] == 2 && g5.nbr[DIR_E] == 6);
+    Decomposition d3 = make_decomposition(100, 3, true, "1d", "");
+    CHECK(d3.row_starts[1] == 34 && d3.row_starts[3] == 100);
+    CHECK(clamp_halo_depth(d3, 99) == 33);
+}
+
+static void test_patterns() {
+    Decomposition d = make_decomposition(140, 2, false, "1d", "");
+    PatternSpec p2 = make_pattern(2, d, 0);
+    CHECK(p2.cells.size() == 20);
+    CHECK(p2.cells[0].first == 139 && p2.cells[0].second == 127 && p2.cells[9].second == 136);
+    CHECK(p2.cells[10].first == 279);
+    PatternSpec p3 = make_pattern(3, make_decomposition(6, 1, false, "1d", ""), 0);
+    CHECK(p3.cells.size() == 2);  // P=1: else-if never sets the lower corners
+    PatternSpec p3b = make_pattern(3, make_decomposition(6, 2, false, "1d", ""), 0);
+    CHECK(p3b.cells.size() == 4 && p3b.cells[2].first == 11 && p3b.cells[2].second == 0);
+    PatternSpec p4 = make_pattern(4, make_decomposition(6, 2, false, "1d", ""), 0);
+    CHECK(p4.cells.size() == 3 && p4.cells[2].second == 5);
+    bool threw = false;
+    try {
+        make_pattern(7, d, 0);
+    } catch (const ContractError& e) {
+        threw = std::string(e.what()) == "Pattern 7 has not been implemented \n" && e.exit_status == 255;
+    }
+    CHECK(threw);
+}
+
+static void test_plan() {
+    for (i64 nw : {1, 2, 61, 62, 63, 130, 512}) {
+        for (bool xwrap : {false, true}) {
+            std::vector<Region> rg = {{0, 7, 0, nw}, {7, 40, 0, nw}};
+            PlanStats st;
+            auto lanes = build_plan(rg, nw, 40, 9, 2, xwrap, &st);
+            std::vector<int> cover((size_t)(40 * nw), 0);
+            for (size_t w = 0; w < lanes.size() / 64; ++w) {
+                int nrows = lanes[w * 64].nrows;
+                for (int l = 0; l < 64; ++l) {
+                    const LaneDesc& d = lanes[w * 64 + l];
+                    CHECK(d.nrows == nrows);
+                    CHECK(d.col >= -1 && d.col <= nw);
+                    if (xwrap) CHECK(d.col >= 0 && d.col < nw);
+                    if (d.flags & LANE_STORE)
+                        for (int r = 0; r < d.nrows; ++r) cover[(size_t)((d.row0 + r) * nw + d.col)]++;
+                }
+            }
+            bool all1 = true;
+            for (int c : cover) all1 &= c == 1;
+            CHECK(all1);
+        }
+    }
+}
+
+static void test_cpu_step() {
+    for (i64 W : {1, 2, 5, 63, 64, 65, 127, 137, 200}) {
+        for (i64 H : {1, 3, 17}) {
+            auto b = random_board(H, W, (unsigned)(W * 131 + H));
+            Layout L(H, W, 1);
+            std::vector<u64> a((size_t)L.words(), 0), c((size_t)L.words(), 0);
+            auto pw = pack(b, H, W);
+            cpu::insert_words(a.data(), L, pw.data());
+            u64* cur = a.data();
+            u64* oth = c.data();
+            auto ref = b;
+            for (int g = 0; g < 4; ++g) {
+                cpu::fill_ghost_cols_wrap(cur, L, 0, H);
+                cpu::fill_ghost_rows_wrap(cur, L);
+                cpu::step_rows(cur, oth, L, 0, H);
+                std::swap(cur, oth);
+                ref = byte_step(ref, H, W);
+            }
+            std::vector<u64> out((size_t)(H * L.nw));
+            cpu::extract_words(cur, L, out.data());
+            CHECK(out == pack(ref, H, W));
+        }
+    }
+}
+
+// Engine over P thread-ranks; returns the global board (H x nw words) of the result.
+static std::vector<u64> run_engines(i64 N, int P, bool global, const std::string& decomp, const std::string& grid,
+                                    int depth, unsigned pattern, int gens, bool compat, u64* fp_out = nullptr) {
+    Decomposition d = make_decomposition(N, P, global, decomp, grid);
+    auto group = make_thread_group(P);
+    const i64 gw = ceil_div(d.W, 64);
+    std::vector<u64> board((size_t)(d.H * gw), 0);
+    std::vector<std::thread> th;
+    std::vector<u64> fps((size_t)P);
+    for (int r = 0; r < P; ++r)
+        th.emplace_back([&, r] {
+            auto t = std::make_shared<ThreadTransport>(group, r);
+            Geometry g = make_geometry(d, r);
+            EngineConfig c;
+            c.backend = "cpu";
+            c.halo_depth = depth;
+            c.compat = compat;
+            auto e = Engine::create(g, c, t);
+            e->init(make_pattern(pattern, d, 77));
+            e->run((u64)gens);
+            auto w = e->tile_words();
+            fps[(size_t)r] = e->fingerprint();
+            i64 nw = e->layout().nw;
+            for (i64 y = 0; y < g.h; ++y)
+                memcpy(&board[(size_t)((g.row0 + y) * gw + g.word0())], &w[(size_t)(y * nw)], (size_t)nw * 8);
+        });
+    for (auto& x : th) x.join();
+    if (fp_out) *fp_out = fps[0];
+    return board;
+}
+
+static void test_engines() {
+    // 1-D and 2-D, P in {1,2,3,4}, depth in {1,3,8}, vs a single-rank depth-1 run of the global board
+    for (int P : {1, 2, 3, 4}) {
+        for (int depth : {1, 3, 8}) {
+            auto ref = run_engines(64 * P, 1, true, "1d", "", 1, 5, 13, false);
+            auto got = run_engines(64 * P, P, true, "1d", "", depth, 5, 13, false);
+            CHECK(got == ref);
+            if (P == 4 || P == 2) {
+                auto g2 = run_engines(64 * P, P, true, "2d", P == 4 ? "2x2" : "2x1", depth, 5, 13, false);
+                CHECK(g2 == ref);
+            }
+        }
+    }
+    // per-rank mode (reference geometry), odd width, vs byte oracle of the (P*N) x N torus
+    for (int P : {1, 2, 3}) {
+        const i64 N = 37;
+        Decomposition d = make_decomposition(N, P, false, "1d", "");
+        auto got = run_engines(N, P, false, "1d", "", 4, 5, 9, false);
+        std::vector<u8> b((size_t)(d.H * d.W));
+        const i64 gw = ceil_div(d.W, 64);
+        for (i64 y = 0; y < d.H; ++y)
+            for (i64 x = 0; x < d.W; ++x)
+                b[(size_t)(y * d.W + x)] = (u8)((random_word(77, y, x / 64, gw) >> (x % 64)) & 1);
+        for (int g = 0; g < 9; ++g) b = byte_step(b, d.H, d.W);
+        CHECK(got == pack(b, d.H, d.W));
+    }
+    // fingerprint invariance across decompositions
+    u64 f1 = 0, f2 = 0, f3 = 0;
+    run_engines(256, 1, true, "1d", "", 8, 5, 20, false, &f1);
+    run_engines(256, 4, true, "1d", "", 8, 5, 20, false, &f2);
+    run_engines(256, 4, true, "2d", "2x2", 8, 5, 20, false, &f3);
+    CHECK(f1 == f2 && f2 == f3 && f1 != 0);
+}
+
+static void test_compat() {
+    // Quirk model (survey Q3): P=1, pattern 4 blinker across the x-wrap, constant ghost rows =
+    // (above = own first row, below = own last row).
+    const i64 N = 6;
+    auto got = run_engines(N, 1, false, "1d", "", 1, 4, 1, true);
+    // emulate: ghost above = row0 (1 1 0 0 0 1), below = row5 (0s)
+    std::vector<u8> b((size_t)(N * N), 0);
+    b[0] = b[1] = b[5] = 1;
+    std::vector<u8> ext((size_t)((N + 2) * N), 0);
+    for (i64 x = 0; x < N; ++x) ext[(size_t)x] = b[(size_t)x];                       // above
+    for (i64 y = 0; y < N; ++y)
+        for (i64 x = 0; x < N; ++x) ext[(size_t)((y + 1) * N + x)] = b[(size_t)(y * N + x)];
+    std::vector<u8> o((size_t)(N * N));
+    for (i64 y = 0; y < N; ++y)
+        for (i64 x = 0; x < N; ++x) {
+            int n = 0;
+            for (int dy = -1; dy <= 1; ++dy)
+                for (int dx = -1; dx <= 1; ++dx)
+                    if (dy || dx) n += ext[(size_t)((y + 1 + dy) * N + pmod(x + dx, N))];
+            u8 c = b[(size_t)(y * N + x)];
+            o[(size_t)(y * N + x)] = (u8)(n == 3 || (c && n == 2));
+        }
+    CHECK(got == pack(o, N, N));
+}
+
+static void test_dump() {
+    std::vector<u64> w = {0b100011ull};
+    std::string s = io::format_rows(w.data(), 1, 6, 1, 0);
+    CHECK(s == "Row  0: 1 1 0 0 0 1 \n");
+    CHECK(io::dump_header(3) ==
+          "######################### FINAL WORLD IN RANK 3 IS ###############################\n");
+    CHECK(io::timing_line(0.5, 1234) == "TOTAL DURATION : 0.50000, number of cell updates = 1234\n");
+    CHECK(io::dump_filename(2, 8) == "Rank_2_of_8.txt");
+    std::vector<u64> w2 = {~0ull, 0x5ull};
+    std::string s2 = io::format_rows(w2.data(), 1, 67, 2, 123);
+    CHECK(s2.substr(0, 9) == "Row 123: " && s2.size() == 9 + 2 * 67 + 1 && s2.substr(9 + 128, 6) == "1 0 1 ");
+}
+
+static void test_bits() {
+    CHECK(bitop3_ref(0xF0, 0xCC, 0xAA, kLutXor3) == (0xF0ull ^ 0xCC ^ 0xAA) && kLutY1 != kLutY2);
+    std::vector<u64> row = {0x8000000000000001ull};
+    CHECK(wrap64(row.data(), 64, -64) == row[0] && wrap64(row.data(), 64, 1) == ((row[0] >> 1) | (row[0] << 63)));
+    std::vector<u64> r5 = {0b10011ull};  // width 5: periodic 1 1 0 0 1
+    u64 v = wrap64(r5.data(), 5, 5);
+    CHECK((v & 0x3FF) == 0b1001110011ull);
+}
+
+int main() {
+    test_cli();
+    test_geometry();
+    test_patterns();
+    test_plan();
+    test_bits();
+    test_cpu_step();
+    test_dump();
+    test_engines();
+    test_compat();
+    printf("gol_unit: %d checks passed, %d failed\n", g_pass, g_fail);
+    return g_fail ? 1 : 0;
+}

@@ -1,0 +1,170 @@
+"""The flagship "model": a Game of Life simulation on one rank of a (possibly multi-GPU) job.
+
+Reference behaviour being reproduced (cited for parity checks):
+
+* board = P stacked N x N tiles forming a (P*N) x N torus (``gol-main.c:76``, ``gol-main.c:84-87``);
+* rule B3/S23 (``gol-with-cuda.cu:239-257``);
+* patterns 0-4 (``gol-with-cuda.cu:55-171``) plus pattern 5 (seeded random, decomposition-invariant);
+* per-rank dump files (``gol-main.c:17-28, 64-73, 134-139``).
+
+The heavy lifting is native: :class:`Simulation` drives a ``_gol.Engine`` (HIP or CPU backend).
+"""
+from __future__ import annotations
+
+import dataclasses
+import os
+from typing import Optional
+
+import numpy as np
+
+from .._native import _gol
+from ..ops.bitpack import unpack_words
+
+
+@dataclasses.dataclass(frozen=True)
+class LifeRule:
+    """A Life-like rule in B/S notation.  The native kernels implement B3/S23 (Conway)."""
+
+    birth: tuple = (3,)
+    survive: tuple = (2, 3)
+
+    @property
+    def notation(self) -> str:
+        return "B" + "".join(map(str, self.birth)) + "/S" + "".join(map(str, self.survive))
+
+    def apply(self, alive: np.ndarray, neighbours: np.ndarray) -> np.ndarray:
+        born = np.isin(neighbours, self.birth) & ~alive
+        keep = np.isin(neighbours, self.survive) & alive
+        return born | keep
+
+
+CONWAY = LifeRule()
+
+
+def default_backend() -> str:
+    b = os.environ.get("GOL_BACKEND", "auto")
+    if b != "auto":
+        return b
+    return "hip" if _gol.hip_device_count() > 0 else "cpu"
+
+
+class Simulation:
+    """One rank's view of a Game of Life job.
+
+    Parameters
+    ----------
+    N:            the reference ``worldSize`` (per-rank tile side), or the global side with ``global_mode``.
+    transport:    a ``_gol.Transport``; defaults to a single-rank transport.  See
+                  :mod:`gol_amd.parallel` for torch.distributed / RCCL / thread transports.
+    backend:      ``"hip"``, ``"cpu"`` or ``"auto"``.
+    halo_depth:   generations per halo exchange (temporal blocking depth, <= 64; HIP caps at 16).
+    decomp/grid:  ``"1d"`` row strips (reference) or ``"2d"`` blocks, optional ``"PxxPy"`` grid.
+    compat:       reproduce the reference's halo quirks (frozen gen-0 halos, P<=2 swap).
+    """
+
+    def __init__(
+        self,
+        N: int,
+        transport=None,
+        *,
+        backend: str = "auto",
+        global_mode: bool = False,
+        decomp: str = "1d",
+        grid: str = "",
+        halo_depth: int = 8,
+        overlap: bool = True,
+        graph: bool = True,
+        compat: bool = False,
+        device: Optional[int] = None,
+        kernel: str = "temporal",
+        rows_per_wave: int = 0,
+        waves_target: int = 0,
+        profile: bool = False,
+    ):
+        self.transport = transport if transport is not None else _gol.SelfTransport()
+        P, rank = self.transport.size(), self.transport.rank()
+        self.backend = default_backend() if backend == "auto" else backend
+        self.decomposition = _gol.make_decomposition(N, P, global_mode, decomp, grid)
+        self.geometry = _gol.make_geometry(self.decomposition, rank)
+        cfg = _gol.EngineConfig()
+        cfg.backend = self.backend
+        cfg.halo_depth = halo_depth
+        cfg.overlap = overlap
+        cfg.graph = graph
+        cfg.compat = compat
+        cfg.kernel = kernel
+        cfg.rows_per_wave = rows_per_wave
+        cfg.waves_target = waves_target
+        cfg.profile = profile
+        if self.backend == "hip":
+            n = _gol.hip_device_count()
+            if n <= 0:
+                raise RuntimeError("backend 'hip' requested but no HIP device is visible")
+            cfg.device = (rank if device is None else device) % n
+        self.config = cfg
+        self.engine = _gol.Engine.create(self.geometry, cfg, self.transport)
+        self.pattern = None
+
+    # -- lifecycle -------------------------------------------------------------------------
+    def init(self, pattern: int = 5, seed: int = 0x5EED) -> "Simulation":
+        self.pattern = _gol.make_pattern(pattern, self.decomposition, seed)
+        self.engine.init(self.pattern)
+        return self
+
+    def step(self, generations: int = 1) -> "Simulation":
+        self.engine.run(int(generations))
+        return self
+
+    run = step
+
+    def synchronize(self) -> None:
+        self.engine.synchronize()
+
+    # -- state -----------------------------------------------------------------------------
+    @property
+    def generation(self) -> int:
+        return self.engine.generation
+
+    def words(self) -> np.ndarray:
+        """Local tile as packed uint64 words, shape (h, ceil(w/64)); bit b of word c = column 64c+b."""
+        return self.engine.tile_words()
+
+    def board(self) -> np.ndarray:
+        """Local tile as a (h, w) uint8 array of 0/1 cells."""
+        return unpack_words(self.words(), self.geometry.w)
+
+    def set_board(self, cells: np.ndarray) -> None:
+        from ..ops.bitpack import pack_cells
+
+        cells = np.asarray(cells)
+        if cells.shape != (self.geometry.h, self.geometry.w):
+            raise ValueError(f"expected a {(self.geometry.h, self.geometry.w)} board, got {cells.shape}")
+        self.engine.set_tile_words(pack_cells(cells))
+
+    def population(self) -> int:
+        """Global live-cell count (collective)."""
+        return int(self.engine.population())
+
+    def fingerprint(self) -> int:
+        """Decomposition-invariant fingerprint of the global board (collective)."""
+        return int(self.engine.fingerprint())
+
+    def stats(self) -> dict:
+        return self.engine.stats()
+
+    def describe(self) -> str:
+        return self.engine.describe()
+
+    # -- I/O -------------------------------------------------------------------------------
+    def dump(self, path: Optional[str] = None) -> str:
+        """Write this rank's reference-format dump file (collective); returns the path."""
+        if path is None:
+            path = _gol.dump_filename(self.geometry.rank, self.decomposition.P)
+        _gol.write_dumps(self.engine, path)
+        return path
+
+    def checkpoint(self, prefix: str) -> None:
+        _gol.save_checkpoint(self.engine, prefix, self.pattern.seed if self.pattern else 0)
+
+    def restore(self, prefix: str) -> int:
+        return int(_gol.load_checkpoint(self.engine, prefix))

@@ -1,0 +1,16 @@
+"""Parallelism: spatial domain decomposition (1-D row strips / 2-D blocks with corner halos) across
+ranks, one process per GPU, RCCL halo exchange over xGMI (see :mod:`.dist`)."""
+from .dist import (  # noqa: F401
+    env_rank,
+    init_distributed,
+    rccl_transport,
+    tcp_transport,
+    thread_transports,
+    torch_transport,
+)
+from .._native import _gol as _native
+
+
+def decomposition(N: int, P: int, global_mode: bool = False, decomp: str = "1d", grid: str = ""):
+    """The native decomposition (tile extents per rank, process grid, dump strips)."""
+    return _native.make_decomposition(N, P, global_mode, decomp, grid)
