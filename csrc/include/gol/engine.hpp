@@ -108,6 +108,8 @@ class Engine {
     // Compat mode: install constant depth-1 ghost rows (both buffers); rows are full-pitch.
     virtual void do_set_compat_halos(const std::vector<u64>& above, const std::vector<u64>& below) = 0;
     virtual std::vector<u64> read_row(i64 r) = 0;  // full-pitch row r of the current buffer
+    // Largest superstep depth <= want that the backend can run (HIP: instantiated kernel depths).
+    virtual int supported_depth(int want) const { return want; }
     void setup_compat();
     void maybe_inject_fault();
 

@@ -116,7 +116,7 @@ void Engine::maybe_inject_fault() {
 void Engine::run(u64 generations) {
     while (generations > 0) {
         maybe_inject_fault();
-        int k = cfg_.compat ? 1 : (int)std::min<u64>((u64)L_.R, generations);
+        int k = cfg_.compat ? 1 : supported_depth((int)std::min<u64>((u64)L_.R, generations));
         do_superstep(k);
         gen_ += (u64)k;
         generations -= (u64)k;

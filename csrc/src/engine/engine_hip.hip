@@ -292,6 +292,12 @@ class HipEngine : public Engine {
         return row;
     }
 
+    int supported_depth(int want) const override {
+        if (cfg_.kernel == "lds") return 1;
+        while (want > 1 && !hipk::step_depth_supported(want)) --want;
+        return std::max(1, want);
+    }
+
    private:
     // ----- plans -----
     u32 step_flags() const {

@@ -1,0 +1,167 @@
+"""The `gol` executable keeps the reference contract (gol-main.c:30-146) byte for byte.
+
+Runs the native binary on the CPU backend (GOL_BACKEND=cpu) so it works without a GPU; multi-rank
+runs use thread mode (GOL_NRANKS), the torchrun-style TCP rendezvous, and mpirun (MPICH) when
+available.
+"""
+import os
+import shutil
+import socket
+import subprocess
+
+import numpy as np
+import pytest
+
+from gol_amd.ops import initial_board, numpy_step, quirk_model
+from gol_amd.utils import read_dump
+
+USAGE = (
+    "GOL requires 5 arguments: pattern number, sq size of the world and the number of itterations, "
+    "threads per block and output-on-off e.g. ./gol 0 32 2 512 0 \n"
+)
+BANNER = "This is the Game of Life running in parallel on a GPU on multiple ranks.\n"
+
+
+def run(gol_bin, args, cwd, env=None, nranks=None):
+    e = dict(os.environ)
+    e["GOL_BACKEND"] = "cpu"
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "PMI_RANK", "PMI_SIZE"):
+        e.pop(k, None)
+    if nranks:
+        e["GOL_NRANKS"] = str(nranks)
+    if env:
+        e.update(env)
+    return subprocess.run([gol_bin, *map(str, args)], cwd=cwd, env=e, capture_output=True, text=True, timeout=120)
+
+
+def load_board(cwd, P):
+    parts = []
+    for r in range(P):
+        rank, first, cells = read_dump(os.path.join(cwd, f"Rank_{r}_of_{P}.txt"))
+        assert rank == r
+        parts.append((first, cells))
+    parts.sort(key=lambda t: t[0])
+    return np.vstack([c for _, c in parts])
+
+
+def test_usage(gol_bin, tmp_path):
+    r = run(gol_bin, [1, 2, 3], tmp_path)
+    assert r.returncode == 255 and r.stdout == USAGE
+
+
+def test_unknown_pattern(gol_bin, tmp_path):
+    r = run(gol_bin, [9, 8, 1, 64, 1], tmp_path)
+    assert r.returncode == 255
+    assert r.stdout == "Pattern 9 has not been implemented \n"
+    # like the reference, the dump file was opened before the pattern check
+    assert os.path.exists(tmp_path / "Rank_0_of_1.txt")
+
+
+def test_report_lines(gol_bin, tmp_path):
+    r = run(gol_bin, [5, 64, 10, 512, 0], tmp_path)
+    assert r.returncode == 0, r.stderr
+    lines = r.stdout.splitlines(keepends=True)
+    assert len(lines) == 2 and lines[1] == BANNER
+    assert lines[0].startswith("TOTAL DURATION : ") and lines[0].endswith(", number of cell updates = 40960\n")
+    assert not list(tmp_path.glob("Rank_*"))  # on_off != 1 writes nothing
+
+
+def test_dump_bytes(gol_bin, tmp_path):
+    r = run(gol_bin, [4, 6, 0, 64, 1], tmp_path)
+    assert r.returncode == 0
+    text = (tmp_path / "Rank_0_of_1.txt").read_text()
+    expect = "#" * 25 + " FINAL WORLD IN RANK 0 IS " + "#" * 31 + "\n" + "Row  0: 1 1 0 0 0 1 \n"
+    expect += "".join("Row  %d: 0 0 0 0 0 0 \n" % i for i in range(1, 6))
+    assert text == expect
+
+
+@pytest.mark.parametrize("pattern", [0, 1, 2, 3, 4, 5])
+@pytest.mark.parametrize("P", [1, 2, 3, 4])
+def test_patterns_multi_rank_threads(gol_bin, tmp_path, pattern, P):
+    N, gens = 140, 7
+    r = run(gol_bin, [pattern, N, gens, 256, 1], tmp_path, nranks=P)
+    assert r.returncode == 0, r.stderr
+    assert r.stdout.endswith(f"number of cell updates = {P * N * N * gens}\n" + BANNER)
+    got = load_board(tmp_path, P)
+    assert np.array_equal(got, numpy_step(initial_board(pattern, N, P, True), gens))
+
+
+@pytest.mark.parametrize("P", [1, 2, 3, 4])
+def test_compat_reference_quirks(gol_bin, tmp_path, P):
+    N, gens = 24, 9
+    r = run(gol_bin, [5, N, gens, 64, 1], tmp_path, env={"GOL_COMPAT": "reference"}, nranks=P)
+    assert r.returncode == 0, r.stderr
+    got = load_board(tmp_path, P)
+    assert np.array_equal(got, quirk_model(initial_board(5, N, P, True), P, gens))
+
+
+@pytest.mark.parametrize("env", [{"GOL_DECOMP": "2d", "GOL_GRID": "2x2"}, {"GOL_GLOBAL": "1"},
+                                 {"GOL_GLOBAL": "1", "GOL_DECOMP": "2d"}, {"GOL_HALO_DEPTH": "1"}])
+def test_decompositions_identical_dumps(gol_bin, tmp_path, env):
+    N, gens, P = 256, 12, 4
+    r = run(gol_bin, [5, N, gens, 256, 1], tmp_path, env=env, nranks=P)
+    assert r.returncode == 0, r.stderr
+    got = load_board(tmp_path, P)
+    per_rank = env.get("GOL_GLOBAL") != "1"
+    assert np.array_equal(got, numpy_step(initial_board(5, N, P, per_rank), gens))
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+@pytest.mark.parametrize("P", [2, 3])
+def test_torchrun_style_tcp(gol_bin, tmp_path, P):
+    N, gens = 96, 10
+    port = _free_port()
+    procs = []
+    for r in range(P):
+        e = dict(os.environ, GOL_BACKEND="cpu", RANK=str(r), WORLD_SIZE=str(P), LOCAL_RANK=str(r),
+                 MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([gol_bin, "5", str(N), str(gens), "256", "1"], cwd=tmp_path, env=e,
+                                      stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True))
+    outs = [p.communicate(timeout=120) for p in procs]
+    assert all(p.returncode == 0 for p in procs), outs
+    assert outs[0][0].endswith(BANNER) and outs[1][0] == ""
+    assert np.array_equal(load_board(tmp_path, P), numpy_step(initial_board(5, N, P, True), gens))
+
+
+MPIRUN = shutil.which("mpirun", path="/opt/conda/bin")
+
+
+@pytest.mark.skipif(MPIRUN is None, reason="no mpirun")
+def test_mpirun_launch(gol_bin, tmp_path):
+    N, gens, P = 64, 6, 2
+    e = dict(os.environ, GOL_BACKEND="cpu")
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK"):
+        e.pop(k, None)
+    r = subprocess.run([MPIRUN, "-n", str(P), gol_bin, "3", str(N), str(gens), "256", "1"], cwd=tmp_path, env=e,
+                       capture_output=True, text=True, timeout=120)
+    if r.returncode != 0 and "HYDU" in (r.stderr + r.stdout):
+        pytest.skip("mpirun cannot launch in this sandbox: " + r.stderr[-200:])
+    assert r.returncode == 0, r.stderr
+    assert np.array_equal(load_board(tmp_path, P), numpy_step(initial_board(3, N, P, True), gens))
+
+
+def test_checkpoint_restart(gol_bin, tmp_path):
+    N, P = 128, 2
+    a = tmp_path / "a"
+    b = tmp_path / "b"
+    a.mkdir()
+    b.mkdir()
+    r = run(gol_bin, [5, N, 20, 256, 1], a, nranks=P, env={"GOL_CHECKPOINT_EVERY": "8",
+                                                          "GOL_CHECKPOINT_PATH": str(tmp_path / "ck")})
+    assert r.returncode == 0, r.stderr
+    # restart from the generation-16 snapshot and finish the same 20 generations
+    r2 = run(gol_bin, [5, N, 20, 256, 1], b, nranks=P, env={"GOL_RESTART": str(tmp_path / "ck")})
+    assert r2.returncode == 0, r2.stderr
+    for q in range(P):
+        assert (a / f"Rank_{q}_of_{P}.txt").read_text() == (b / f"Rank_{q}_of_{P}.txt").read_text()
+
+
+def test_fault_injection_aborts_all_ranks(gol_bin, tmp_path):
+    r = run(gol_bin, [5, 64, 40, 256, 0], tmp_path, nranks=3, env={"GOL_FAULT": "1:16"})
+    assert r.returncode == 3
+    assert "injected failure on rank 1" in r.stderr
