@@ -106,7 +106,8 @@ struct WaveRunner {
     const i64 hp;  // h * pitch
     const uint2* ld;
     uint2* st;
-    int lrow;     // tile row of the next load (WRAPY only)
+    i64 st_stride;  // pitch for output lanes, 0 for halo/idle lanes (they write a trash slot)
+    int lrow;       // tile row of the next load (WRAPY only)
     uint2 pf[3];
     Pipe<K> P;
 
@@ -125,7 +126,13 @@ struct WaveRunner {
         lrow = d.row0 - K;
         if (WRAPY && lrow < 0) lrow += p.h;
         ld = reinterpret_cast<const uint2*>(src + (i64)(lrow + p.R) * p.pitch + (d.col + 1));
-        st = reinterpret_cast<uint2*>(dst + (i64)(d.row0 + p.R) * p.pitch + (d.col + 1));
+        // Every lane stores every row (no branch: the row loop stays one basic block, so the
+        // scheduler can interleave consecutive rows).  Halo/idle lanes write their own column of the
+        // last slack row of the allocation (row h+R+3), which nothing reads.
+        const bool out = d.flags & LANE_STORE;
+        const i64 srow = out ? (i64)(d.row0 + p.R) : (i64)(p.h + 2 * p.R + 3);
+        st = reinterpret_cast<uint2*>(dst + srow * p.pitch + (d.col + 1));
+        st_stride = out ? p.pitch : 0;
         pf[0] = *ld;
         next_row();
         pf[1] = *ld;
@@ -142,8 +149,8 @@ struct WaveRunner {
         next_row();
         u32 lo = x.x, hi = x.y;
         if (!advance<K, PH, GUARD>(P, lo, hi, i)) return;
-        if (d.flags & LANE_STORE) *st = make_uint2(lo, hi);
-        st += p.pitch;
+        *st = make_uint2(lo, hi);
+        st += st_stride;
     }
 
     __device__ __forceinline__ void run() {
