@@ -40,6 +40,8 @@ struct StepParams {
 
 // Supported temporal depths (template instantiations).
 bool step_depth_supported(int k);
+// Resident 256-thread workgroups per CU of step_temporal<k> (occupancy query).
+int step_blocks_per_cu(int k, bool wrapy);
 int max_step_depth();
 // Launch K generations: src -> dst over the waves of `plan` (n_waves * 64 LaneDescs in device memory).
 void launch_step(int k, const u64* src, u64* dst, const LaneDesc* plan, i64 n_waves, const StepParams& p,

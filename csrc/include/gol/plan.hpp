@@ -61,4 +61,10 @@ std::vector<LaneDesc> build_plan(const std::vector<Region>& regions, i64 nw, i64
 // while keeping the 2k-row vertical halo overhead small.
 i64 choose_rows_per_chunk(const std::vector<Region>& regions, int k, i64 target_waves, i64 min_rows);
 
+// Occupancy-balanced segment height: the smallest S >= min_rows whose plan fits in ONE round of
+// `resident_waves` (every wave resident from the start, equal work, no straggler workgroups).
+// Time ~ rounds x (S + k), so one full round with the shortest segments is optimal.
+i64 balanced_rows_per_chunk(const std::vector<Region>& regions, i64 nw, i64 h, int k, i64 resident_waves,
+                            i64 min_rows, bool xwrap);
+
 }  // namespace gol

@@ -31,6 +31,28 @@ i64 choose_rows_per_chunk(const std::vector<Region>& regions, int k, i64 target_
     return std::max<i64>(1, std::min(s, max_rows));
 }
 
+i64 balanced_rows_per_chunk(const std::vector<Region>& regions, i64 nw, i64 h, int k, i64 resident_waves,
+                            i64 min_rows, bool xwrap) {
+    i64 max_rows = 1;
+    for (const Region& r : regions) max_rows = std::max(max_rows, r.r1 - r.r0);
+    auto waves = [&](i64 S) {
+        PlanStats st;
+        build_plan(regions, nw, h, S, k, xwrap, &st);
+        return st.waves;
+    };
+    i64 lo = std::max<i64>(1, std::min(min_rows, max_rows)), hi = max_rows;
+    if (waves(lo) <= resident_waves) return lo;
+    if (waves(hi) > resident_waves) return hi;  // cannot fit one round: fewest, tallest segments
+    while (hi - lo > 1) {  // waves(lo) > target >= waves(hi)
+        i64 mid = (lo + hi) / 2;
+        if (waves(mid) <= resident_waves)
+            hi = mid;
+        else
+            lo = mid;
+    }
+    return hi;
+}
+
 std::vector<LaneDesc> build_plan(const std::vector<Region>& regions, i64 nw, i64 h, i64 rows_per_chunk, int k,
                                  bool xwrap, PlanStats* stats) {
     if (rows_per_chunk < 1) rows_per_chunk = 1;

@@ -340,8 +340,13 @@ class HipEngine : public Engine {
         if (it != plans_.end()) return it->second;
         std::vector<Region> rg = regions(kind, k);
         DevPlan p;
-        i64 target = cfg_.waves_target > 0 ? cfg_.waves_target : (i64)cus_ * 8;
-        i64 rows = cfg_.rows_per_wave > 0 ? cfg_.rows_per_wave : choose_rows_per_chunk(rg, k, target, 4 * (i64)k);
+        i64 rows = cfg_.rows_per_wave;
+        if (rows <= 0 && cfg_.waves_target > 0) rows = choose_rows_per_chunk(rg, k, cfg_.waves_target, 4 * (i64)k);
+        if (rows <= 0) {
+            // one full round of resident waves (occupancy of this kernel instantiation)
+            const i64 resident = (i64)hipk::step_blocks_per_cu(k, step_flags() & hipk::STEP_WRAP_Y) * kWavesPerBlock * cus_;
+            rows = balanced_rows_per_chunk(rg, L_.nw, L_.h, k, resident, 2 * (i64)k, xwrap_by_plan());
+        }
         std::vector<LaneDesc> lanes = build_plan(rg, L_.nw, L_.h, rows, k, xwrap_by_plan(), &p.st);
         p.waves = (i64)lanes.size() / kWaveLanes;
         HIP_CHECK(hipMalloc(&p.d, lanes.size() * sizeof(LaneDesc)));

@@ -237,6 +237,24 @@ bool step_depth_supported(int k) {
 
 int max_step_depth() { return 16; }
 
+int step_blocks_per_cu(int k, bool wrapy) {
+    int nb = 0;
+    hipError_t e = hipErrorInvalidValue;
+    switch (k) {
+#define GOL_CASE(K)                                                                                       \
+    case K:                                                                                               \
+        e = wrapy ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, step_temporal<K, true>, 256, 0)    \
+                  : hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, step_temporal<K, false>, 256, 0);  \
+        break;
+        GOL_FOR_EACH_DEPTH(GOL_CASE)
+#undef GOL_CASE
+        default:
+            break;
+    }
+    if (e != hipSuccess || nb < 1) return 1;
+    return std::min(nb, 8);
+}
+
 void launch_step(int k, const u64* src, u64* dst, const LaneDesc* plan, i64 n_waves, const StepParams& p,
                  hipStream_t s) {
     const dim3 grid((unsigned)(n_waves / kWavesPerBlock)), block(256);
