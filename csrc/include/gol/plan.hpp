@@ -57,6 +57,9 @@ struct PlanStats {
 std::vector<LaneDesc> build_plan(const std::vector<Region>& regions, i64 nw, i64 h, i64 rows_per_chunk, int k,
                                  bool xwrap, PlanStats* stats = nullptr);
 
+// Number of waves (padded to whole workgroups) of the plan, without materialising lanes.
+i64 plan_waves(const std::vector<Region>& regions, i64 nw, i64 h, i64 rows_per_chunk);
+
 // Pick a segment height so that the sweep has enough waves to fill the GPU (about `target_waves`)
 // while keeping the 2k-row vertical halo overhead small.
 i64 choose_rows_per_chunk(const std::vector<Region>& regions, int k, i64 target_waves, i64 min_rows);

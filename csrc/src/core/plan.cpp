@@ -35,11 +35,9 @@ i64 balanced_rows_per_chunk(const std::vector<Region>& regions, i64 nw, i64 h, i
                             i64 min_rows, bool xwrap) {
     i64 max_rows = 1;
     for (const Region& r : regions) max_rows = std::max(max_rows, r.r1 - r.r0);
-    auto waves = [&](i64 S) {
-        PlanStats st;
-        build_plan(regions, nw, h, S, k, xwrap, &st);
-        return st.waves;
-    };
+    (void)k;
+    (void)xwrap;
+    auto waves = [&](i64 S) { return plan_waves(regions, nw, h, S); };
     i64 lo = std::max<i64>(1, std::min(min_rows, max_rows)), hi = max_rows;
     if (waves(lo) <= resident_waves) return lo;
     if (waves(hi) > resident_waves) return hi;  // cannot fit one round: fewest, tallest segments
@@ -53,10 +51,13 @@ i64 balanced_rows_per_chunk(const std::vector<Region>& regions, i64 nw, i64 h, i
     return hi;
 }
 
-std::vector<LaneDesc> build_plan(const std::vector<Region>& regions, i64 nw, i64 h, i64 rows_per_chunk, int k,
-                                 bool xwrap, PlanStats* stats) {
+namespace {
+
+// Cut the regions into segments of <= rows_per_chunk rows x <= 62 words and pack them into waves:
+// full-width segments get a wave each; narrow ones (same height) are packed first-fit-decreasing.
+std::vector<std::vector<Item>> pack_waves(const std::vector<Region>& regions, i64 nw, i64 h, i64 rows_per_chunk) {
     if (rows_per_chunk < 1) rows_per_chunk = 1;
-    std::vector<Item> items;
+    std::map<i64, std::vector<Item>> by_rows;
     for (const Region& rg : regions) {
         i64 rows = rg.r1 - rg.r0, words = rg.c1 - rg.c0;
         if (rows <= 0 || words <= 0) continue;
@@ -66,22 +67,15 @@ std::vector<LaneDesc> build_plan(const std::vector<Region>& regions, i64 nw, i64
         i64 r = rg.r0;
         for (i64 ch = 0; ch < nch; ++ch) {
             i64 nr = base + (ch < extra ? 1 : 0);
-            for (i64 c = rg.c0; c < rg.c1; c += kSegWords) {
-                items.push_back({r, nr, c, std::min<i64>(kSegWords, rg.c1 - c)});
-            }
+            for (i64 c = rg.c0; c < rg.c1; c += kSegWords)
+                by_rows[nr].push_back({r, nr, c, std::min<i64>(kSegWords, rg.c1 - c)});
             r += nr;
         }
     }
-
-    // Group by height; full-width segments get a wave each, narrow ones are packed first-fit.
-    std::map<i64, std::vector<Item>> by_rows;
-    for (const Item& it : items) by_rows[it.nrows].push_back(it);
-
     std::vector<std::vector<Item>> waves;
     for (auto& kv : by_rows) {
-        std::vector<Item>& v = kv.second;
         std::vector<Item> narrow;
-        for (const Item& it : v) {
+        for (const Item& it : kv.second) {
             if (it.lanes() == kWaveLanes)
                 waves.push_back({it});
             else
@@ -90,9 +84,11 @@ std::vector<LaneDesc> build_plan(const std::vector<Region>& regions, i64 nw, i64
         std::stable_sort(narrow.begin(), narrow.end(),
                          [](const Item& a, const Item& b) { return a.lanes() > b.lanes(); });
         std::vector<std::pair<int, std::vector<Item>>> open;  // used lanes, items
+        size_t first_open = 0;  // waves before this index are full (< 3 free lanes)
         for (const Item& it : narrow) {
             bool placed = false;
-            for (auto& w : open) {
+            for (size_t j = first_open; j < open.size(); ++j) {
+                auto& w = open[j];
                 if (w.first + it.lanes() <= kWaveLanes) {
                     w.first += it.lanes();
                     w.second.push_back(it);
@@ -101,10 +97,22 @@ std::vector<LaneDesc> build_plan(const std::vector<Region>& regions, i64 nw, i64
                 }
             }
             if (!placed) open.push_back({it.lanes(), {it}});
+            while (first_open < open.size() && open[first_open].first > kWaveLanes - 3) ++first_open;
         }
         for (auto& w : open) waves.push_back(std::move(w.second));
     }
+    return waves;
+}
 
+}  // namespace
+
+i64 plan_waves(const std::vector<Region>& regions, i64 nw, i64 h, i64 rows_per_chunk) {
+    return round_up(std::max<i64>(1, (i64)pack_waves(regions, nw, h, rows_per_chunk).size()), kWavesPerBlock);
+}
+
+std::vector<LaneDesc> build_plan(const std::vector<Region>& regions, i64 nw, i64 h, i64 rows_per_chunk, int k,
+                                 bool xwrap, PlanStats* stats) {
+    std::vector<std::vector<Item>> waves = pack_waves(regions, nw, h, rows_per_chunk);
     i64 nwaves = round_up(std::max<i64>(1, (i64)waves.size()), kWavesPerBlock);
     std::vector<LaneDesc> lanes((size_t)(nwaves * kWaveLanes));
     PlanStats st;

@@ -205,8 +205,10 @@ class HipEngine : public Engine {
         HIP_CHECK(hipEventRecord(ev_ready_, s_comp_));
         synchronize();
         if (dcells) HIP_CHECK(hipFree(dcells));
-        // Build the plans for the common depths now, so graph capture never allocates.
-        prepare(cfg_.compat ? 1 : L_.R);
+        // Build the plans for every depth a run can use (remainder supersteps included) now, so
+        // neither graph capture nor a timed loop ever builds or uploads a plan.
+        for (int k = 1; k <= (cfg_.compat ? 1 : L_.R); ++k)
+            if (supported_depth(k) == k) prepare(k);
         const DevPlan& fp = plan(0, cfg_.compat ? 1 : L_.R);
         stats_.plan_waves = fp.waves;
         stats_.lane_efficiency =
