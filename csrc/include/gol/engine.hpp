@@ -38,6 +38,7 @@ struct EngineConfig {
     i64 rows_per_wave = 0;            // plan segment height override (0 = auto)
     int waves_target = 0;             // plan wave-count target (0 = auto)
     std::string kernel = "temporal";  // temporal | lds
+    std::string prefetch = "lds";     // temporal kernel row prefetch: lds (DMA ring) | reg
     std::string transport = "auto";   // auto | device | host  (host = stage halos through host memory)
     bool profile = false;             // per-phase event timing
     int graph_supersteps = 0;         // supersteps per captured graph (0 = auto, even)

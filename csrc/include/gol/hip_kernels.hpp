@@ -28,7 +28,14 @@ enum : u32 {
     STEP_WRAP_X = 1u << 0,  // LDS kernel: tile is its own E/W neighbour (w % 64 == 0); the temporal
                             // kernel gets x-wrap from its plan (build_plan(..., xwrap = true))
     STEP_WRAP_Y = 1u << 1,  // tile is its own N/S neighbour: rows are read modulo h, no ghost rows
+    STEP_PF_LDS = 1u << 2,  // temporal kernel: prefetch rows through a per-wave LDS ring (DMA)
 };
+
+// Rows the HIP engine allocates past the bottom halo: prefetch overrun + the trash row the
+// temporal kernel's halo lanes store into.
+constexpr int kSlackRows = 16;
+// Per-wave LDS prefetch ring depth (rows) of the temporal kernel.
+constexpr int kRingRows = 10;
 
 struct StepParams {
     i64 pitch;
@@ -40,8 +47,8 @@ struct StepParams {
 
 // Supported temporal depths (template instantiations).
 bool step_depth_supported(int k);
-// Resident 256-thread workgroups per CU of step_temporal<k> (occupancy query).
-int step_blocks_per_cu(int k, bool wrapy);
+// Resident 256-thread workgroups per CU of step_temporal<k> for the given STEP_* flags.
+int step_blocks_per_cu(int k, u32 flags);
 int max_step_depth();
 // Launch K generations: src -> dst over the waves of `plan` (n_waves * 64 LaneDescs in device memory).
 void launch_step(int k, const u64* src, u64* dst, const LaneDesc* plan, i64 n_waves, const StepParams& p,

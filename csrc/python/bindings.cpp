@@ -234,6 +234,7 @@ PYBIND11_MODULE(_gol, m) {
         .def_readwrite("rows_per_wave", &EngineConfig::rows_per_wave)
         .def_readwrite("waves_target", &EngineConfig::waves_target)
         .def_readwrite("kernel", &EngineConfig::kernel)
+        .def_readwrite("prefetch", &EngineConfig::prefetch)
         .def_readwrite("transport", &EngineConfig::transport)
         .def_readwrite("profile", &EngineConfig::profile)
         .def_readwrite("graph_supersteps", &EngineConfig::graph_supersteps);

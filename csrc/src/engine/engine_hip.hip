@@ -68,7 +68,7 @@ class HipEngine : public Engine {
         if (R != L_.R) L_ = Layout(L_.h, L_.w, R);
         stats_.depth = R;
         // slack rows: the temporal kernel prefetches 3 rows past a segment's last input row
-        const size_t bytes = (size_t)(L_.words() + 4 * L_.pitch) * 8;
+        const size_t bytes = (size_t)(L_.words() + hipk::kSlackRows * L_.pitch) * 8;
         for (int i = 0; i < 2; ++i) {
             HIP_CHECK(hipMalloc(&buf_[i], bytes));
             HIP_CHECK(hipMemset(buf_[i], 0, bytes));
@@ -306,6 +306,7 @@ class HipEngine : public Engine {
         u32 f = 0;
         if (self_y() && !cfg_.compat) f |= hipk::STEP_WRAP_Y;
         if (xwrap_by_plan()) f |= hipk::STEP_WRAP_X;
+        if (cfg_.prefetch == "lds") f |= hipk::STEP_PF_LDS;
         return f;
     }
 
@@ -346,7 +347,7 @@ class HipEngine : public Engine {
         if (rows <= 0 && cfg_.waves_target > 0) rows = choose_rows_per_chunk(rg, k, cfg_.waves_target, 4 * (i64)k);
         if (rows <= 0) {
             // one full round of resident waves (occupancy of this kernel instantiation)
-            const i64 resident = (i64)hipk::step_blocks_per_cu(k, step_flags() & hipk::STEP_WRAP_Y) * kWavesPerBlock * cus_;
+            const i64 resident = (i64)hipk::step_blocks_per_cu(k, step_flags()) * kWavesPerBlock * cus_;
             rows = balanced_rows_per_chunk(rg, L_.nw, L_.h, k, resident, 2 * (i64)k, xwrap_by_plan());
         }
         std::vector<LaneDesc> lanes = build_plan(rg, L_.nw, L_.h, rows, k, xwrap_by_plan(), &p.st);

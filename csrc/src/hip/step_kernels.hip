@@ -98,17 +98,34 @@ __device__ __forceinline__ bool advance(Pipe<K>& P, u32& lo, u32& hi, int i) {
     return true;
 }
 
-template <int K, bool WRAPY>
+typedef __attribute__((address_space(3))) void lds_void_t;
+typedef __attribute__((address_space(1))) void glb_void_t;
+
+// Row prefetch.  PF_LDS: each wave owns a ring of kRingRows rows in LDS, filled by
+// global_load_lds_dword DMA (2 per row: lo / hi halves) kRingRows-1 rows ahead of use — deep
+// prefetch that costs no VGPRs.  The ring row for iteration i was issued at iteration i-kRingRows+1;
+// at least 2*kRingRows-4 vector-memory ops (DMAs, stores) were issued after it, so a counted
+// `s_waitcnt vmcnt(2*kRingRows-4)` retires it while the newer rows stay in flight.
+// PF_REG: a register triple prefetched one row-triple ahead, pinned above the compute with a
+// sched_barrier (otherwise the scheduler sinks the loads to the end of the loop body).
+enum { PF_REG = 0, PF_LDS = 1 };
+constexpr int kRingWait = 2 * kRingRows - 4;
+
+template <int K, bool WRAPY, int PF>
 struct WaveRunner {
     const StepParams& p;
     const LaneDesc& d;
-    const int n;  // input rows of the segment: nrows + 2K
+    const int n;   // input rows of the segment: nrows + 2K
     const i64 hp;  // h * pitch
     const uint2* ld;
     uint2* st;
     i64 st_stride;  // pitch for output lanes, 0 for halo/idle lanes (they write a trash slot)
     int lrow;       // tile row of the next load (WRAPY only)
-    uint2 pf[3];
+    uint2 pf[3];    // PF_REG
+    u32* ring;      // PF_LDS: kRingRows x {lo, hi} x 64 lanes
+    int slot;       // PF_LDS: ring slot of the next row to consume
+    int fill;       // PF_LDS: ring slot the next DMA writes
+    int lane;
     Pipe<K> P;
 
     __device__ __forceinline__ void next_row() {
@@ -121,36 +138,73 @@ struct WaveRunner {
         }
     }
 
-    __device__ __forceinline__ WaveRunner(const u64* src, u64* dst, const LaneDesc& d_, int nrows, const StepParams& p_)
-        : p(p_), d(d_), n(nrows + 2 * K), hp((i64)p_.h * p_.pitch) {
+    __device__ __forceinline__ void issue_dma() {
+        const u32* g = reinterpret_cast<const u32*>(ld);
+        u32* dst = ring + fill * 128;
+        __builtin_amdgcn_global_load_lds((glb_void_t*)g, (lds_void_t*)dst, 4, 0, 0);
+        __builtin_amdgcn_global_load_lds((glb_void_t*)(g + 1), (lds_void_t*)(dst + 64), 4, 0, 0);
+        fill = fill + 1 == kRingRows ? 0 : fill + 1;
+        next_row();
+    }
+
+    __device__ __forceinline__ WaveRunner(const u64* src, u64* dst, const LaneDesc& d_, int nrows,
+                                          const StepParams& p_, u32* ring_)
+        : p(p_), d(d_), n(nrows + 2 * K), hp((i64)p_.h * p_.pitch), ring(ring_), slot(0), fill(0) {
+        lane = threadIdx.x & 63;
         lrow = d.row0 - K;
         if (WRAPY && lrow < 0) lrow += p.h;
         ld = reinterpret_cast<const uint2*>(src + (i64)(lrow + p.R) * p.pitch + (d.col + 1));
         // Every lane stores every row (no branch: the row loop stays one basic block, so the
         // scheduler can interleave consecutive rows).  Halo/idle lanes write their own column of the
-        // last slack row of the allocation (row h+R+3), which nothing reads.
+        // last slack row of the allocation, which nothing reads.
         const bool out = d.flags & LANE_STORE;
-        const i64 srow = out ? (i64)(d.row0 + p.R) : (i64)(p.h + 2 * p.R + 3);
+        const i64 srow = out ? (i64)(d.row0 + p.R) : (i64)(p.h + 2 * p.R + kSlackRows - 1);
         st = reinterpret_cast<uint2*>(dst + srow * p.pitch + (d.col + 1));
         st_stride = out ? p.pitch : 0;
-        pf[0] = *ld;
-        next_row();
-        pf[1] = *ld;
-        next_row();
-        pf[2] = *ld;
-        next_row();
+        if (PF == PF_LDS) {
+            for (int j = 0; j < kRingRows - 1; ++j) issue_dma();
+        } else {
+            pf[0] = *ld;
+            next_row();
+            pf[1] = *ld;
+            next_row();
+            pf[2] = *ld;
+            next_row();
+        }
+    }
+
+    // Next input row (lo, hi) in order.
+    template <int PH>
+    __device__ __forceinline__ void fetch(u32& lo, u32& hi) {
+        if (PF == PF_LDS) {
+            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kRingWait) : "memory");
+            const u32* r = ring + slot * 128;
+            lo = r[lane];
+            hi = r[64 + lane];
+            slot = slot + 1 == kRingRows ? 0 : slot + 1;
+            issue_dma();  // refills the slot consumed by the previous row
+        } else {
+            const uint2 x = pf[PH];
+            pf[PH] = *ld;  // prefetch 3 rows ahead (the allocation has slack rows past the halo)
+            next_row();
+            lo = x.x;
+            hi = x.y;
+        }
+    }
+
+    template <int PH, bool GUARD>
+    __device__ __forceinline__ void compute_store(u32 lo, u32 hi, int i) {
+        if (!advance<K, PH, GUARD>(P, lo, hi, i)) return;
+        *st = make_uint2(lo, hi);
+        st += st_stride;
     }
 
     template <int PH, bool GUARD>
     __device__ __forceinline__ void body(int i) {
         if (GUARD && i >= n) return;
-        const uint2 x = pf[PH];
-        pf[PH] = *ld;  // prefetch 3 rows ahead (the allocation has slack rows past the halo)
-        next_row();
-        u32 lo = x.x, hi = x.y;
-        if (!advance<K, PH, GUARD>(P, lo, hi, i)) return;
-        *st = make_uint2(lo, hi);
-        st += st_stride;
+        u32 lo, hi;
+        fetch<PH>(lo, hi);
+        compute_store<PH, GUARD>(lo, hi, i);
     }
 
     __device__ __forceinline__ void run() {
@@ -162,25 +216,48 @@ struct WaveRunner {
             body<2, true>(i + 2);
         }
         for (; i + 3 <= n; i += 3) {
-            body<0, false>(i);
-            body<1, false>(i + 1);
-            body<2, false>(i + 2);
+            if (PF == PF_REG) {
+                // hoist the whole next triple's loads above this triple's compute
+                const uint2 x0 = pf[0], x1 = pf[1], x2 = pf[2];
+                pf[0] = *ld;
+                next_row();
+                pf[1] = *ld;
+                next_row();
+                pf[2] = *ld;
+                next_row();
+                __builtin_amdgcn_sched_barrier(0);
+                compute_store<0, false>(x0.x, x0.y, i);
+                compute_store<1, false>(x1.x, x1.y, i + 1);
+                compute_store<2, false>(x2.x, x2.y, i + 2);
+            } else {
+                body<0, false>(i);
+                body<1, false>(i + 1);
+                body<2, false>(i + 2);
+            }
         }
         if (i < n) body<0, false>(i);
         if (i + 1 < n) body<1, false>(i + 1);
+        if (PF == PF_LDS) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // drain DMAs before exit
     }
 };
 
-template <int K, bool WRAPY>
+template <int K, bool WRAPY, int PF>
 __global__ __launch_bounds__(256) void step_temporal(const u64* __restrict__ src, u64* __restrict__ dst,
                                                      const LaneDesc* __restrict__ plan, StepParams p) {
-    const i64 wave = (i64)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
+    const int wv = threadIdx.x >> 6;
+    const i64 wave = (i64)blockIdx.x * kWavesPerBlock + wv;
     const int lane = threadIdx.x & 63;
     const LaneDesc d = plan[wave * kWaveLanes + lane];
     const int nrows = __builtin_amdgcn_readfirstlane(d.nrows);
     if (nrows <= 0) return;  // padding wave (uniform)
-    WaveRunner<K, WRAPY> w(src, dst, d, nrows, p);
-    w.run();
+    if constexpr (PF == PF_LDS) {
+        __shared__ __attribute__((aligned(16))) u32 ring[kWavesPerBlock * kRingRows * 128];
+        WaveRunner<K, WRAPY, PF> w(src, dst, d, nrows, p, ring + wv * kRingRows * 128);
+        w.run();
+    } else {
+        WaveRunner<K, WRAPY, PF> w(src, dst, d, nrows, p, nullptr);
+        w.run();
+    }
 }
 
 // ------------------------------------------------------------------------------------------
@@ -237,14 +314,23 @@ bool step_depth_supported(int k) {
 
 int max_step_depth() { return 16; }
 
-int step_blocks_per_cu(int k, bool wrapy) {
+template <int K>
+hipError_t occupancy(int* nb, bool wrapy, bool lds) {
+    if (lds)
+        return wrapy ? hipOccupancyMaxActiveBlocksPerMultiprocessor(nb, step_temporal<K, true, PF_LDS>, 256, 0)
+                     : hipOccupancyMaxActiveBlocksPerMultiprocessor(nb, step_temporal<K, false, PF_LDS>, 256, 0);
+    return wrapy ? hipOccupancyMaxActiveBlocksPerMultiprocessor(nb, step_temporal<K, true, PF_REG>, 256, 0)
+                 : hipOccupancyMaxActiveBlocksPerMultiprocessor(nb, step_temporal<K, false, PF_REG>, 256, 0);
+}
+
+int step_blocks_per_cu(int k, u32 flags) {
     int nb = 0;
     hipError_t e = hipErrorInvalidValue;
+    const bool wrapy = flags & STEP_WRAP_Y, lds = flags & STEP_PF_LDS;
     switch (k) {
-#define GOL_CASE(K)                                                                                       \
-    case K:                                                                                               \
-        e = wrapy ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, step_temporal<K, true>, 256, 0)    \
-                  : hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, step_temporal<K, false>, 256, 0);  \
+#define GOL_CASE(K)                          \
+    case K:                                  \
+        e = occupancy<K>(&nb, wrapy, lds);   \
         break;
         GOL_FOR_EACH_DEPTH(GOL_CASE)
 #undef GOL_CASE
@@ -258,14 +344,18 @@ int step_blocks_per_cu(int k, bool wrapy) {
 void launch_step(int k, const u64* src, u64* dst, const LaneDesc* plan, i64 n_waves, const StepParams& p,
                  hipStream_t s) {
     const dim3 grid((unsigned)(n_waves / kWavesPerBlock)), block(256);
-    const bool wy = p.flags & STEP_WRAP_Y;
+    const bool wy = p.flags & STEP_WRAP_Y, lds = p.flags & STEP_PF_LDS;
     switch (k) {
-#define GOL_CASE(K)                                                                          \
-    case K:                                                                                  \
-        if (wy)                                                                              \
-            hipLaunchKernelGGL((step_temporal<K, true>), grid, block, 0, s, src, dst, plan, p);  \
-        else                                                                                 \
-            hipLaunchKernelGGL((step_temporal<K, false>), grid, block, 0, s, src, dst, plan, p); \
+#define GOL_CASE(K)                                                                                     \
+    case K:                                                                                             \
+        if (wy && lds)                                                                                  \
+            hipLaunchKernelGGL((step_temporal<K, true, PF_LDS>), grid, block, 0, s, src, dst, plan, p);  \
+        else if (wy)                                                                                    \
+            hipLaunchKernelGGL((step_temporal<K, true, PF_REG>), grid, block, 0, s, src, dst, plan, p);  \
+        else if (lds)                                                                                   \
+            hipLaunchKernelGGL((step_temporal<K, false, PF_LDS>), grid, block, 0, s, src, dst, plan, p); \
+        else                                                                                            \
+            hipLaunchKernelGGL((step_temporal<K, false, PF_REG>), grid, block, 0, s, src, dst, plan, p); \
         break;
         GOL_FOR_EACH_DEPTH(GOL_CASE)
 #undef GOL_CASE

@@ -119,6 +119,7 @@ EngineConfig engine_config(const Options& o, const std::string& backend, int dev
     c.rows_per_wave = o.rows_per_wave;
     c.waves_target = o.waves_target;
     c.kernel = env_str("GOL_KERNEL", "temporal");
+    c.prefetch = env_str("GOL_PREFETCH", "lds");
     c.transport = o.transport == "rccl" ? "device" : o.transport;
     c.profile = o.profile;
     c.graph_supersteps = (int)env_int("GOL_GRAPH_SUPERSTEPS", 0);

@@ -77,6 +77,7 @@ class Simulation:
         compat: bool = False,
         device: Optional[int] = None,
         kernel: str = "temporal",
+        prefetch: str = os.environ.get("GOL_PREFETCH", "lds"),
         rows_per_wave: int = 0,
         waves_target: int = 0,
         profile: bool = False,
@@ -93,6 +94,7 @@ class Simulation:
         cfg.graph = graph
         cfg.compat = compat
         cfg.kernel = kernel
+        cfg.prefetch = prefetch
         cfg.rows_per_wave = rows_per_wave
         cfg.waves_target = waves_target
         cfg.profile = profile
