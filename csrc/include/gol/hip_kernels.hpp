@@ -29,11 +29,12 @@ enum : u32 {
                             // kernel gets x-wrap from its plan (build_plan(..., xwrap = true))
     STEP_WRAP_Y = 1u << 1,  // tile is its own N/S neighbour: rows are read modulo h, no ghost rows
     STEP_PF_LDS = 1u << 2,  // temporal kernel: prefetch rows through a per-wave LDS ring (DMA)
+    STEP_SKEW = 1u << 3,    // temporal kernel: skewed level pipeline (K independent chains per row)
 };
 
-// Rows the HIP engine allocates past the bottom halo: prefetch overrun + the trash row the
-// temporal kernel's halo lanes store into.
-constexpr int kSlackRows = 16;
+// Rows the HIP engine allocates past the bottom halo: prefetch / flush overrun (skewed pipeline:
+// K-1 rows, LDS ring: kRingRows-1 rows) + the trash row the temporal kernel's halo lanes store into.
+constexpr int kSlackRows = 32;
 // Per-wave LDS prefetch ring depth (rows) of the temporal kernel.
 constexpr int kRingRows = 10;
 

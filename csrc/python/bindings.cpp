@@ -235,6 +235,7 @@ PYBIND11_MODULE(_gol, m) {
         .def_readwrite("waves_target", &EngineConfig::waves_target)
         .def_readwrite("kernel", &EngineConfig::kernel)
         .def_readwrite("prefetch", &EngineConfig::prefetch)
+        .def_readwrite("pipeline", &EngineConfig::pipeline)
         .def_readwrite("transport", &EngineConfig::transport)
         .def_readwrite("profile", &EngineConfig::profile)
         .def_readwrite("graph_supersteps", &EngineConfig::graph_supersteps);

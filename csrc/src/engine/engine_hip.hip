@@ -307,6 +307,7 @@ class HipEngine : public Engine {
         if (self_y() && !cfg_.compat) f |= hipk::STEP_WRAP_Y;
         if (xwrap_by_plan()) f |= hipk::STEP_WRAP_X;
         if (cfg_.prefetch == "lds") f |= hipk::STEP_PF_LDS;
+        if (cfg_.pipeline == "skew") f |= hipk::STEP_SKEW;
         return f;
     }
 

@@ -98,6 +98,52 @@ __device__ __forceinline__ bool advance(Pipe<K>& P, u32& lo, u32& hi, int i) {
     return true;
 }
 
+// Skewed pipeline: level l consumes the row level l-1 produced in the PREVIOUS iteration (held in
+// dl/dh), so the K levels of one iteration are independent dependency chains the scheduler can
+// interleave (K-way ILP instead of one K-deep chain of DPP -> alignbit -> bitop3 steps).  Level l
+// receives input index i-2l at iteration i and emits index i-2l-1; the last level emits index
+// i-2K+1, i.e. the pipeline is K-1 rows longer than the unskewed one.  Garbage entering a level
+// before its first valid row only reaches output indices outside the valid range, so no guards
+// are needed — the caller just does not store the first 3K-1 outputs.
+template <int K>
+struct SkewPipe : Pipe<K> {
+    u32 dl[K], dh[K];  // dl[l], dh[l]: input of level l (l >= 1) for the current iteration
+};
+
+template <int K, int PH>
+__device__ __forceinline__ void advance_skew(SkewPipe<K>& P, u32& lo, u32& hi) {
+    constexpr int s = PH, sp = (PH + 2) % 3, spp = (PH + 1) % 3;
+    u32 out_lo = 0, out_hi = 0;
+#pragma unroll
+    for (int l = K - 1; l >= 0; --l) {
+        const u32 a = l ? P.dl[l] : lo, b = l ? P.dh[l] : hi;
+        const u32 ph = dpp_prev(b), nl = dpp_next(a);
+        const u32 L0 = __builtin_amdgcn_alignbit(a, ph, 31);
+        const u32 L1 = __builtin_amdgcn_alignbit(b, a, 31);
+        const u32 R0 = __builtin_amdgcn_alignbit(b, a, 1);
+        const u32 R1 = __builtin_amdgcn_alignbit(nl, b, 1);
+        P.s0[l][s][0] = b3<kLutXor3>(L0, a, R0);
+        P.s1[l][s][0] = b3<kLutMaj>(L0, a, R0);
+        P.s0[l][s][1] = b3<kLutXor3>(L1, b, R1);
+        P.s1[l][s][1] = b3<kLutMaj>(L1, b, R1);
+        P.x[l][s][0] = a;
+        P.x[l][s][1] = b;
+        const u32 o_lo = rule32(P.s0[l][spp][0], P.s1[l][spp][0], P.s0[l][sp][0], P.s1[l][sp][0], P.s0[l][s][0],
+                                P.s1[l][s][0], P.x[l][sp][0]);
+        const u32 o_hi = rule32(P.s0[l][spp][1], P.s1[l][spp][1], P.s0[l][sp][1], P.s1[l][sp][1], P.s0[l][s][1],
+                                P.s1[l][s][1], P.x[l][sp][1]);
+        if (l == K - 1) {
+            out_lo = o_lo;
+            out_hi = o_hi;
+        } else {
+            P.dl[l + 1] = o_lo;
+            P.dh[l + 1] = o_hi;
+        }
+    }
+    lo = out_lo;
+    hi = out_hi;
+}
+
 typedef __attribute__((address_space(3))) void lds_void_t;
 typedef __attribute__((address_space(1))) void glb_void_t;
 
@@ -111,11 +157,13 @@ typedef __attribute__((address_space(1))) void glb_void_t;
 enum { PF_REG = 0, PF_LDS = 1 };
 constexpr int kRingWait = 2 * kRingRows - 4;
 
-template <int K, bool WRAPY, int PF>
+template <int K, bool WRAPY, int MODE>
 struct WaveRunner {
+    static constexpr int PF = MODE & 1;                // PF_REG | PF_LDS
+    static constexpr bool SKEW = (MODE & 2) != 0;     // skewed (ILP) level pipeline
     const StepParams& p;
     const LaneDesc& d;
-    const int n;   // input rows of the segment: nrows + 2K
+    const int n;   // row iterations: nrows + 2K (+ K-1 flush rows when skewed)
     const i64 hp;  // h * pitch
     const uint2* ld;
     uint2* st;
@@ -126,7 +174,7 @@ struct WaveRunner {
     int slot;       // PF_LDS: ring slot of the next row to consume
     int fill;       // PF_LDS: ring slot the next DMA writes
     int lane;
-    Pipe<K> P;
+    std::conditional_t<SKEW, SkewPipe<K>, Pipe<K>> P;
 
     __device__ __forceinline__ void next_row() {
         ld += p.pitch;
@@ -149,7 +197,7 @@ struct WaveRunner {
 
     __device__ __forceinline__ WaveRunner(const u64* src, u64* dst, const LaneDesc& d_, int nrows,
                                           const StepParams& p_, u32* ring_)
-        : p(p_), d(d_), n(nrows + 2 * K), hp((i64)p_.h * p_.pitch), ring(ring_), slot(0), fill(0) {
+        : p(p_), d(d_), n(nrows + (SKEW ? 3 * K - 1 : 2 * K)), hp((i64)p_.h * p_.pitch), ring(ring_), slot(0), fill(0) {
         lane = threadIdx.x & 63;
         lrow = d.row0 - K;
         if (WRAPY && lrow < 0) lrow += p.h;
@@ -194,7 +242,12 @@ struct WaveRunner {
 
     template <int PH, bool GUARD>
     __device__ __forceinline__ void compute_store(u32 lo, u32 hi, int i) {
-        if (!advance<K, PH, GUARD>(P, lo, hi, i)) return;
+        if constexpr (SKEW) {
+            advance_skew<K, PH>(P, lo, hi);
+            if (GUARD && i < 3 * K - 1) return;  // outputs before the first valid row
+        } else {
+            if (!advance<K, PH, GUARD>(P, lo, hi, i)) return;
+        }
         *st = make_uint2(lo, hi);
         st += st_stride;
     }
@@ -208,7 +261,8 @@ struct WaveRunner {
     }
 
     __device__ __forceinline__ void run() {
-        constexpr int i0 = ((2 * K + 2) / 3) * 3;  // first multiple of 3 >= 2K: pipeline full
+        // first multiple of 3 at which the pipeline is full (2K rows; 3K-1 when skewed)
+        constexpr int i0 = SKEW ? 3 * K : ((2 * K + 2) / 3) * 3;
         int i = 0;
         for (; i < i0; i += 3) {
             body<0, true>(i);
@@ -241,7 +295,8 @@ struct WaveRunner {
     }
 };
 
-template <int K, bool WRAPY, int PF>
+// MODE bit 0: PF_LDS prefetch ring; bit 1: skewed level pipeline.
+template <int K, bool WRAPY, int MODE>
 __global__ __launch_bounds__(256) void step_temporal(const u64* __restrict__ src, u64* __restrict__ dst,
                                                      const LaneDesc* __restrict__ plan, StepParams p) {
     const int wv = threadIdx.x >> 6;
@@ -250,14 +305,34 @@ __global__ __launch_bounds__(256) void step_temporal(const u64* __restrict__ src
     const LaneDesc d = plan[wave * kWaveLanes + lane];
     const int nrows = __builtin_amdgcn_readfirstlane(d.nrows);
     if (nrows <= 0) return;  // padding wave (uniform)
-    if constexpr (PF == PF_LDS) {
+    if constexpr ((MODE & 1) == PF_LDS) {
         __shared__ __attribute__((aligned(16))) u32 ring[kWavesPerBlock * kRingRows * 128];
-        WaveRunner<K, WRAPY, PF> w(src, dst, d, nrows, p, ring + wv * kRingRows * 128);
+        WaveRunner<K, WRAPY, MODE> w(src, dst, d, nrows, p, ring + wv * kRingRows * 128);
         w.run();
     } else {
-        WaveRunner<K, WRAPY, PF> w(src, dst, d, nrows, p, nullptr);
+        WaveRunner<K, WRAPY, MODE> w(src, dst, d, nrows, p, nullptr);
         w.run();
     }
+}
+
+template <int K, bool WRAPY>
+const void* kernel_ptr(int mode) {
+    switch (mode & 3) {
+        case 0:
+            return (const void*)step_temporal<K, WRAPY, 0>;
+        case 1:
+            return (const void*)step_temporal<K, WRAPY, 1>;
+        case 2:
+            return (const void*)step_temporal<K, WRAPY, 2>;
+        default:
+            return (const void*)step_temporal<K, WRAPY, 3>;
+    }
+}
+
+template <int K>
+const void* kernel_for(u32 flags) {
+    const int mode = ((flags & STEP_PF_LDS) ? 1 : 0) | ((flags & STEP_SKEW) ? 2 : 0);
+    return (flags & STEP_WRAP_Y) ? kernel_ptr<K, true>(mode) : kernel_ptr<K, false>(mode);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -314,54 +389,34 @@ bool step_depth_supported(int k) {
 
 int max_step_depth() { return 16; }
 
-template <int K>
-hipError_t occupancy(int* nb, bool wrapy, bool lds) {
-    if (lds)
-        return wrapy ? hipOccupancyMaxActiveBlocksPerMultiprocessor(nb, step_temporal<K, true, PF_LDS>, 256, 0)
-                     : hipOccupancyMaxActiveBlocksPerMultiprocessor(nb, step_temporal<K, false, PF_LDS>, 256, 0);
-    return wrapy ? hipOccupancyMaxActiveBlocksPerMultiprocessor(nb, step_temporal<K, true, PF_REG>, 256, 0)
-                 : hipOccupancyMaxActiveBlocksPerMultiprocessor(nb, step_temporal<K, false, PF_REG>, 256, 0);
-}
-
-int step_blocks_per_cu(int k, u32 flags) {
-    int nb = 0;
-    hipError_t e = hipErrorInvalidValue;
-    const bool wrapy = flags & STEP_WRAP_Y, lds = flags & STEP_PF_LDS;
+static const void* kernel_of(int k, u32 flags) {
     switch (k) {
-#define GOL_CASE(K)                          \
-    case K:                                  \
-        e = occupancy<K>(&nb, wrapy, lds);   \
-        break;
+#define GOL_CASE(K) \
+    case K:         \
+        return kernel_for<K>(flags);
         GOL_FOR_EACH_DEPTH(GOL_CASE)
 #undef GOL_CASE
         default:
-            break;
+            return nullptr;
     }
-    if (e != hipSuccess || nb < 1) return 1;
+}
+
+int step_blocks_per_cu(int k, u32 flags) {
+    const void* f = kernel_of(k, flags);
+    int nb = 0;
+    if (!f || hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, f, 256, 0) != hipSuccess || nb < 1) return 1;
     return std::min(nb, 8);
 }
 
 void launch_step(int k, const u64* src, u64* dst, const LaneDesc* plan, i64 n_waves, const StepParams& p,
                  hipStream_t s) {
+    const void* f = kernel_of(k, p.flags);
+    if (!f) throw Error(strprintf("no step kernel instantiated for depth %d", k));
     const dim3 grid((unsigned)(n_waves / kWavesPerBlock)), block(256);
-    const bool wy = p.flags & STEP_WRAP_Y, lds = p.flags & STEP_PF_LDS;
-    switch (k) {
-#define GOL_CASE(K)                                                                                     \
-    case K:                                                                                             \
-        if (wy && lds)                                                                                  \
-            hipLaunchKernelGGL((step_temporal<K, true, PF_LDS>), grid, block, 0, s, src, dst, plan, p);  \
-        else if (wy)                                                                                    \
-            hipLaunchKernelGGL((step_temporal<K, true, PF_REG>), grid, block, 0, s, src, dst, plan, p);  \
-        else if (lds)                                                                                   \
-            hipLaunchKernelGGL((step_temporal<K, false, PF_LDS>), grid, block, 0, s, src, dst, plan, p); \
-        else                                                                                            \
-            hipLaunchKernelGGL((step_temporal<K, false, PF_REG>), grid, block, 0, s, src, dst, plan, p); \
-        break;
-        GOL_FOR_EACH_DEPTH(GOL_CASE)
-#undef GOL_CASE
-        default:
-            throw Error(strprintf("no step kernel instantiated for depth %d", k));
-    }
+    StepParams pp = p;
+    void* args[] = {(void*)&src, (void*)&dst, (void*)&plan, (void*)&pp};
+    hipError_t e = hipLaunchKernel(f, grid, block, args, 0, s);
+    if (e != hipSuccess) throw Error(strprintf("step kernel launch failed: %s", hipGetErrorString(e)));
 }
 
 void launch_step_lds(const u64* src, u64* dst, const Layout& L, i64 r0, i64 r1, u32 flags, hipStream_t s) {

@@ -78,6 +78,7 @@ class Simulation:
         device: Optional[int] = None,
         kernel: str = "temporal",
         prefetch: str = os.environ.get("GOL_PREFETCH", "lds"),
+        pipeline: str = os.environ.get("GOL_PIPELINE", "skew"),
         rows_per_wave: int = 0,
         waves_target: int = 0,
         profile: bool = False,
@@ -95,6 +96,7 @@ class Simulation:
         cfg.compat = compat
         cfg.kernel = kernel
         cfg.prefetch = prefetch
+        cfg.pipeline = pipeline
         cfg.rows_per_wave = rows_per_wave
         cfg.waves_target = waves_target
         cfg.profile = profile

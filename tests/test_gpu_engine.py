@@ -100,3 +100,13 @@ def test_naive_yardstick(gol):
     t, pop = gol.native.naive_byte_run(256, 10, 256, True, 0x5EED)
     assert t > 0
     assert pop == int(numpy_step(random_board(256, 256, 0x5EED), 10).sum())
+
+
+@pytest.mark.parametrize("pipeline", ["skew", "chain"])
+@pytest.mark.parametrize("prefetch", ["lds", "reg"])
+@pytest.mark.parametrize("depth", [1, 3, 8, 16])
+def test_kernel_variants(gol, pipeline, prefetch, depth):
+    N, gens = 700, 3 * depth + 5
+    s = _sim(gol, N, halo_depth=depth, pipeline=pipeline, prefetch=prefetch).init(5, seed=depth)
+    s.step(gens)
+    assert np.array_equal(s.board(), numpy_step(initial_board(5, N, 1, True, depth), gens))

@@ -1,0 +1,84 @@
+// Standalone timing harness for the temporal stencil kernel (single tile, periodic, balanced plan).
+// Used to A/B compiler flags / code variants of step_kernels.hip without rebuilding the framework:
+//   hipcc --offload-arch=gfx950 -O3 -Icsrc/include [variant flags] tools/kbench.cpp \
+//         csrc/src/hip/step_kernels.hip csrc/src/hip/aux_kernels.hip csrc/src/core/plan.cpp \
+//         csrc/src/core/geometry.cpp csrc/src/core/config.cpp -o build/kbench_<variant>
+//   build/kbench_<variant> [N=32768] [K=8] [gens=960] [pf=0|1]
+#include <hip/hip_runtime.h>
+
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+#include "gol/hip_kernels.hpp"
+#include "gol/plan.hpp"
+
+using namespace gol;
+
+#define CK(x)                                                                   \
+    do {                                                                        \
+        hipError_t e = (x);                                                     \
+        if (e != hipSuccess) {                                                  \
+            fprintf(stderr, "%s: %s\n", #x, hipGetErrorString(e));              \
+            exit(1);                                                            \
+        }                                                                       \
+    } while (0)
+
+int main(int argc, char** argv) {
+    const i64 N = argc > 1 ? atoll(argv[1]) : 32768;
+    const int K = argc > 2 ? atoi(argv[2]) : 8;
+    const int gens = argc > 3 ? atoi(argv[3]) : 960;
+    const int pf = argc > 4 ? atoi(argv[4]) : 0;
+    const int skew = argc > 5 ? atoi(argv[5]) : 0;
+    Layout L(N, N, K);
+    const size_t bytes = (size_t)(L.words() + hipk::kSlackRows * L.pitch) * 8;
+    u64 *a, *b;
+    CK(hipMalloc(&a, bytes));
+    CK(hipMalloc(&b, bytes));
+    CK(hipMemset(a, 0, bytes));
+    CK(hipMemset(b, 0, bytes));
+    hipk::InitParams ip{0, 0, L.nw, 0x5EED, 2};
+    hipk::launch_init_fill(a, L, ip, 0);
+    hipDeviceProp_t prop;
+    CK(hipGetDeviceProperties(&prop, 0));
+    const u32 flags = hipk::STEP_WRAP_Y | (pf ? hipk::STEP_PF_LDS : 0u) | (skew ? hipk::STEP_SKEW : 0u);
+    const i64 resident = (i64)hipk::step_blocks_per_cu(K, flags) * kWavesPerBlock * prop.multiProcessorCount;
+    std::vector<Region> rg = {{0, N, 0, L.nw}};
+    const i64 rows = balanced_rows_per_chunk(rg, L.nw, N, K, resident, 2 * K, true);
+    PlanStats st;
+    std::vector<LaneDesc> lanes = build_plan(rg, L.nw, N, rows, K, true, &st);
+    LaneDesc* dplan;
+    CK(hipMalloc(&dplan, lanes.size() * sizeof(LaneDesc)));
+    CK(hipMemcpy(dplan, lanes.data(), lanes.size() * sizeof(LaneDesc), hipMemcpyHostToDevice));
+    hipk::StepParams sp{L.pitch, (i32)L.h, (i32)L.nw, L.R, flags};
+    const int steps = gens / K;
+    for (int w = 0; w < 4; ++w) {
+        hipk::launch_step(K, a, b, dplan, st.waves, sp, 0);
+        std::swap(a, b);
+    }
+    CK(hipDeviceSynchronize());
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    float best = 1e30f;
+    for (int rep = 0; rep < 3; ++rep) {
+        CK(hipEventRecord(e0, 0));
+        for (int s = 0; s < steps; ++s) {
+            hipk::launch_step(K, a, b, dplan, st.waves, sp, 0);
+            std::swap(a, b);
+        }
+        CK(hipEventRecord(e1, 0));
+        CK(hipEventSynchronize(e1));
+        float ms = 0;
+        CK(hipEventElapsedTime(&ms, e0, e1));
+        if (ms < best) best = ms;
+    }
+    CK(hipGetLastError());
+    const double per_gen_us = best * 1e3 / (steps * K);
+    printf("{\"N\": %lld, \"K\": %d, \"skew\": %d, \"pf\": %d, \"rows\": %lld, \"waves\": %lld, \"blocks_per_cu\": %d, "
+           "\"us_per_gen\": %.3f, \"cells_per_s\": %.4e}\n",
+           (long long)N, K, skew, pf, (long long)rows, (long long)st.waves, hipk::step_blocks_per_cu(K, flags), per_gen_us,
+           (double)N * N / (per_gen_us * 1e-6));
+    return 0;
+}
