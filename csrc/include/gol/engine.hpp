@@ -38,8 +38,8 @@ struct EngineConfig {
     i64 rows_per_wave = 0;            // plan segment height override (0 = auto)
     int waves_target = 0;             // plan wave-count target (0 = auto)
     std::string kernel = "temporal";  // temporal | lds
-    std::string prefetch = "lds";     // temporal kernel row prefetch: lds (DMA ring) | reg
-    std::string pipeline = "skew";    // temporal kernel level pipeline: skew (ILP) | chain
+    std::string prefetch = "reg";     // temporal kernel row prefetch: reg (pinned triple) | lds (DMA ring)
+    std::string pipeline = "chain";   // temporal kernel level pipeline: chain | skew (ILP variant)
     std::string transport = "auto";   // auto | device | host  (host = stage halos through host memory)
     bool profile = false;             // per-phase event timing
     int graph_supersteps = 0;         // supersteps per captured graph (0 = auto, even)

@@ -119,8 +119,8 @@ EngineConfig engine_config(const Options& o, const std::string& backend, int dev
     c.rows_per_wave = o.rows_per_wave;
     c.waves_target = o.waves_target;
     c.kernel = env_str("GOL_KERNEL", "temporal");
-    c.prefetch = env_str("GOL_PREFETCH", "lds");
-    c.pipeline = env_str("GOL_PIPELINE", "skew");
+    c.prefetch = env_str("GOL_PREFETCH", "reg");
+    c.pipeline = env_str("GOL_PIPELINE", "chain");
     c.transport = o.transport == "rccl" ? "device" : o.transport;
     c.profile = o.profile;
     c.graph_supersteps = (int)env_int("GOL_GRAPH_SUPERSTEPS", 0);

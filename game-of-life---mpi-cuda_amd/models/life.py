@@ -77,8 +77,8 @@ class Simulation:
         compat: bool = False,
         device: Optional[int] = None,
         kernel: str = "temporal",
-        prefetch: str = os.environ.get("GOL_PREFETCH", "lds"),
-        pipeline: str = os.environ.get("GOL_PIPELINE", "skew"),
+        prefetch: str = os.environ.get("GOL_PREFETCH", "reg"),
+        pipeline: str = os.environ.get("GOL_PIPELINE", "chain"),
         rows_per_wave: int = 0,
         waves_target: int = 0,
         profile: bool = False,

@@ -26,6 +26,14 @@ __global__ void chain(unsigned* out, unsigned long long* cyc, int iters) {
                                "v_bitop3_b32 %4, %4, %6, %6 bitop3:0x96\n v_bitop3_b32 %5, %5, %6, %6 bitop3:0x96\n")
                          : "+v"(a), "+v"(b), "+v"(c), "+v"(d), "+v"(e), "+v"(f)
                          : "v"(a ^ 0x5a5a5a5au));
+        } else if (MODE == 6) {  // 4 independent bitop3 streams, all operands in VGPR bank 0
+            asm volatile(REP16("v_bitop3_b32 v40, v40, v44, v48 bitop3:0x96\n v_bitop3_b32 v52, v52, v56, v60 bitop3:0x96\n"
+                               "v_bitop3_b32 v64, v64, v68, v72 bitop3:0x96\n v_bitop3_b32 v76, v76, v80, v84 bitop3:0x96\n")
+                         ::: "v40", "v44", "v48", "v52", "v56", "v60", "v64", "v68", "v72", "v76", "v80", "v84");
+        } else if (MODE == 7) {  // 4 independent bitop3 streams, operands in banks 0,1,2
+            asm volatile(REP16("v_bitop3_b32 v40, v40, v41, v42 bitop3:0x96\n v_bitop3_b32 v52, v52, v53, v54 bitop3:0x96\n"
+                               "v_bitop3_b32 v64, v64, v65, v66 bitop3:0x96\n v_bitop3_b32 v76, v76, v77, v78 bitop3:0x96\n")
+                         ::: "v40", "v41", "v42", "v52", "v53", "v54", "v64", "v65", "v66", "v76", "v77", "v78");
         } else if (MODE == 5) {  // 6 independent dpp wave_shr streams
             asm volatile(REP16("v_mov_b32_dpp %0, %0 wave_shr:1 row_mask:0xf bank_mask:0xf\n"
                                "v_mov_b32_dpp %1, %1 wave_shr:1 row_mask:0xf bank_mask:0xf\n"
@@ -59,14 +67,15 @@ double run(int blocks, int threads, int iters, int per_iter) {
 int main() {
     const int it = 2000;
     const char* names[] = {"dep bitop3", "dep dpp wave_shr (+s_nop1)", "dep dpp row_shr (+s_nop1)", "dep alignbit",
-                           "6x indep bitop3", "6x indep dpp wave_shr"};
-    const int per[] = {16, 16, 16, 16, 96, 96};
+                           "6x indep bitop3", "6x indep dpp wave_shr", "4x indep bitop3 same bank", "4x indep bitop3 3 banks"};
+    const int per[] = {16, 16, 16, 16, 96, 96, 64, 64};
     for (int waves : {1, 2, 4}) {
         // one workgroup of `waves` x 4 waves -> `waves` waves per SIMD on one CU
         int threads = 256 * waves;
-        double r[6] = {run<0>(1, threads, it, per[0]), run<1>(1, threads, it, per[1]), run<2>(1, threads, it, per[2]),
-                       run<3>(1, threads, it, per[3]), run<4>(1, threads, it, per[4]), run<5>(1, threads, it, per[5])};
-        for (int m = 0; m < 6; ++m)
+        double r[8] = {run<0>(1, threads, it, per[0]), run<1>(1, threads, it, per[1]), run<2>(1, threads, it, per[2]),
+                       run<3>(1, threads, it, per[3]), run<4>(1, threads, it, per[4]), run<5>(1, threads, it, per[5]),
+                       run<6>(1, threads, it, per[6]), run<7>(1, threads, it, per[7])};
+        for (int m = 0; m < 8; ++m)
             printf("waves/SIMD=%d  %-28s %.2f cycles per instruction (wave 0 view)\n", waves, names[m], r[m]);
     }
     return 0;
