@@ -52,12 +52,56 @@ GOL_HD u64 bitop3_ref(u64 a, u64 b, u64 c, unsigned lut) {
     return r;
 }
 
-// Horizontal 3-sum of a 64-cell word given its neighbouring words in the row.
+// ---------------------------------------------------------------------------------------------
+// Storage format of a board word ("split"): the 64 cells of word c (columns 64c .. 64c+63) are
+// stored with the EVEN columns in bits 0..31 (column 64c+2j at bit j) and the ODD columns in bits
+// 32..63 (column 64c+2j+1 at bit 32+j).  An even cell's right neighbour is then the same bit of the
+// odd half and an odd cell's left neighbour the same bit of the even half, so each 32-bit half
+// needs ONE funnel shift for its horizontal neighbour sum instead of two.  Everything at word
+// granularity (halos, plans, exchange, ghost words) is format-agnostic; only bit-level I/O
+// (init, pattern cells, masks, dumps) converts with split_word / merge_word.
+// ---------------------------------------------------------------------------------------------
+
+GOL_HD u64 compact_even_bits(u64 x) {  // bits 0,2,4,.. -> 0..31
+    x &= 0x5555555555555555ull;
+    x = (x | (x >> 1)) & 0x3333333333333333ull;
+    x = (x | (x >> 2)) & 0x0F0F0F0F0F0F0F0Full;
+    x = (x | (x >> 4)) & 0x00FF00FF00FF00FFull;
+    x = (x | (x >> 8)) & 0x0000FFFF0000FFFFull;
+    x = (x | (x >> 16)) & 0x00000000FFFFFFFFull;
+    return x;
+}
+GOL_HD u64 spread_even_bits(u64 x) {  // bits 0..31 -> 0,2,4,..
+    x &= 0x00000000FFFFFFFFull;
+    x = (x | (x << 16)) & 0x0000FFFF0000FFFFull;
+    x = (x | (x << 8)) & 0x00FF00FF00FF00FFull;
+    x = (x | (x << 4)) & 0x0F0F0F0F0F0F0F0Full;
+    x = (x | (x << 2)) & 0x3333333333333333ull;
+    x = (x | (x << 1)) & 0x5555555555555555ull;
+    return x;
+}
+// natural (bit b = column 64c+b) -> split storage
+GOL_HD u64 split_word(u64 v) { return compact_even_bits(v) | (compact_even_bits(v >> 1) << 32); }
+// split storage -> natural
+GOL_HD u64 merge_word(u64 s) { return spread_even_bits(s) | (spread_even_bits(s >> 32) << 1); }
+// storage bit of column c within its word
+GOL_HD int storage_bit(i64 c) {
+    const int b = (int)(c & 63);
+    return (b & 1) ? 32 + (b >> 1) : (b >> 1);
+}
+// valid-cell mask of storage word c of a row of width w
+GOL_HD u64 storage_mask(i64 c, i64 w) { return split_word(word_mask(c, w)); }
+
+// Horizontal 3-sum (L + C + R, 2 bits per cell) of a split-format word given its row neighbours.
 GOL_HD void hsum64(u64 prev, u64 cur, u64 next, u64& s0, u64& s1) {
-    u64 L = (cur << 1) | (prev >> 63);
-    u64 R = (cur >> 1) | (next << 63);
-    s0 = L ^ cur ^ R;
-    s1 = (L & cur) | (L & R) | (cur & R);
+    const u32 lo = (u32)cur, hi = (u32)(cur >> 32);
+    const u32 prevhi = (u32)(prev >> 32), nextlo = (u32)next;
+    const u32 Le = (hi << 1) | (prevhi >> 31);  // even cells: left = odd half shifted, right = odd half
+    const u32 Ro = (lo >> 1) | (nextlo << 31);  // odd cells: left = even half, right = even half shifted
+    const u32 s0e = Le ^ lo ^ hi, s1e = (Le & lo) | (Le & hi) | (lo & hi);
+    const u32 s0o = lo ^ hi ^ Ro, s1o = (lo & hi) | (lo & Ro) | (hi & Ro);
+    s0 = (u64)s0e | ((u64)s0o << 32);
+    s1 = (u64)s1e | ((u64)s1o << 32);
 }
 
 // B3/S23 from three horizontal sums (rows above, centre, below) and the centre word.
@@ -71,18 +115,32 @@ GOL_HD u64 rule64(u64 a0, u64 a1, u64 b0, u64 b1, u64 c0, u64 c1, u64 x) {
     return (x0 & y1) | (~x0 & x & y2);
 }
 
-// Extract `n` (1..64) bits of a row starting at column s (no wrap; s + n <= row width).
-GOL_HD u64 extract_bits(const u64* row, i64 s, int n) {
+// Word accessors for the bit-level helpers below: natural words as stored, or split-format
+// storage words merged back to natural order on the fly.
+struct NaturalRow {
+    const u64* p;
+    GOL_HD u64 operator[](i64 i) const { return p[i]; }
+};
+struct SplitRow {
+    const u64* p;
+    GOL_HD u64 operator[](i64 i) const { return merge_word(p[i]); }
+};
+
+// Extract `n` (1..64) bits (natural order) of a row starting at column s (no wrap; s + n <= w).
+template <typename Row>
+GOL_HD u64 extract_bits(Row row, i64 s, int n) {
     i64 i = s >> 6;
     int off = (int)(s & 63);
     u64 v = row[i] >> off;
     if (off && off + n > 64) v |= row[i + 1] << (64 - off);
     return n >= 64 ? v : (v & ((1ull << n) - 1ull));
 }
+GOL_HD u64 extract_bits(const u64* row, i64 s, int n) { return extract_bits(NaturalRow{row}, s, n); }
 
-// 64 cells of a periodic row of width w starting at (any) column `start`, i.e. columns
-// start .. start+63 taken mod w.  Used to refresh the ghost bits of an x-periodic row.
-GOL_HD u64 wrap64(const u64* row, i64 w, i64 start) {
+// 64 cells (natural order) of a periodic row of width w starting at (any) column `start`, i.e.
+// columns start .. start+63 taken mod w.  Used to refresh the ghost bits of an x-periodic row.
+template <typename Row>
+GOL_HD u64 wrap64(Row row, i64 w, i64 start) {
     i64 s = start % w;
     if (s < 0) s += w;
     u64 res = 0;
@@ -96,9 +154,11 @@ GOL_HD u64 wrap64(const u64* row, i64 w, i64 start) {
     }
     return res;
 }
+GOL_HD u64 wrap64(const u64* row, i64 w, i64 start) { return wrap64(NaturalRow{row}, w, start); }
 
-// Ghost words of one x-periodic row.  `row` points at word 0 of the row; words -1 and nw are the
-// ghost words and bits >= w%64 of word nw-1 are ghost bits.  Only cells in [0, w) are read.
+// Ghost words of one x-periodic row in split storage.  `row` points at word 0 of the row; words
+// -1 and nw are the ghost words and columns >= w of word nw-1 are ghost cells.  Only cells in
+// [0, w) are read.  (Word-aligned widths are a pure word copy, independent of the format.)
 GOL_HD void wrap_row_ghosts(u64* row, i64 w, i64 nw) {
     int rem = (int)(w & 63);
     if (rem == 0) {
@@ -107,13 +167,14 @@ GOL_HD void wrap_row_ghosts(u64* row, i64 w, i64 nw) {
         row[nw] = first;
         return;
     }
-    u64 left = wrap64(row, w, -64);
-    u64 tail = wrap64(row, w, w);  // columns w, w+1, ... (placed from bit rem upwards)
-    u64 right = wrap64(row, w, 64 * nw);
+    const SplitRow src{row};
+    u64 left = wrap64(src, w, -64);
+    u64 tail = wrap64(src, w, w);  // columns w, w+1, ... (placed from bit rem upwards)
+    u64 right = wrap64(src, w, 64 * nw);
     u64 keep = (1ull << rem) - 1ull;
-    row[nw - 1] = (row[nw - 1] & keep) | (tail << rem);
-    row[-1] = left;
-    row[nw] = right;
+    row[nw - 1] = split_word((merge_word(row[nw - 1]) & keep) | (tail << rem));
+    row[-1] = split_word(left);
+    row[nw] = split_word(right);
 }
 
 // Fingerprint contribution of one (masked) word at global word index `gidx`.  The fingerprint is

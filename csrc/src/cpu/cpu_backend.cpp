@@ -65,27 +65,28 @@ void init_tile(u64* buf, const Layout& L, const Geometry& g, const PatternSpec& 
                 v = ~0ull;
             else if (p.fill == Fill::Random)
                 v = random_word(p.seed, g.row0 + r, gw0 + c, gwords);
-            row[c] = v & L.mask(c);
+            row[c] = split_word(v & L.mask(c));
         }
     }
     for (const auto& rc : p.cells) {
         i64 r = rc.first - g.row0, c = rc.second - g.col0;
         if (r < 0 || r >= L.h || c < 0 || c >= L.w) continue;
-        buf[L.index(r, c >> 6)] |= 1ull << (c & 63);
+        buf[L.index(r, c >> 6)] |= 1ull << storage_bit(c);
     }
 }
 
+// Board storage is split-format (bits.hpp); dense words are natural order.
 void extract_words(const u64* buf, const Layout& L, u64* dense) {
     for (i64 r = 0; r < L.h; ++r) {
         const u64* row = buf + L.index(r, 0);
-        for (i64 c = 0; c < L.nw; ++c) dense[r * L.nw + c] = row[c] & L.mask(c);
+        for (i64 c = 0; c < L.nw; ++c) dense[r * L.nw + c] = merge_word(row[c]) & L.mask(c);
     }
 }
 
 void insert_words(u64* buf, const Layout& L, const u64* dense) {
     for (i64 r = 0; r < L.h; ++r) {
         u64* row = buf + L.index(r, 0);
-        for (i64 c = 0; c < L.nw; ++c) row[c] = dense[r * L.nw + c] & L.mask(c);
+        for (i64 c = 0; c < L.nw; ++c) row[c] = split_word(dense[r * L.nw + c] & L.mask(c));
     }
 }
 
@@ -93,17 +94,18 @@ u64 population(const u64* buf, const Layout& L) {
     u64 n = 0;
     for (i64 r = 0; r < L.h; ++r) {
         const u64* row = buf + L.index(r, 0);
-        for (i64 c = 0; c < L.nw; ++c) n += (u64)__builtin_popcountll(row[c] & L.mask(c));
+        for (i64 c = 0; c < L.nw; ++c) n += (u64)__builtin_popcountll(row[c] & storage_mask(c, L.w));
     }
     return n;
 }
 
+// Defined on natural-order words, so it does not depend on the storage format.
 u64 fingerprint(const u64* buf, const Layout& L, i64 grow0, i64 gword0, i64 gwords) {
     u64 s = 0;
     for (i64 r = 0; r < L.h; ++r) {
         const u64* row = buf + L.index(r, 0);
         for (i64 c = 0; c < L.nw; ++c)
-            s += fingerprint_word((u64)(grow0 + r) * (u64)gwords + (u64)(gword0 + c), row[c] & L.mask(c));
+            s += fingerprint_word((u64)(grow0 + r) * (u64)gwords + (u64)(gword0 + c), merge_word(row[c]) & L.mask(c));
     }
     return s;
 }

@@ -12,6 +12,7 @@
 #include <cstring>
 #include <map>
 
+#include "gol/bits.hpp"
 #include "gol/engine.hpp"
 #include "gol/hip_kernels.hpp"
 
@@ -124,8 +125,12 @@ class HipEngine : public Engine {
         std::vector<u64> d((size_t)(L_.h * L_.nw));
         HIP_CHECK(hipMemcpy2D(d.data(), (size_t)L_.nw * 8, buf_[cur_] + L_.index(0, 0), (size_t)L_.pitch * 8,
                               (size_t)L_.nw * 8, (size_t)L_.h, hipMemcpyDeviceToHost));
-        if (L_.w % 64)
-            for (i64 r = 0; r < L_.h; ++r) d[(size_t)(r * L_.nw + L_.nw - 1)] &= L_.mask(L_.nw - 1);
+        // device storage is split-format (bits.hpp); the API is natural-order words
+        for (i64 r = 0; r < L_.h; ++r)
+            for (i64 c = 0; c < L_.nw; ++c) {
+                u64& x = d[(size_t)(r * L_.nw + c)];
+                x = merge_word(x) & L_.mask(c);
+            }
         return d;
     }
 
@@ -134,7 +139,10 @@ class HipEngine : public Engine {
         synchronize();
         std::vector<u64> m = dense;
         for (i64 r = 0; r < L_.h; ++r)
-            for (i64 c = 0; c < L_.nw; ++c) m[(size_t)(r * L_.nw + c)] &= L_.mask(c);
+            for (i64 c = 0; c < L_.nw; ++c) {
+                u64& x = m[(size_t)(r * L_.nw + c)];
+                x = split_word(x & L_.mask(c));
+            }
         HIP_CHECK(hipMemcpy2D(buf_[cur_] + L_.index(0, 0), (size_t)L_.pitch * 8, m.data(), (size_t)L_.nw * 8,
                               (size_t)L_.nw * 8, (size_t)L_.h, hipMemcpyHostToDevice));
         post(buf_[cur_], s_comp_);

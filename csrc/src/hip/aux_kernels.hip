@@ -21,7 +21,7 @@ __global__ void k_init_fill(u64* __restrict__ buf, i64 pitch, int R, i64 h, i64 
             v = ~0ull;
         else if (ip.fill == 2)
             v = random_word(ip.seed, ip.row0 + r, ip.gword0 + c, ip.gwords);
-        buf[(r + R) * pitch + c + 1] = v & word_mask(c, w);
+        buf[(r + R) * pitch + c + 1] = split_word(v & word_mask(c, w));  // split storage (bits.hpp)
     }
 }
 
@@ -29,7 +29,7 @@ __global__ void k_set_cells(u64* __restrict__ buf, i64 pitch, int R, const i64* 
     const i64 e = (i64)blockIdx.x * blockDim.x + threadIdx.x;
     if (e >= n) return;
     const i64 r = cells[2 * e], c = cells[2 * e + 1];
-    atomicOr((unsigned long long*)&buf[(r + R) * pitch + (c >> 6) + 1], 1ull << (c & 63));
+    atomicOr((unsigned long long*)&buf[(r + R) * pitch + (c >> 6) + 1], 1ull << storage_bit(c));
 }
 
 __global__ void k_fill_ghost_cols(u64* __restrict__ buf, i64 pitch, int R, i64 w, i64 nw, i64 r_lo, i64 r_hi) {
@@ -67,7 +67,7 @@ __global__ __launch_bounds__(256) void k_reduce_board(const u64* __restrict__ bu
     const i64 n = h * nw;
     for (i64 e = (i64)blockIdx.x * blockDim.x + threadIdx.x; e < n; e += (i64)gridDim.x * blockDim.x) {
         const i64 r = e / nw, c = e - r * nw;
-        const u64 v = buf[(r + R) * pitch + c + 1] & word_mask(c, w);
+        const u64 v = merge_word(buf[(r + R) * pitch + c + 1]) & word_mask(c, w);  // natural order
         pop += (u64)__popcll(v);
         fp += fingerprint_word((u64)(grow0 + r) * (u64)gwords + (u64)(gword0 + c), v);
     }

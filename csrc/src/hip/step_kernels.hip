@@ -4,14 +4,16 @@
 // reference gol-with-cuda.cu:189-262, which reads 9 bytes per cell per generation from global memory):
 //
 //  * 1 bit per cell, 64 cells per lane: each lane owns one u64 word column of the tile (two VGPRs,
-//    lo = cells 0..31, hi = cells 32..63) and streams DOWN the rows.  A wave64 covers 64 adjacent
-//    words = 4096 cells per row; the work plan (plan.hpp) packs segments of <= 62 output words plus
-//    one halo lane on each side into the 64 lanes.
-//  * Horizontal neighbours: the previous lane's hi word (v_mov_b32_dpp wave_shr:1) and the next
-//    lane's lo word (wave_shl:1), funnel-shifted in with v_alignbit_b32 — no LDS, no barriers.
+//    split storage: lo = the 32 even columns, hi = the 32 odd columns, bits.hpp) and streams DOWN
+//    the rows.  A wave64 covers 64 adjacent words = 4096 cells per row; the work plan (plan.hpp)
+//    packs segments of <= 62 output words plus one halo lane on each side into the 64 lanes.
+//  * Horizontal neighbours: with split storage an even cell's right neighbour and an odd cell's
+//    left neighbour are the same bit of the other half, so per 64 cells only two neighbour words
+//    are shifted: the previous lane's hi (v_mov_b32_dpp wave_shr:1) funnelled into hi, and the next
+//    lane's lo (wave_shl:1) funnelled into lo, one v_alignbit_b32 each — no LDS, no barriers.
 //  * Bit-sliced counting: per row the horizontal 3-sum (xor3 / maj = 1 v_bitop3 each), then the
-//    vertical 3-sum of those 2-bit sums and the rule in 8 more v_bitop3 (bits.hpp): 13 VALU ops per
-//    32 cells per generation.
+//    vertical 3-sum of those 2-bit sums and the rule in 8 more v_bitop3 (bits.hpp): 12 VALU ops per
+//    32 cells per generation (13 with natural bit order, which needs 4 funnel shifts per word).
 //  * Temporal blocking: K generation levels are chained in registers.  Level l keeps a 3-row
 //    window (horizontal sums of rows r-2, r-1 and its centre row); when a row arrives at level l it
 //    emits row r-1 of generation l+1 to level l+1.  One HBM pass = K generations, so the kernel is
@@ -60,6 +62,20 @@ __device__ __forceinline__ u32 rule32(u32 a0, u32 a1, u32 b0, u32 b1, u32 c0, u3
     return b3<kLutOut>(x0, y1, t);
 }
 
+// Horizontal 3-sums of one split-format word (bits.hpp: lo = even columns, hi = odd columns).
+// Even cell j: left = odd cell j-1 (hi shifted up one, bit 0 from the previous lane's hi), right =
+// odd cell j (hi).  Odd cell j: left = even cell j (lo), right = even cell j+1 (lo shifted down one,
+// bit 31 from the next lane's lo).  2 DPP + 2 funnel shifts + 4 bitop3 per 64 cells.
+__device__ __forceinline__ void hsum_split(u32 lo, u32 hi, u32& s0lo, u32& s1lo, u32& s0hi, u32& s1hi) {
+    const u32 ph = dpp_prev(hi), nl = dpp_next(lo);
+    const u32 Le = __builtin_amdgcn_alignbit(hi, ph, 31);  // (hi << 1) | (ph >> 31)
+    const u32 Ro = __builtin_amdgcn_alignbit(nl, lo, 1);   // (lo >> 1) | (nl << 31)
+    s0lo = b3<kLutXor3>(Le, lo, hi);
+    s1lo = b3<kLutMaj>(Le, lo, hi);
+    s0hi = b3<kLutXor3>(lo, hi, Ro);
+    s1hi = b3<kLutMaj>(lo, hi, Ro);
+}
+
 template <int K>
 struct Pipe {
     u32 s0[K][3][2];  // horizontal sum bit 0, per level, ring slot, half
@@ -78,15 +94,7 @@ __device__ __forceinline__ bool advance(Pipe<K>& P, u32& lo, u32& hi, int i) {
         const int s = (PH + l) % 3;     // slot of the arriving row
         const int sp = (s + 2) % 3;     // previous row (centre of the output)
         const int spp = (s + 1) % 3;    // two rows back
-        const u32 ph = dpp_prev(hi), nl = dpp_next(lo);
-        const u32 L0 = __builtin_amdgcn_alignbit(lo, ph, 31);
-        const u32 L1 = __builtin_amdgcn_alignbit(hi, lo, 31);
-        const u32 R0 = __builtin_amdgcn_alignbit(hi, lo, 1);
-        const u32 R1 = __builtin_amdgcn_alignbit(nl, hi, 1);
-        P.s0[l][s][0] = b3<kLutXor3>(L0, lo, R0);
-        P.s1[l][s][0] = b3<kLutMaj>(L0, lo, R0);
-        P.s0[l][s][1] = b3<kLutXor3>(L1, hi, R1);
-        P.s1[l][s][1] = b3<kLutMaj>(L1, hi, R1);
+        hsum_split(lo, hi, P.s0[l][s][0], P.s1[l][s][0], P.s0[l][s][1], P.s1[l][s][1]);
         P.x[l][s][0] = lo;
         P.x[l][s][1] = hi;
         if (GUARD && i < 2 * l + 2) return false;
@@ -117,15 +125,7 @@ __device__ __forceinline__ void advance_skew(SkewPipe<K>& P, u32& lo, u32& hi) {
 #pragma unroll
     for (int l = K - 1; l >= 0; --l) {
         const u32 a = l ? P.dl[l] : lo, b = l ? P.dh[l] : hi;
-        const u32 ph = dpp_prev(b), nl = dpp_next(a);
-        const u32 L0 = __builtin_amdgcn_alignbit(a, ph, 31);
-        const u32 L1 = __builtin_amdgcn_alignbit(b, a, 31);
-        const u32 R0 = __builtin_amdgcn_alignbit(b, a, 1);
-        const u32 R1 = __builtin_amdgcn_alignbit(nl, b, 1);
-        P.s0[l][s][0] = b3<kLutXor3>(L0, a, R0);
-        P.s1[l][s][0] = b3<kLutMaj>(L0, a, R0);
-        P.s0[l][s][1] = b3<kLutXor3>(L1, b, R1);
-        P.s1[l][s][1] = b3<kLutMaj>(L1, b, R1);
+        hsum_split(a, b, P.s0[l][s][0], P.s1[l][s][0], P.s0[l][s][1], P.s1[l][s][1]);
         P.x[l][s][0] = a;
         P.x[l][s][1] = b;
         const u32 o_lo = rule32(P.s0[l][spp][0], P.s1[l][spp][0], P.s0[l][sp][0], P.s1[l][sp][0], P.s0[l][s][0],

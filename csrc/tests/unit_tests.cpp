@@ -267,6 +267,40 @@ static void test_bits() {
     std::vector<u64> r5 = {0b10011ull};  // width 5: periodic 1 1 0 0 1
     u64 v = wrap64(r5.data(), 5, 5);
     CHECK((v & 0x3FF) == 0b1001110011ull);
+    // split storage: round trip, bit positions, and hsum64 vs a natural-order horizontal sum
+    u64 z = 0x9E3779B97F4A7C15ull;
+    for (int t = 0; t < 200; ++t) {
+        z = mix64(z + (u64)t);
+        CHECK(merge_word(split_word(z)) == z && split_word(merge_word(z)) == z);
+    }
+    for (int c = 0; c < 64; ++c) CHECK(split_word(1ull << c) == (1ull << storage_bit(c)));
+    CHECK(split_word(0x2ull) == (1ull << 32) && storage_mask(0, 3) == 0x100000003ull);
+    for (int t = 0; t < 100; ++t) {
+        const u64 p = mix64(3 * (u64)t + 1), c = mix64(3 * (u64)t + 2), n = mix64(3 * (u64)t + 3);
+        u64 s0, s1;
+        hsum64(split_word(p), split_word(c), split_word(n), s0, s1);
+        const u64 L = (c << 1) | (p >> 63), R = (c >> 1) | (n << 63);
+        CHECK(merge_word(s0) == (L ^ c ^ R) && merge_word(s1) == ((L & c) | (L & R) | (c & R)));
+    }
+    // ghost fill of an unaligned periodic row in split storage (width 70 = 2 words)
+    {
+        const i64 w = 70;
+        std::vector<u8> cells((size_t)w);
+        std::vector<u64> nat(2, 0);
+        for (i64 x = 0; x < w; ++x) {
+            cells[(size_t)x] = (u8)(mix64((u64)x) & 1);
+            if (cells[(size_t)x]) nat[(size_t)(x >> 6)] |= 1ull << (x & 63);
+        }
+        std::vector<u64> row = {0, split_word(nat[0]), split_word(nat[1]), 0};
+        wrap_row_ghosts(row.data() + 1, w, 2);
+        bool ok = true;
+        for (i64 x = -64; x < 128 + 64; ++x) {
+            const i64 word = x < 0 ? -1 : x >> 6;
+            const u64 bit = (merge_word(row[(size_t)(word + 1)]) >> (x & 63)) & 1;
+            ok = ok && bit == cells[(size_t)pmod(x, w)];
+        }
+        CHECK(ok);
+    }
 }
 
 int main() {
