@@ -25,6 +25,7 @@
 #include "gol/pattern.hpp"
 #include "gol/plan.hpp"
 #include "gol/transport.hpp"
+#include "gol/watchdog.hpp"
 
 namespace gol {
 
@@ -43,6 +44,7 @@ struct EngineConfig {
     std::string transport = "auto";   // auto | device | host  (host = stage halos through host memory)
     bool profile = false;             // per-phase event timing
     int graph_supersteps = 0;         // supersteps per captured graph (0 = auto, even)
+    double watchdog_s = 0;            // abort the job after this long without progress (0 = off)
 };
 
 struct EngineStats {
@@ -114,6 +116,20 @@ class Engine {
     virtual int supported_depth(int want) const { return want; }
     void setup_compat();
     void maybe_inject_fault();
+    // Watchdog mode: wait until earlier work has completed (bounded lookahead), polling the
+    // transport's asynchronous error state; then kick the watchdog.  No-op without a watchdog.
+    void progress(const char* next_phase);
+    virtual void fence() {}
+    [[noreturn]] void fatal(const std::string& what, int code);
+    struct Armed {  // arms the watchdog (if any) for the lifetime of a run() call
+        explicit Armed(Watchdog* w) : w_(w) {
+            if (w_) w_->arm(true);
+        }
+        ~Armed() {
+            if (w_) w_->arm(false);
+        }
+        Watchdog* w_;
+    };
 
     Geometry g_;
     EngineConfig cfg_;
@@ -122,6 +138,8 @@ class Engine {
     EngineStats stats_;
     u64 gen_ = 0;
     i64 fault_gen_ = -1;
+    std::string fault_mode_ = "abort";  // GOL_FAULT=rank:gen[:abort|hang|exit]
+    std::unique_ptr<Watchdog> wd_;
 };
 
 std::unique_ptr<Engine> make_cpu_engine(const Geometry& g, const EngineConfig& c, std::shared_ptr<Transport> t);

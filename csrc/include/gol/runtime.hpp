@@ -33,9 +33,11 @@ std::shared_ptr<Transport> make_control_transport(const LaunchInfo& li, int* arg
 // and throws ContractError with the reference's messages (gol-with-cuda.cu:290-300) on failure.
 std::string select_backend(const Options& o, int rank, int local_rank);
 
-// Wrap a control plane with RCCL when the backend is hip and P > 1 (unless GOL_TRANSPORT=host).
+// Wrap a control plane with RCCL when the backend is hip, P > 1 and every rank has its own GPU
+// (`device` must be current).  Ranks sharing a GPU, or GOL_TRANSPORT=host, stage halos through host
+// memory over the control plane instead.
 std::shared_ptr<Transport> make_data_transport(std::shared_ptr<Transport> control, const std::string& backend,
-                                               const Options& o);
+                                               const Options& o, int device);
 
 EngineConfig engine_config(const Options& o, const std::string& backend, int device);
 

@@ -64,6 +64,8 @@ class Transport {
     virtual void gatherv(const void* send, size_t n, std::vector<std::vector<u8>>* out, int root);
     // Fatal error on this rank: make every rank exit instead of hanging (reference Q11).
     [[noreturn]] virtual void abort(int code);
+    // Asynchronous failure of the data plane (e.g. ncclCommGetAsyncError); empty when healthy.
+    virtual std::string async_error() { return ""; }
 };
 
 // P = 1.

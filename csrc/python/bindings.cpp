@@ -238,7 +238,8 @@ PYBIND11_MODULE(_gol, m) {
         .def_readwrite("pipeline", &EngineConfig::pipeline)
         .def_readwrite("transport", &EngineConfig::transport)
         .def_readwrite("profile", &EngineConfig::profile)
-        .def_readwrite("graph_supersteps", &EngineConfig::graph_supersteps);
+        .def_readwrite("graph_supersteps", &EngineConfig::graph_supersteps)
+        .def_readwrite("watchdog_s", &EngineConfig::watchdog_s);
 
     py::class_<Engine>(m, "Engine")
         .def_static(

@@ -66,6 +66,13 @@ class RcclTransport : public Transport {
     void gatherv(const void* send, size_t n, std::vector<std::vector<u8>>* out, int root) override {
         ctl_->gatherv(send, n, out, root);
     }
+    std::string async_error() override {
+        if (!comm_) return "";
+        ncclResult_t st = ncclSuccess;
+        if (ncclCommGetAsyncError(comm_, &st) != ncclSuccess) return "ncclCommGetAsyncError failed";
+        if (st == ncclSuccess || st == ncclInProgress) return "";
+        return std::string("RCCL asynchronous error: ") + ncclGetErrorString(st);
+    }
     [[noreturn]] void abort(int code) override {
         if (comm_) ncclCommAbort(comm_);
         comm_ = nullptr;

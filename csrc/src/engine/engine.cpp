@@ -1,10 +1,15 @@
 // gol-mi355x: engine base (superstep loop, halo plan, compat mode, fault injection) + CPU backend.
 #include "gol/engine.hpp"
 
+#include <unistd.h>
+
 #include <algorithm>
+#include <chrono>
 #include <cstring>
+#include <thread>
 
 #include "gol/cpu.hpp"
+#include "gol/trace.hpp"
 
 namespace gol {
 
@@ -29,8 +34,33 @@ Engine::Engine(const Geometry& g, const EngineConfig& c, std::shared_ptr<Transpo
     if (!f.empty()) {
         int fr = -1;
         long long fg = -1;
-        if (sscanf(f.c_str(), "%d:%lld", &fr, &fg) == 2 && fr == g_.rank) fault_gen_ = fg;
+        char mode[16] = {0};
+        const int n = sscanf(f.c_str(), "%d:%lld:%15s", &fr, &fg, mode);
+        if (n >= 2 && fr == g_.rank) {
+            fault_gen_ = fg;
+            if (n == 3) fault_mode_ = mode;
+            if (fault_mode_ != "abort" && fault_mode_ != "hang" && fault_mode_ != "exit")
+                throw Error("GOL_FAULT mode must be abort, hang or exit (got '" + fault_mode_ + "')");
+        }
     }
+    if (cfg_.watchdog_s > 0) {
+        wd_ = std::make_unique<Watchdog>(cfg_.watchdog_s, [this](const std::string& what) {
+            fatal("watchdog: " + what, 4);
+        });
+    }
+}
+
+void Engine::fatal(const std::string& what, int code) {
+    fprintf(stderr, "[gol] rank %d, generation %llu: %s; aborting the job\n", g_.rank, (unsigned long long)gen_,
+            what.c_str());
+    t_->abort(code);
+    _exit(code);  // not reached: Transport::abort does not return
+}
+
+void Engine::progress(const char* next_phase) {
+    if (!wd_) return;
+    fence();
+    wd_->kick(next_phase);
 }
 
 std::unique_ptr<Engine> Engine::create(const Geometry& g, const EngineConfig& c, std::shared_ptr<Transport> t) {
@@ -77,6 +107,7 @@ std::vector<Engine::HaloItem> Engine::halo_items(int k) const {
 }
 
 void Engine::init(const PatternSpec& p) {
+    trace::Range range("gol.init");
     gen_ = 0;
     stats_ = EngineStats{};
     stats_.depth = L_.R;
@@ -107,21 +138,33 @@ void Engine::setup_compat() {
 
 void Engine::maybe_inject_fault() {
     if (fault_gen_ >= 0 && (i64)gen_ >= fault_gen_) {
-        fprintf(stderr, "[gol] GOL_FAULT: injected failure on rank %d at generation %llu\n", g_.rank,
+        fprintf(stderr, "[gol] GOL_FAULT: injected %s on rank %d at generation %llu\n", fault_mode_.c_str(), g_.rank,
                 (unsigned long long)gen_);
+        fflush(stderr);
+        if (fault_mode_ == "hang") {
+            fault_gen_ = -1;
+            for (;;) std::this_thread::sleep_for(std::chrono::seconds(1));  // only a watchdog ends this
+        }
+        if (fault_mode_ == "exit") _exit(3);  // crash without telling the peers
         t_->abort(3);
     }
 }
 
 void Engine::run(u64 generations) {
+    trace::Range range("gol.run");
+    Armed armed(wd_.get());
     while (generations > 0) {
         maybe_inject_fault();
         int k = cfg_.compat ? 1 : supported_depth((int)std::min<u64>((u64)L_.R, generations));
-        do_superstep(k);
+        {
+            trace::Range r("gol.superstep");
+            do_superstep(k);
+        }
         gen_ += (u64)k;
         generations -= (u64)k;
         stats_.generations += (u64)k;
         stats_.supersteps += 1;
+        progress("superstep");
     }
     maybe_inject_fault();
 }

@@ -9,10 +9,13 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cstring>
 #include <map>
+#include <thread>
 
 #include "gol/bits.hpp"
+#include "gol/trace.hpp"
 #include "gol/engine.hpp"
 #include "gol/hip_kernels.hpp"
 
@@ -107,6 +110,10 @@ class HipEngine : public Engine {
         hipHostFree(h_red_);
         hipEventDestroy(ev_ready_);
         hipEventDestroy(ev_halo_);
+        for (auto e : fence_ev_)
+            if (e) hipEventDestroy(e);
+        for (auto e : {ev_sync_comm_, ev_sync_comp_})
+            if (e) hipEventDestroy(e);
         if (cfg_.profile)
             for (auto e : {ev_t0_, ev_t1_, ev_t2_, ev_t3_}) hipEventDestroy(e);
         hipStreamDestroy(s_comp_);
@@ -116,8 +123,19 @@ class HipEngine : public Engine {
     std::string backend_name() const override { return "hip"; }
 
     void synchronize() override {
+        if (wd_) {  // poll instead of blocking, so asynchronous transport errors surface
+            HIP_CHECK(hipEventRecord(ev_sync_comm_ ? ev_sync_comm_ : make_sync_events(), s_comm_));
+            HIP_CHECK(hipEventRecord(ev_sync_comp_, s_comp_));
+            wait_watched(ev_sync_comm_);
+            wait_watched(ev_sync_comp_);
+        }
         HIP_CHECK(hipStreamSynchronize(s_comm_));
         HIP_CHECK(hipStreamSynchronize(s_comp_));
+    }
+    hipEvent_t make_sync_events() {
+        HIP_CHECK(hipEventCreateWithFlags(&ev_sync_comm_, hipEventDisableTiming));
+        HIP_CHECK(hipEventCreateWithFlags(&ev_sync_comp_, hipEventDisableTiming));
+        return ev_sync_comm_;
     }
 
     std::vector<u64> tile_words() override {
@@ -171,16 +189,21 @@ class HipEngine : public Engine {
             hipGraphExec_t exec = graph_for(k, m);
             if (!exec) break;
             maybe_inject_fault();
-            HIP_CHECK(hipGraphLaunch(exec, s_comp_));
+            {
+                trace::Range r("gol.graph_launch");
+                HIP_CHECK(hipGraphLaunch(exec, s_comp_));
+            }
             gen_ += per;
             generations -= per;
             stats_.generations += per;
             stats_.supersteps += (u64)m;
             stats_.graph_launches += 1;
+            progress("graph");
         }
     }
 
     void run(u64 generations) override {
+        Armed armed(wd_.get());
         if (cfg_.graph && !cfg_.profile) run_graphed(generations);
         Engine::run(generations);
     }
@@ -463,6 +486,7 @@ class HipEngine : public Engine {
     }
 
     void exchange_device(int k, const std::vector<HaloItem>& items, int parity, hipStream_t s) {
+        trace::Range r("gol.exchange_device");
         const DevCopies& dc = copies(k, parity);
         if (dc.npack) hipk::launch_copy_regions(dc.pack, dc.npack, dc.max_pack, s);
         std::vector<Message> sends, recvs;
@@ -474,6 +498,7 @@ class HipEngine : public Engine {
     }
 
     void exchange_staged(int k, const std::vector<HaloItem>& items, int parity, hipStream_t s) {
+        trace::Range r("gol.exchange_staged");
         const DevCopies& dc = copies(k, parity);
         if (dc.npack) hipk::launch_copy_regions(dc.pack, dc.npack, dc.max_pack, s);
         std::vector<Message> dsends, drecvs;
@@ -542,7 +567,36 @@ class HipEngine : public Engine {
         return exec;
     }
 
+    // ----- watchdog support -----
+    // Wait for `ev` without blocking in the driver, so a stuck or failed exchange is noticed: the
+    // transport's asynchronous error state is polled while waiting.
+    void wait_watched(hipEvent_t ev) {
+        for (;;) {
+            const hipError_t e = hipEventQuery(ev);
+            if (e == hipSuccess) return;
+            if (e != hipErrorNotReady) HIP_CHECK(e);
+            const std::string ae = t_->async_error();
+            if (!ae.empty()) fatal(ae, 5);
+            std::this_thread::sleep_for(std::chrono::microseconds(50));
+        }
+    }
+    // Bounded lookahead: the host runs at most kFenceDepth units (supersteps or graph launches)
+    // ahead of the GPU, so watchdog kicks track completed GPU work.
+    static constexpr int kFenceDepth = 4;
+    void fence() override {
+        if (!fence_ev_[0])
+            for (auto& e : fence_ev_) HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        HIP_CHECK(hipEventRecord(fence_ev_[fence_i_], s_comp_));
+        fence_used_[fence_i_] = true;
+        fence_i_ = (fence_i_ + 1) % kFenceDepth;
+        if (fence_used_[fence_i_]) wait_watched(fence_ev_[fence_i_]);
+    }
+
     int dev_ = 0, cus_ = 256;
+    hipEvent_t fence_ev_[kFenceDepth] = {};
+    hipEvent_t ev_sync_comm_ = nullptr, ev_sync_comp_ = nullptr;
+    bool fence_used_[kFenceDepth] = {};
+    int fence_i_ = 0;
     u64* buf_[2] = {nullptr, nullptr};
     size_t alloc_bytes_ = 0;
     int cur_ = 0;

@@ -7,6 +7,7 @@
 // abort every rank instead of leaving the others hanging (survey Q8, Q11).
 #include "gol/runtime.hpp"
 
+#include <algorithm>
 #include <chrono>
 #include <cstring>
 #include <exception>
@@ -17,6 +18,7 @@
 
 #include "gol/io.hpp"
 #include "gol/pattern.hpp"
+#include "gol/trace.hpp"
 
 namespace gol {
 
@@ -102,10 +104,36 @@ std::string select_backend(const Options& o, int rank, int local_rank) {
     return b;
 }
 
+// True when every rank drives a different GPU (RCCL needs one rank per device; the reference's
+// `rank % deviceCount` oversubscription, gol-with-cuda.cu:296, puts several ranks on one GPU).
+static bool devices_distinct(Transport& control, int device) {
+    char host[256] = {0};
+    gethostname(host, sizeof(host) - 1);
+    const std::string me = strprintf("%s#%d", host, device);
+    std::vector<std::vector<u8>> all;
+    control.gatherv(me.data(), me.size(), &all, 0);
+    u8 ok = 1;
+    if (control.rank() == 0) {
+        std::vector<std::string> ids;
+        for (auto& v : all) ids.emplace_back(v.begin(), v.end());
+        std::sort(ids.begin(), ids.end());
+        ok = std::adjacent_find(ids.begin(), ids.end()) == ids.end() ? 1 : 0;
+    }
+    control.broadcast(&ok, 1, 0);
+    return ok != 0;
+}
+
 std::shared_ptr<Transport> make_data_transport(std::shared_ptr<Transport> control, const std::string& backend,
-                                               const Options& o) {
-    if (backend == "hip" && control->size() > 1 && o.transport != "host") return make_rccl_transport(control);
-    return control;
+                                               const Options& o, int device) {
+    if (backend != "hip" || control->size() == 1 || o.transport == "host") return control;
+    if (!devices_distinct(*control, device)) {
+        if (o.transport == "rccl")
+            throw Error("GOL_TRANSPORT=rccl needs one rank per GPU, but ranks share a device");
+        if (control->rank() == 0 && o.verbose)
+            fprintf(stderr, "[gol] ranks share GPUs: halos are staged through host memory\n");
+        return control;
+    }
+    return make_rccl_transport(control);
 }
 
 EngineConfig engine_config(const Options& o, const std::string& backend, int device) {
@@ -124,6 +152,7 @@ EngineConfig engine_config(const Options& o, const std::string& backend, int dev
     c.transport = o.transport == "rccl" ? "device" : o.transport;
     c.profile = o.profile;
     c.graph_supersteps = (int)env_int("GOL_GRAPH_SUPERSTEPS", 0);
+    c.watchdog_s = o.watchdog_s;
     return c;
 }
 
@@ -132,6 +161,7 @@ EngineConfig engine_config(const Options& o, const std::string& backend, int dev
 // ---------------------------------------------------------------------------------------------
 
 void write_dumps(Engine& eng, FILE* fp) {
+    trace::Range range("gol.dump");
     const Geometry& g = eng.geometry();
     const Decomposition& d = g.dec;
     Transport& t = eng.transport();
@@ -188,6 +218,7 @@ std::string ckpt_name(const std::string& prefix, int rank, int P) {
 }  // namespace
 
 void save_checkpoint(Engine& eng, const std::string& prefix, u64 seed) {
+    trace::Range range("gol.checkpoint");
     const Geometry& g = eng.geometry();
     std::vector<u64> words = eng.tile_words();
     CkptHeader hd{};
@@ -285,11 +316,12 @@ int run_rank(const CliArgs& a, const Options& o, const LaunchInfo& li, std::shar
         if (backend == "hip") {
             int n = hip_device_count();
             device = local % n;
+            hip_set_device(device);  // before RCCL init: the communicator binds the current device
         }
         Decomposition dec = make_decomposition((i64)a.world_size, P, o.global_mode, o.decomp, o.grid);
         Geometry g = make_geometry(dec, rank);
         PatternSpec pat = make_pattern(a.pattern, dec, o.seed);
-        std::shared_ptr<Transport> t = make_data_transport(control, backend, o);
+        std::shared_ptr<Transport> t = make_data_transport(control, backend, o, device);
         std::unique_ptr<Engine> eng = Engine::create(g, engine_config(o, backend, device), t);
         if (o.verbose && rank == 0) fprintf(stderr, "[gol] %s\n", eng->describe().c_str());
         eng->init(pat);

@@ -303,7 +303,26 @@ static void test_bits() {
     }
 }
 
+static void test_watchdog() {
+    std::atomic<int> fired{0};
+    {
+        Watchdog wd(0.05, [&](const std::string&) { fired++; });
+        std::this_thread::sleep_for(std::chrono::milliseconds(150));
+        CHECK(fired.load() == 0);  // disarmed: never fires
+        wd.arm(true);
+        for (int i = 0; i < 10; ++i) {  // kicked in time: no fire
+            std::this_thread::sleep_for(std::chrono::milliseconds(10));
+            wd.kick("work");
+        }
+        CHECK(fired.load() == 0);
+        std::this_thread::sleep_for(std::chrono::milliseconds(200));
+        CHECK(fired.load() >= 1);  // stalled while armed: fires
+        wd.arm(false);
+    }
+}
+
 int main() {
+    test_watchdog();
     test_cli();
     test_geometry();
     test_patterns();

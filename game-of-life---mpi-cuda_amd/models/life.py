@@ -60,6 +60,7 @@ class Simulation:
     halo_depth:   generations per halo exchange (temporal blocking depth, <= 64; HIP caps at 16).
     decomp/grid:  ``"1d"`` row strips (reference) or ``"2d"`` blocks, optional ``"PxxPy"`` grid.
     compat:       reproduce the reference's halo quirks (frozen gen-0 halos, P<=2 swap).
+    watchdog:     seconds without progress before the job is aborted (0 = off; GOL_WATCHDOG).
     """
 
     def __init__(
@@ -82,6 +83,7 @@ class Simulation:
         rows_per_wave: int = 0,
         waves_target: int = 0,
         profile: bool = False,
+        watchdog: float = float(os.environ.get("GOL_WATCHDOG", "0")),
     ):
         self.transport = transport if transport is not None else _gol.SelfTransport()
         P, rank = self.transport.size(), self.transport.rank()
@@ -100,6 +102,7 @@ class Simulation:
         cfg.rows_per_wave = rows_per_wave
         cfg.waves_target = waves_target
         cfg.profile = profile
+        cfg.watchdog_s = float(watchdog)
         if self.backend == "hip":
             n = _gol.hip_device_count()
             if n <= 0:

@@ -164,4 +164,52 @@ def test_checkpoint_restart(gol_bin, tmp_path):
 def test_fault_injection_aborts_all_ranks(gol_bin, tmp_path):
     r = run(gol_bin, [5, 64, 40, 256, 0], tmp_path, nranks=3, env={"GOL_FAULT": "1:16"})
     assert r.returncode == 3
-    assert "injected failure on rank 1" in r.stderr
+    assert "injected abort on rank 1" in r.stderr
+
+
+def test_watchdog_ends_hung_thread_job(gol_bin, tmp_path):
+    """A rank that hangs (GOL_FAULT mode 'hang') is detected by the progress watchdog (exit 4)."""
+    r = run(gol_bin, [5, 64, 400, 256, 0], tmp_path, nranks=2,
+            env={"GOL_FAULT": "1:16:hang", "GOL_WATCHDOG": "1"})
+    assert r.returncode == 4, r.stderr
+    assert "watchdog: no progress" in r.stderr
+
+
+def _tcp_job(gol_bin, tmp_path, P, env, args=(5, 64, 400, 256, 0)):
+    port = _free_port()
+    procs = []
+    for q in range(P):
+        e = dict(os.environ, GOL_BACKEND="cpu", RANK=str(q), WORLD_SIZE=str(P), LOCAL_RANK=str(q),
+                 MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), **env)
+        procs.append(subprocess.Popen([gol_bin, *map(str, args)], cwd=tmp_path, env=e, stdout=subprocess.PIPE,
+                                      stderr=subprocess.PIPE, text=True))
+    outs = []
+    for p in procs:
+        try:
+            outs.append(p.communicate(timeout=60))
+        except subprocess.TimeoutExpired:
+            for x in procs:
+                x.kill()
+            pytest.fail("a rank hung: the failure was not propagated")
+    return [p.returncode for p in procs], outs
+
+
+def test_watchdog_multiprocess_hang(gol_bin, tmp_path):
+    codes, outs = _tcp_job(gol_bin, tmp_path, 3, {"GOL_FAULT": "1:16:hang", "GOL_WATCHDOG": "2"})
+    assert all(c != 0 for c in codes), (codes, outs)
+    assert any("watchdog" in err for _, err in outs)
+
+
+def test_crashed_peer_does_not_hang_job(gol_bin, tmp_path):
+    """A rank that dies without telling anyone (mode 'exit'): the others fail instead of hanging."""
+    codes, outs = _tcp_job(gol_bin, tmp_path, 3, {"GOL_FAULT": "2:8:exit", "GOL_WATCHDOG": "5"})
+    assert codes[2] == 3
+    assert all(c != 0 for c in codes), (codes, outs)
+
+
+def test_roctx_ranges_enabled(gol_bin, tmp_path):
+    """GOL_ROCTX=1 loads the roctx library and brackets phases; the run output is unchanged."""
+    r = run(gol_bin, [4, 64, 10, 256, 1], tmp_path, env={"GOL_ROCTX": "1"})
+    assert r.returncode == 0, r.stderr
+    assert "no roctx library" not in r.stderr
+    assert r.stdout.endswith(BANNER)

@@ -1,0 +1,71 @@
+"""The `gol` program on the HIP backend: multi-rank jobs oversubscribing one MI355X.
+
+The reference maps rank r to GPU `r % deviceCount` (gol-with-cuda.cu:296), so `mpirun -n P` on one
+GPU is its only multi-rank test rig.  Here P thread-ranks share device 0; RCCL needs
+one rank per GPU, so the runtime stages halos through host memory (the same canonical-order
+exchange, the same engine overlap/graph code).  Every dump is compared with the numpy torus oracle.
+"""
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+from gol_amd.ops import initial_board, numpy_step, quirk_model
+from gol_amd.utils import read_dump
+
+pytestmark = pytest.mark.gpu
+
+
+def _run(gol_bin, args, cwd, nranks, env=None):
+    e = dict(os.environ)
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "PMI_RANK", "PMI_SIZE"):
+        e.pop(k, None)
+    e.update(GOL_BACKEND="hip", GOL_NRANKS=str(nranks), GOL_VERBOSE="1")
+    if env:
+        e.update(env)
+    return subprocess.run([gol_bin, *map(str, args)], cwd=cwd, env=e, capture_output=True, text=True, timeout=300)
+
+
+def _board(cwd, P):
+    parts = []
+    for r in range(P):
+        rank, first, cells = read_dump(os.path.join(cwd, f"Rank_{r}_of_{P}.txt"))
+        parts.append((first, cells))
+    parts.sort(key=lambda t: t[0])
+    return np.vstack([c for _, c in parts])
+
+
+@pytest.mark.parametrize(
+    "P,env",
+    [
+        (2, {}),
+        (3, {"GOL_HALO_DEPTH": "4"}),
+        (4, {"GOL_OVERLAP": "0"}),
+        (4, {"GOL_GRAPH": "0", "GOL_HALO_DEPTH": "3"}),
+        (4, {"GOL_GLOBAL": "1", "GOL_DECOMP": "2d", "GOL_GRID": "2x2"}),
+        (2, {"GOL_GLOBAL": "1", "GOL_DECOMP": "2d", "GOL_GRID": "2x1", "GOL_OVERLAP": "0"}),
+        (3, {"GOL_WATCHDOG": "60"}),
+    ],
+)
+def test_threads_on_one_gpu_vs_oracle(gol_bin, tmp_path, P, env):
+    N, gens = 256, 45
+    r = _run(gol_bin, [5, N, gens, 256, 1], tmp_path, P, env)
+    assert r.returncode == 0, r.stderr
+    glob = env.get("GOL_GLOBAL") == "1"
+    ref = numpy_step(initial_board(5, N, P, not glob), gens)
+    assert np.array_equal(_board(tmp_path, P), ref)
+
+
+@pytest.mark.parametrize("P", [1, 2, 3])
+def test_compat_mode_on_gpu(gol_bin, tmp_path, P):
+    N, gens = 70, 6
+    r = _run(gol_bin, [5, N, gens, 256, 1], tmp_path, P, {"GOL_COMPAT": "reference"})
+    assert r.returncode == 0, r.stderr
+    assert np.array_equal(_board(tmp_path, P), quirk_model(initial_board(5, N, P, True), P, gens))
+
+
+def test_watchdog_hang_on_gpu(gol_bin, tmp_path):
+    r = _run(gol_bin, [5, 512, 4000, 256, 0], tmp_path, 2, {"GOL_FAULT": "1:64:hang", "GOL_WATCHDOG": "2"})
+    assert r.returncode == 4, r.stderr
+    assert "watchdog: no progress" in r.stderr

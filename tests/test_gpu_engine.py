@@ -110,3 +110,12 @@ def test_kernel_variants(gol, pipeline, prefetch, depth):
     s = _sim(gol, N, halo_depth=depth, pipeline=pipeline, prefetch=prefetch).init(5, seed=depth)
     s.step(gens)
     assert np.array_equal(s.board(), numpy_step(initial_board(5, N, 1, True, depth), gens))
+
+
+@pytest.mark.parametrize("graph", [True, False])
+def test_watchdog_fenced_run(gol, graph):
+    """Watchdog mode bounds the host lookahead with polled events; results are unchanged."""
+    N, gens = 512, 8 * 40 + 3
+    s = _sim(gol, N, halo_depth=8, graph=graph, watchdog=60.0).init(5, seed=21)
+    s.step(gens)
+    assert np.array_equal(s.board(), numpy_step(initial_board(5, N, 1, True, 21), gens))
