@@ -36,7 +36,8 @@ def main() -> int:
     ap.add_argument("--scaling", choices=["weak", "strong"], default="weak")
     ap.add_argument("--decomp", default="1d", help="1d | 2d | auto")
     ap.add_argument("--halo-depth", type=int, default=int(os.environ.get("GOL_HALO_DEPTH", "8")))
-    ap.add_argument("--kernel", default=os.environ.get("GOL_KERNEL", "temporal"))
+    ap.add_argument("--kernel", default=os.environ.get("GOL_KERNEL", "auto"),
+                    help="auto (timed at init) | temporal | tile | lds")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--no-overlap", action="store_true")
     ap.add_argument("--yardstick", action="store_true", help="also time the naive byte-per-cell kernel (rank 0)")
@@ -79,12 +80,19 @@ def main() -> int:
     dec = sim.decomposition
     cells = dec.H * dec.W
 
+    import torch
+
+    def device_sync():
+        sim.synchronize()  # the engine's own HIP streams
+        if backend == "hip" and torch.cuda.is_available():
+            torch.cuda.synchronize()
+
     sim.step(warmup)
-    sim.synchronize()
+    device_sync()
     transport.barrier()
     t0 = time.perf_counter()
     sim.step(steps)
-    sim.synchronize()
+    device_sync()
     t1 = time.perf_counter()
     transport.barrier()
     elapsed = transport.allreduce_max(t1 - t0)
@@ -122,7 +130,7 @@ def main() -> int:
                 "parallelism": f"{'2d' if dec.Px > 1 else '1d'}-spatial p{P} ({dec.Px}x{dec.Py})",
                 "backend": backend,
                 "halo_depth": st["depth"],
-                "kernel": args.kernel,
+                "kernel": st["kernel"],
                 "graph_launches": st["graph_launches"],
                 "plan_waves": st["plan_waves"],
                 "lane_efficiency": round(st["lane_efficiency"], 4),

@@ -38,7 +38,9 @@ struct EngineConfig {
     int device = -1;                  // HIP device (-1: current)
     i64 rows_per_wave = 0;            // plan segment height override (0 = auto)
     int waves_target = 0;             // plan wave-count target (0 = auto)
-    std::string kernel = "temporal";  // temporal | lds
+    std::string kernel = "auto";      // auto (timed at init) | temporal (register pipeline) |
+                                      // tile (LDS-resident) | lds (1 gen, reference-class LDS tile)
+    int tile_waves = 8;               // tile kernel: waves per workgroup (4, 8, 16)
     std::string prefetch = "reg";     // temporal kernel row prefetch: reg (pinned triple) | lds (DMA ring)
     std::string pipeline = "chain";   // temporal kernel level pipeline: chain | skew (ILP variant)
     std::string transport = "auto";   // auto | device | host  (host = stage halos through host memory)
@@ -58,6 +60,7 @@ struct EngineStats {
     double lane_efficiency = 0;  // output words / (64 * input rows * waves) for the full plan
     double t_exchange_ms = 0;  // profile only
     double t_compute_ms = 0;   // profile only
+    std::string kernel;        // stencil kernel in use (HIP: temporal | tile | lds; CPU: cpu)
 };
 
 class Engine {

@@ -54,6 +54,13 @@ int max_step_depth();
 // Launch K generations: src -> dst over the waves of `plan` (n_waves * 64 LaneDescs in device memory).
 void launch_step(int k, const u64* src, u64* dst, const LaneDesc* plan, i64 n_waves, const StepParams& p,
                  hipStream_t s);
+// LDS-resident temporal kernel (step_tile): one workgroup of `nw_per_wg` (4, 8, 16) waves per plan
+// wave; `rows` = the plan's rows per chunk (<= tile_max_rows(k), the 160 KiB LDS limit).
+constexpr size_t kMaxLdsBytes = 160 * 1024;
+i64 tile_max_rows(int k);
+int tile_blocks_per_cu(int nw_per_wg, i64 rows, int k, u32 flags);
+void launch_step_tile(int nw_per_wg, int k, const u64* src, u64* dst, const LaneDesc* plan, i64 n_tiles, i64 rows,
+                      const StepParams& p, hipStream_t s);
 // Single-generation LDS-tiled kernel over output rows [r0, r1) (all words).
 void launch_step_lds(const u64* src, u64* dst, const Layout& L, i64 r0, i64 r1, u32 flags, hipStream_t s);
 

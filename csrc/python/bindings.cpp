@@ -102,6 +102,7 @@ py::dict stats_dict(const EngineStats& s) {
     d["lane_efficiency"] = s.lane_efficiency;
     d["t_exchange_ms"] = s.t_exchange_ms;
     d["t_compute_ms"] = s.t_compute_ms;
+    d["kernel"] = s.kernel;
     return d;
 }
 
@@ -239,7 +240,8 @@ PYBIND11_MODULE(_gol, m) {
         .def_readwrite("transport", &EngineConfig::transport)
         .def_readwrite("profile", &EngineConfig::profile)
         .def_readwrite("graph_supersteps", &EngineConfig::graph_supersteps)
-        .def_readwrite("watchdog_s", &EngineConfig::watchdog_s);
+        .def_readwrite("watchdog_s", &EngineConfig::watchdog_s)
+        .def_readwrite("tile_waves", &EngineConfig::tile_waves);
 
     py::class_<Engine>(m, "Engine")
         .def_static(

@@ -111,6 +111,7 @@ void Engine::init(const PatternSpec& p) {
     gen_ = 0;
     stats_ = EngineStats{};
     stats_.depth = L_.R;
+    stats_.kernel = backend_name() == "cpu" ? "cpu" : cfg_.kernel;
     do_init(p);
     if (cfg_.compat) setup_compat();
 }

@@ -43,6 +43,7 @@ namespace {
 struct DevPlan {
     LaneDesc* d = nullptr;
     i64 waves = 0;
+    i64 rows = 0;  // rows per chunk
     PlanStats st;
 };
 
@@ -62,13 +63,18 @@ class HipEngine : public Engine {
         HIP_CHECK(hipGetDeviceProperties(&prop, dev_));
         cus_ = prop.multiProcessorCount;
         int R = L_.R;
-        if (cfg_.kernel == "lds") {
+        kernel_ = cfg_.kernel;
+        if (kernel_ == "lds") {
             R = 1;
-        } else if (cfg_.kernel != "temporal") {
-            throw Error("GOL_KERNEL must be temporal or lds");
+        } else if (kernel_ == "tile") {
+            R = std::min(R, 32);  // any depth; LDS rows bound it (tile_max_rows)
+        } else if (kernel_ == "temporal" || kernel_ == "auto") {
+            // auto: the depth must suit both candidates (instantiated temporal depths)
+            R = std::min(R, hipk::max_step_depth());
+            while (!hipk::step_depth_supported(R)) --R;
+        } else {
+            throw Error("GOL_KERNEL must be auto, temporal, tile or lds (got '" + kernel_ + "')");
         }
-        R = std::min(R, hipk::max_step_depth());
-        while (!hipk::step_depth_supported(R)) --R;
         if (R != L_.R) L_ = Layout(L_.h, L_.w, R);
         stats_.depth = R;
         // slack rows: the temporal kernel prefetches 3 rows past a segment's last input row
@@ -236,6 +242,11 @@ class HipEngine : public Engine {
         HIP_CHECK(hipEventRecord(ev_ready_, s_comp_));
         synchronize();
         if (dcells) HIP_CHECK(hipFree(dcells));
+        if (cfg_.kernel == "auto" && !tuned_) {
+            autotune_kernel();
+            tuned_ = true;
+        }
+        stats_.kernel = kernel_;
         // Build the plans for every depth a run can use (remainder supersteps included) now, so
         // neither graph capture nor a timed loop ever builds or uploads a plan.
         for (int k = 1; k <= (cfg_.compat ? 1 : L_.R); ++k)
@@ -326,7 +337,10 @@ class HipEngine : public Engine {
     }
 
     int supported_depth(int want) const override {
+        // Depends on the CONFIGURED kernel only: every rank must cut the same supersteps (the halo
+        // exchange sizes follow k), even when GOL_KERNEL=auto resolves differently per rank.
         if (cfg_.kernel == "lds") return 1;
+        if (cfg_.kernel == "tile") return std::max(1, want);
         while (want > 1 && !hipk::step_depth_supported(want)) --want;
         return std::max(1, want);
     }
@@ -342,10 +356,44 @@ class HipEngine : public Engine {
         return f;
     }
 
+    bool tile_kernel() const { return kernel_ == "tile"; }
+
+    // GOL_KERNEL=auto: time one full-tile superstep of each candidate kernel (into the scratch
+    // buffer, so the board is untouched) and keep the faster one.  The register pipeline wins on
+    // big tiles; the LDS-resident tile kernel on small ones (its vertical halo is shared by a whole
+    // workgroup), e.g. a strong-scaled board's strips.
+    void autotune_kernel() {
+        const int k = cfg_.compat ? 1 : L_.R;
+        float best = 1e30f;
+        std::string pick = "temporal";
+        hipEvent_t e0, e1;
+        HIP_CHECK(hipEventCreate(&e0));
+        HIP_CHECK(hipEventCreate(&e1));
+        for (const char* cand : {"temporal", "tile"}) {
+            kernel_ = cand;
+            if (kernel_ == "tile" && hipk::tile_max_rows(k) < 1) continue;
+            launch(0, k, buf_[cur_], buf_[cur_ ^ 1], s_comp_);  // warm-up (and plan build)
+            HIP_CHECK(hipEventRecord(e0, s_comp_));
+            for (int i = 0; i < 3; ++i) launch(0, k, buf_[cur_], buf_[cur_ ^ 1], s_comp_);
+            HIP_CHECK(hipEventRecord(e1, s_comp_));
+            HIP_CHECK(hipEventSynchronize(e1));
+            float ms = 0;
+            HIP_CHECK(hipEventElapsedTime(&ms, e0, e1));
+            tune_ms_[kernel_] = ms / 3;
+            if (ms < best) {
+                best = ms;
+                pick = kernel_;
+            }
+        }
+        HIP_CHECK(hipEventDestroy(e0));
+        HIP_CHECK(hipEventDestroy(e1));
+        kernel_ = pick;
+    }
+
     bool can_overlap() const {
         // interior must exist, and the LDS kernel reads ghost words for every row (2-D needs them)
         if (L_.h <= 2 * (i64)L_.R) return false;
-        if (cfg_.kernel == "lds" && g_.dec.Px > 1) return false;
+        if (kernel_ == "lds" && g_.dec.Px > 1) return false;
         return true;
     }
 
@@ -370,27 +418,41 @@ class HipEngine : public Engine {
     }
 
     const DevPlan& plan(int kind, int k) {
-        const int key = kind * 1000 + k;
+        const int key = (tile_kernel() ? 100000 : 0) + kind * 1000 + k;
         auto it = plans_.find(key);
         if (it != plans_.end()) return it->second;
         std::vector<Region> rg = regions(kind, k);
         DevPlan p;
         i64 rows = cfg_.rows_per_wave;
-        if (rows <= 0 && cfg_.waves_target > 0) rows = choose_rows_per_chunk(rg, k, cfg_.waves_target, 4 * (i64)k);
-        if (rows <= 0) {
-            // one full round of resident waves (occupancy of this kernel instantiation)
-            const i64 resident = (i64)hipk::step_blocks_per_cu(k, step_flags()) * kWavesPerBlock * cus_;
-            rows = balanced_rows_per_chunk(rg, L_.nw, L_.h, k, resident, 2 * (i64)k, xwrap_by_plan());
+        if (tile_kernel()) {
+            // step_tile: one workgroup per plan wave, one tile per CU per round; rows are capped by
+            // the 160 KiB of LDS (double-buffered tile + 2k halo rows), extra rounds beyond that
+            const i64 rmax = hipk::tile_max_rows(k);
+            if (rmax < 1) throw Error(strprintf("GOL_KERNEL=tile: depth %d leaves no LDS rows", k));
+            if (rows > rmax) rows = rmax;
+            for (i64 rounds = 1; rows <= 0; ++rounds) {
+                const i64 r = balanced_rows_per_chunk(rg, L_.nw, L_.h, k, rounds * cus_, 1, xwrap_by_plan());
+                if (r <= rmax) rows = r;
+            }
+        } else {
+            if (rows <= 0 && cfg_.waves_target > 0)
+                rows = choose_rows_per_chunk(rg, k, cfg_.waves_target, 4 * (i64)k);
+            if (rows <= 0) {
+                // one full round of resident waves (occupancy of this kernel instantiation)
+                const i64 resident = (i64)hipk::step_blocks_per_cu(k, step_flags()) * kWavesPerBlock * cus_;
+                rows = balanced_rows_per_chunk(rg, L_.nw, L_.h, k, resident, 2 * (i64)k, xwrap_by_plan());
+            }
         }
         std::vector<LaneDesc> lanes = build_plan(rg, L_.nw, L_.h, rows, k, xwrap_by_plan(), &p.st);
         p.waves = (i64)lanes.size() / kWaveLanes;
+        p.rows = rows;
         HIP_CHECK(hipMalloc(&p.d, lanes.size() * sizeof(LaneDesc)));
         HIP_CHECK(hipMemcpy(p.d, lanes.data(), lanes.size() * sizeof(LaneDesc), hipMemcpyHostToDevice));
         return plans_.emplace(key, p).first->second;
     }
 
     void launch(int kind, int k, const u64* src, u64* dst, hipStream_t s) {
-        if (cfg_.kernel == "lds") {
+        if (kernel_ == "lds") {
             // full-row bands only (the LDS variant is never split by columns: can_overlap)
             for (const Region& r : regions(kind, 1))
                 if (r.c0 == 0) hipk::launch_step_lds(src, dst, L_, r.r0, r.r1, step_flags(), s);
@@ -398,7 +460,10 @@ class HipEngine : public Engine {
             const DevPlan& p = plan(kind, k);
             if (p.st.out_words == 0) return;
             hipk::StepParams sp{L_.pitch, (i32)L_.h, (i32)L_.nw, L_.R, step_flags()};
-            hipk::launch_step(k, src, dst, p.d, p.waves, sp, s);
+            if (tile_kernel())
+                hipk::launch_step_tile(cfg_.tile_waves, k, src, dst, p.d, p.waves, p.rows, sp, s);
+            else
+                hipk::launch_step(k, src, dst, p.d, p.waves, sp, s);
         }
         HIP_CHECK(hipGetLastError());
     }
@@ -593,6 +658,9 @@ class HipEngine : public Engine {
     }
 
     int dev_ = 0, cus_ = 256;
+    std::string kernel_;  // resolved kernel: temporal | tile | lds (auto resolves at init)
+    bool tuned_ = false;
+    std::map<std::string, float> tune_ms_;
     hipEvent_t fence_ev_[kFenceDepth] = {};
     hipEvent_t ev_sync_comm_ = nullptr, ev_sync_comp_ = nullptr;
     bool fence_used_[kFenceDepth] = {};

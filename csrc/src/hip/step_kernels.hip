@@ -336,6 +336,149 @@ const void* kernel_for(u32 flags) {
 }
 
 // ------------------------------------------------------------------------------------------
+// step_tile: LDS-resident temporal blocking.  One workgroup of NW waves per plan wave: the plan
+// wave's 64 lanes (segments + halo lanes, plan.hpp) define the tile columns and its `nrows` output
+// rows; the tile plus K halo rows above and below (n_in = nrows + 2K rows x 64 lanes, split
+// storage lo/hi planes, 512 B per row) is staged into LDS with global_load_lds DMA, then the
+// K generations run LDS -> LDS: generation g computes rows [g+1, n_in-g-1), the NW waves each take
+// a contiguous band of rows, stream it with a one-level register window (the same hsum/rule code
+// as step_temporal), and a workgroup barrier separates generations.  The last generation stores
+// straight to HBM.  Compared with step_temporal the vertical halo (2K rows) is shared by the NW
+// waves of the tile instead of being paid by every wave, which is what small tiles (e.g. 8192^2,
+// or a 32768^2 board strong-scaled over 8 GPUs) need; big tiles keep step_temporal (no barriers,
+// no LDS traffic).  K is a runtime argument.
+// ------------------------------------------------------------------------------------------
+constexpr int kTileRowU32 = 128;  // one LDS row: 64 lo words then 64 hi words
+
+template <bool LAST>
+struct BandSink {
+    u32* lds;       // !LAST: destination buffer (row-major, kTileRowU32 per row)
+    uint2* st;      // LAST: global store pointer of the band's first output row
+    i64 st_stride;  // LAST: pitch, or 0 for halo/idle lanes (trash row)
+    int row;        // !LAST: tile row of the next output
+    int lane;
+    __device__ __forceinline__ void put(u32 lo, u32 hi) {
+        if constexpr (LAST) {
+            *st = make_uint2(lo, hi);
+            st += st_stride;
+        } else {
+            lds[row * kTileRowU32 + lane] = lo;
+            lds[row * kTileRowU32 + 64 + lane] = hi;
+            ++row;
+        }
+    }
+};
+
+// Stream input rows in[0 .. n) (n >= 3) through a one-level window; outputs rows 1 .. n-2.
+template <bool LAST>
+__device__ __forceinline__ void tile_band(const u32* __restrict__ in, int n, BandSink<LAST>& out, int lane) {
+    Pipe<1> P;
+    u32 lo, hi;
+#define GOL_TILE_ROW(PH, GUARD, IDX)                                   \
+    lo = in[(IDX) * kTileRowU32 + lane];                               \
+    hi = in[(IDX) * kTileRowU32 + 64 + lane];                          \
+    if (advance<1, PH, GUARD>(P, lo, hi, (IDX))) out.put(lo, hi);
+    GOL_TILE_ROW(0, true, 0)
+    GOL_TILE_ROW(1, true, 1)
+    GOL_TILE_ROW(2, true, 2)
+    int i = 3;
+    for (; i + 3 <= n; i += 3) {
+        // hoist the triple's LDS reads above its compute (stores to the other buffer do not alias)
+        const u32 l0 = in[i * kTileRowU32 + lane], h0 = in[i * kTileRowU32 + 64 + lane];
+        const u32 l1 = in[(i + 1) * kTileRowU32 + lane], h1 = in[(i + 1) * kTileRowU32 + 64 + lane];
+        const u32 l2 = in[(i + 2) * kTileRowU32 + lane], h2 = in[(i + 2) * kTileRowU32 + 64 + lane];
+        __builtin_amdgcn_sched_barrier(0);
+        lo = l0, hi = h0;
+        if (advance<1, 0, false>(P, lo, hi, i)) out.put(lo, hi);
+        lo = l1, hi = h1;
+        if (advance<1, 1, false>(P, lo, hi, i + 1)) out.put(lo, hi);
+        lo = l2, hi = h2;
+        if (advance<1, 2, false>(P, lo, hi, i + 2)) out.put(lo, hi);
+    }
+    if (i < n) {
+        GOL_TILE_ROW(0, false, i)
+    }
+    if (i + 1 < n) {
+        GOL_TILE_ROW(1, false, i + 1)
+    }
+#undef GOL_TILE_ROW
+}
+
+template <int NW, bool WRAPY>
+__global__ __launch_bounds__(64 * NW) void step_tile(const u64* __restrict__ src, u64* __restrict__ dst,
+                                                     const LaneDesc* __restrict__ plan, StepParams p, int K) {
+    extern __shared__ __attribute__((aligned(16))) u32 tile_lds[];
+    const int lane = threadIdx.x & 63;
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const LaneDesc d = plan[(i64)blockIdx.x * kWaveLanes + lane];
+    const int nrows = __builtin_amdgcn_readfirstlane(d.nrows);
+    if (nrows <= 0) return;  // padding tile (uniform over the workgroup)
+    const int n_in = nrows + 2 * K;
+    u32* A = tile_lds;
+    u32* B = tile_lds + n_in * kTileRowU32;
+
+    // 1. stage rows row0-K .. row0+nrows+K-1 (two 4-byte DMAs per row: lo plane, hi plane)
+    for (int i = wv; i < n_in; i += NW) {
+        int r = d.row0 - K + i;
+        if (WRAPY) r = r < 0 ? r + p.h : (r >= p.h ? r - p.h : r);
+        const u32* g = reinterpret_cast<const u32*>(src + (i64)(r + p.R) * p.pitch + (d.col + 1));
+        u32* l = A + i * kTileRowU32;
+        __builtin_amdgcn_global_load_lds((glb_void_t*)g, (lds_void_t*)l, 4, 0, 0);
+        __builtin_amdgcn_global_load_lds((glb_void_t*)(g + 1), (lds_void_t*)(l + 64), 4, 0, 0);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+
+    // 2. K generations; generation g computes tile rows [g+1, n_in-g-1)
+    const bool out_lane = d.flags & LANE_STORE;
+    for (int g = 0; g < K; ++g) {
+        const int lo_r = g + 1, cnt = n_in - 2 * g - 2;
+        const int b = (cnt + NW - 1) / NW;
+        const int r0 = lo_r + wv * b;
+        const int r1 = min(r0 + b, lo_r + cnt);
+        if (r1 > r0) {
+            if (g + 1 < K) {
+                BandSink<false> s{B, nullptr, 0, r0, lane};
+                tile_band<false>(A + (r0 - 1) * kTileRowU32, r1 - r0 + 2, s, lane);
+            } else {
+                // tile row r0 is output row row0 + r0 - K; halo/idle lanes write the trash row
+                const i64 srow = out_lane ? (i64)(d.row0 + r0 - K + p.R) : (i64)(p.h + 2 * p.R + kSlackRows - 1);
+                BandSink<true> s{nullptr, reinterpret_cast<uint2*>(dst + srow * p.pitch + (d.col + 1)),
+                                 out_lane ? p.pitch : 0, 0, lane};
+                tile_band<true>(A + (r0 - 1) * kTileRowU32, r1 - r0 + 2, s, lane);
+            }
+        }
+        if (g + 1 < K) {
+            __syncthreads();
+            u32* t = A;
+            A = B;
+            B = t;
+        }
+    }
+}
+
+// LDS bytes of a tile with `rows` output rows at depth k (+4 rows of over-read slack).
+inline size_t tile_lds_bytes(i64 rows, int k) { return (size_t)(2 * (rows + 2 * k) + 4) * kTileRowU32 * 4; }
+
+template <int NW>
+const void* tile_kernel(u32 flags) {
+    return (flags & STEP_WRAP_Y) ? (const void*)step_tile<NW, true> : (const void*)step_tile<NW, false>;
+}
+
+const void* tile_kernel_for(int nw_per_wg, u32 flags) {
+    switch (nw_per_wg) {
+        case 4:
+            return tile_kernel<4>(flags);
+        case 8:
+            return tile_kernel<8>(flags);
+        case 16:
+            return tile_kernel<16>(flags);
+        default:
+            return nullptr;
+    }
+}
+
+// ------------------------------------------------------------------------------------------
 // LDS-tiled single-generation kernel.
 // ------------------------------------------------------------------------------------------
 constexpr int kLdsRows = 16, kLdsWords = 64;
@@ -417,6 +560,47 @@ void launch_step(int k, const u64* src, u64* dst, const LaneDesc* plan, i64 n_wa
     void* args[] = {(void*)&src, (void*)&dst, (void*)&plan, (void*)&pp};
     hipError_t e = hipLaunchKernel(f, grid, block, args, 0, s);
     if (e != hipSuccess) throw Error(strprintf("step kernel launch failed: %s", hipGetErrorString(e)));
+}
+
+i64 tile_max_rows(int k) {
+    const i64 lds_rows = kMaxLdsBytes / (kTileRowU32 * 4);  // 320 rows of 512 B
+    return (lds_rows - 4) / 2 - 2 * (i64)k;
+}
+
+static const void* tile_kernel_checked(int nw_per_wg, u32 flags) {
+    const void* f = tile_kernel_for(nw_per_wg, flags);
+    if (!f) throw Error(strprintf("step_tile: unsupported waves per workgroup %d (4, 8 or 16)", nw_per_wg));
+    static bool attr_set[64] = {};
+    const int key = (nw_per_wg & 31) * 2 + ((flags & STEP_WRAP_Y) ? 1 : 0);
+    if (!attr_set[key]) {  // allow the full 160 KiB of dynamic LDS
+        hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kMaxLdsBytes);
+        if (e != hipSuccess) throw Error(strprintf("step_tile: hipFuncSetAttribute: %s", hipGetErrorString(e)));
+        attr_set[key] = true;
+    }
+    return f;
+}
+
+int tile_blocks_per_cu(int nw_per_wg, i64 rows, int k, u32 flags) {
+    const void* f = tile_kernel_checked(nw_per_wg, flags);
+    int nb = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, f, 64 * nw_per_wg, tile_lds_bytes(rows, k)) != hipSuccess ||
+        nb < 1)
+        return 1;
+    return std::min(nb, 8);
+}
+
+void launch_step_tile(int nw_per_wg, int k, const u64* src, u64* dst, const LaneDesc* plan, i64 n_tiles, i64 rows,
+                      const StepParams& p, hipStream_t s) {
+    if (k < 1 || k > 64) throw Error(strprintf("step_tile: depth %d outside 1..64", k));
+    if (rows < 1 || rows > tile_max_rows(k))
+        throw Error(strprintf("step_tile: %lld rows per tile exceed the LDS capacity (max %lld at depth %d)",
+                              (long long)rows, (long long)tile_max_rows(k), k));
+    const void* f = tile_kernel_checked(nw_per_wg, p.flags);
+    StepParams pp = p;
+    int kk = k;
+    void* args[] = {(void*)&src, (void*)&dst, (void*)&plan, (void*)&pp, (void*)&kk};
+    hipError_t e = hipLaunchKernel(f, dim3((unsigned)n_tiles), dim3(64 * nw_per_wg), args, tile_lds_bytes(rows, k), s);
+    if (e != hipSuccess) throw Error(strprintf("step_tile launch failed: %s", hipGetErrorString(e)));
 }
 
 void launch_step_lds(const u64* src, u64* dst, const Layout& L, i64 r0, i64 r1, u32 flags, hipStream_t s) {

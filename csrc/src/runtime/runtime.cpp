@@ -146,7 +146,8 @@ EngineConfig engine_config(const Options& o, const std::string& backend, int dev
     c.device = device;
     c.rows_per_wave = o.rows_per_wave;
     c.waves_target = o.waves_target;
-    c.kernel = env_str("GOL_KERNEL", "temporal");
+    c.kernel = env_str("GOL_KERNEL", "auto");
+    c.tile_waves = (int)env_int("GOL_TILE_WAVES", 8);
     c.prefetch = env_str("GOL_PREFETCH", "reg");
     c.pipeline = env_str("GOL_PIPELINE", "chain");
     c.transport = o.transport == "rccl" ? "device" : o.transport;
@@ -292,6 +293,7 @@ void write_metrics(const Options& o, Engine& eng, const CliArgs& a, double durat
     f << "  \"supersteps\": " << s.supersteps << ",\n  \"exchanges\": " << s.exchanges << ",\n";
     f << "  \"halo_bytes_rank0\": " << s.halo_bytes << ",\n";
     f << "  \"graph_launches\": " << s.graph_launches << ",\n";
+    f << "  \"kernel\": \"" << s.kernel << "\",\n";
     f << "  \"plan_waves\": " << s.plan_waves << ",\n  \"lane_efficiency\": " << s.lane_efficiency << ",\n";
     f << "  \"t_exchange_ms\": " << s.t_exchange_ms << ",\n  \"t_compute_ms\": " << s.t_compute_ms << "\n";
     f << "}\n";

@@ -77,13 +77,14 @@ class Simulation:
         graph: bool = True,
         compat: bool = False,
         device: Optional[int] = None,
-        kernel: str = "temporal",
+        kernel: str = os.environ.get("GOL_KERNEL", "auto"),
         prefetch: str = os.environ.get("GOL_PREFETCH", "reg"),
         pipeline: str = os.environ.get("GOL_PIPELINE", "chain"),
         rows_per_wave: int = 0,
         waves_target: int = 0,
         profile: bool = False,
         watchdog: float = float(os.environ.get("GOL_WATCHDOG", "0")),
+        tile_waves: int = int(os.environ.get("GOL_TILE_WAVES", "8")),
     ):
         self.transport = transport if transport is not None else _gol.SelfTransport()
         P, rank = self.transport.size(), self.transport.rank()
@@ -103,6 +104,7 @@ class Simulation:
         cfg.waves_target = waves_target
         cfg.profile = profile
         cfg.watchdog_s = float(watchdog)
+        cfg.tile_waves = int(tile_waves)
         if self.backend == "hip":
             n = _gol.hip_device_count()
             if n <= 0:

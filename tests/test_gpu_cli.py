@@ -69,3 +69,12 @@ def test_watchdog_hang_on_gpu(gol_bin, tmp_path):
     r = _run(gol_bin, [5, 512, 4000, 256, 0], tmp_path, 2, {"GOL_FAULT": "1:64:hang", "GOL_WATCHDOG": "2"})
     assert r.returncode == 4, r.stderr
     assert "watchdog: no progress" in r.stderr
+
+
+@pytest.mark.parametrize("env", [{}, {"GOL_GLOBAL": "1", "GOL_DECOMP": "2d", "GOL_GRID": "2x2"}])
+def test_tile_kernel_multi_rank(gol_bin, tmp_path, env):
+    P, N, gens = 4, 256, 37
+    r = _run(gol_bin, [5, N, gens, 256, 1], tmp_path, P, dict(env, GOL_KERNEL="tile", GOL_HALO_DEPTH="6"))
+    assert r.returncode == 0, r.stderr
+    glob = env.get("GOL_GLOBAL") == "1"
+    assert np.array_equal(_board(tmp_path, P), numpy_step(initial_board(5, N, P, not glob), gens))

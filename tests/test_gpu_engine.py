@@ -119,3 +119,39 @@ def test_watchdog_fenced_run(gol, graph):
     s = _sim(gol, N, halo_depth=8, graph=graph, watchdog=60.0).init(5, seed=21)
     s.step(gens)
     assert np.array_equal(s.board(), numpy_step(initial_board(5, N, 1, True, 21), gens))
+
+
+@pytest.mark.parametrize("tile_waves", [4, 8, 16])
+@pytest.mark.parametrize("depth", [1, 2, 5, 8, 13])
+def test_tile_kernel_depths(gol, tile_waves, depth):
+    """LDS-resident temporal kernel (any runtime depth) vs numpy."""
+    N, gens = 700, 3 * depth + 5
+    s = _sim(gol, N, halo_depth=depth, kernel="tile", tile_waves=tile_waves).init(5, seed=depth)
+    s.step(gens)
+    assert np.array_equal(s.board(), numpy_step(initial_board(5, N, 1, True, depth), gens))
+
+
+@pytest.mark.parametrize("N", [1, 3, 65, 137, 1000, 4096])
+def test_tile_kernel_sizes(gol, N):
+    gens = 29
+    s = _sim(gol, N, halo_depth=8, kernel="tile").init(5, seed=N + 1)
+    s.step(gens)
+    assert np.array_equal(s.board(), numpy_step(initial_board(5, N, 1, True, N + 1), gens))
+
+
+@pytest.mark.parametrize("rows", [1, 5, 64])
+def test_tile_kernel_plan_rows(gol, rows):
+    N, gens = 640, 21
+    s = _sim(gol, N, halo_depth=6, kernel="tile", rows_per_wave=rows).init(5, seed=77)
+    s.step(gens)
+    assert np.array_equal(s.board(), numpy_step(initial_board(5, N, 1, True, 77), gens))
+
+
+@pytest.mark.parametrize("N", [96, 2048])
+def test_auto_kernel_choice(gol, N):
+    """GOL_KERNEL=auto times both kernels at init and keeps one; results are exact either way."""
+    gens = 53
+    s = _sim(gol, N, halo_depth=8, kernel="auto").init(5, seed=N)
+    assert s.stats()["kernel"] in ("temporal", "tile")
+    s.step(gens)
+    assert np.array_equal(s.board(), numpy_step(initial_board(5, N, 1, True, N), gens))

@@ -31,6 +31,8 @@ int main(int argc, char** argv) {
     const int gens = argc > 3 ? atoi(argv[3]) : 960;
     const int pf = argc > 4 ? atoi(argv[4]) : 0;
     const int skew = argc > 5 ? atoi(argv[5]) : 0;
+    const int tile_nw = argc > 6 ? atoi(argv[6]) : 0;  // >0: step_tile with this many waves per workgroup
+    const i64 rows_arg = argc > 7 ? atoll(argv[7]) : 0;
     Layout L(N, N, K);
     const size_t bytes = (size_t)(L.words() + hipk::kSlackRows * L.pitch) * 8;
     u64 *a, *b;
@@ -43,9 +45,19 @@ int main(int argc, char** argv) {
     hipDeviceProp_t prop;
     CK(hipGetDeviceProperties(&prop, 0));
     const u32 flags = hipk::STEP_WRAP_Y | (pf ? hipk::STEP_PF_LDS : 0u) | (skew ? hipk::STEP_SKEW : 0u);
-    const i64 resident = (i64)hipk::step_blocks_per_cu(K, flags) * kWavesPerBlock * prop.multiProcessorCount;
     std::vector<Region> rg = {{0, N, 0, L.nw}};
-    const i64 rows = balanced_rows_per_chunk(rg, L.nw, N, K, resident, 2 * K, true);
+    i64 rows = rows_arg;
+    if (tile_nw > 0) {
+        const i64 rmax = hipk::tile_max_rows(K);
+        if (rows > rmax) rows = rmax;
+        for (i64 rounds = 1; rows <= 0; ++rounds) {
+            const i64 r = balanced_rows_per_chunk(rg, L.nw, N, K, rounds * prop.multiProcessorCount, 1, true);
+            if (r <= rmax) rows = r;
+        }
+    } else if (rows <= 0) {
+        const i64 resident = (i64)hipk::step_blocks_per_cu(K, flags) * kWavesPerBlock * prop.multiProcessorCount;
+        rows = balanced_rows_per_chunk(rg, L.nw, N, K, resident, 2 * K, true);
+    }
     PlanStats st;
     std::vector<LaneDesc> lanes = build_plan(rg, L.nw, N, rows, K, true, &st);
     LaneDesc* dplan;
@@ -53,8 +65,14 @@ int main(int argc, char** argv) {
     CK(hipMemcpy(dplan, lanes.data(), lanes.size() * sizeof(LaneDesc), hipMemcpyHostToDevice));
     hipk::StepParams sp{L.pitch, (i32)L.h, (i32)L.nw, L.R, flags};
     const int steps = gens / K;
+    auto launch = [&](const u64* s, u64* d) {
+        if (tile_nw > 0)
+            hipk::launch_step_tile(tile_nw, K, s, d, dplan, st.waves, rows, sp, 0);
+        else
+            hipk::launch_step(K, s, d, dplan, st.waves, sp, 0);
+    };
     for (int w = 0; w < 4; ++w) {
-        hipk::launch_step(K, a, b, dplan, st.waves, sp, 0);
+        launch(a, b);
         std::swap(a, b);
     }
     CK(hipDeviceSynchronize());
@@ -65,7 +83,7 @@ int main(int argc, char** argv) {
     for (int rep = 0; rep < 3; ++rep) {
         CK(hipEventRecord(e0, 0));
         for (int s = 0; s < steps; ++s) {
-            hipk::launch_step(K, a, b, dplan, st.waves, sp, 0);
+            launch(a, b);
             std::swap(a, b);
         }
         CK(hipEventRecord(e1, 0));
@@ -76,9 +94,10 @@ int main(int argc, char** argv) {
     }
     CK(hipGetLastError());
     const double per_gen_us = best * 1e3 / (steps * K);
-    printf("{\"N\": %lld, \"K\": %d, \"skew\": %d, \"pf\": %d, \"rows\": %lld, \"waves\": %lld, \"blocks_per_cu\": %d, "
-           "\"us_per_gen\": %.3f, \"cells_per_s\": %.4e}\n",
-           (long long)N, K, skew, pf, (long long)rows, (long long)st.waves, hipk::step_blocks_per_cu(K, flags), per_gen_us,
+    const int bpc = tile_nw > 0 ? hipk::tile_blocks_per_cu(tile_nw, rows, K, flags) : hipk::step_blocks_per_cu(K, flags);
+    printf("{\"N\": %lld, \"K\": %d, \"skew\": %d, \"pf\": %d, \"tile_nw\": %d, \"rows\": %lld, \"waves\": %lld, "
+           "\"blocks_per_cu\": %d, \"us_per_gen\": %.3f, \"cells_per_s\": %.4e}\n",
+           (long long)N, K, skew, pf, tile_nw, (long long)rows, (long long)st.waves, bpc, per_gen_us,
            (double)N * N / (per_gen_us * 1e-6));
     return 0;
 }
