@@ -131,6 +131,7 @@ def main() -> int:
                 "backend": backend,
                 "halo_depth": st["depth"],
                 "kernel": st["kernel"],
+                "schedule": st["schedule"],
                 "graph_launches": st["graph_launches"],
                 "plan_waves": st["plan_waves"],
                 "lane_efficiency": round(st["lane_efficiency"], 4),

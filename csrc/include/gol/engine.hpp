@@ -47,6 +47,9 @@ struct EngineConfig {
     bool profile = false;             // per-phase event timing
     int graph_supersteps = 0;         // supersteps per captured graph (0 = auto, even)
     double watchdog_s = 0;            // abort the job after this long without progress (0 = off)
+    int edge_cus = 0;                 // >0: CU-partitioned edge-stream schedule (experimental, opt-in)
+    bool force_split = false;         // run the interior/boundary edge schedule even without neighbours
+    std::string sched = "auto";       // with neighbours: auto (timed at init) | split (overlap) | full
 };
 
 struct EngineStats {
@@ -61,6 +64,7 @@ struct EngineStats {
     double t_exchange_ms = 0;  // profile only
     double t_compute_ms = 0;   // profile only
     std::string kernel;        // stencil kernel in use (HIP: temporal | tile | lds; CPU: cpu)
+    std::string schedule;      // superstep schedule: local (no neighbours) | split | full
 };
 
 class Engine {

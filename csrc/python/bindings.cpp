@@ -103,6 +103,7 @@ py::dict stats_dict(const EngineStats& s) {
     d["t_exchange_ms"] = s.t_exchange_ms;
     d["t_compute_ms"] = s.t_compute_ms;
     d["kernel"] = s.kernel;
+    d["schedule"] = s.schedule;
     return d;
 }
 
@@ -241,7 +242,10 @@ PYBIND11_MODULE(_gol, m) {
         .def_readwrite("profile", &EngineConfig::profile)
         .def_readwrite("graph_supersteps", &EngineConfig::graph_supersteps)
         .def_readwrite("watchdog_s", &EngineConfig::watchdog_s)
-        .def_readwrite("tile_waves", &EngineConfig::tile_waves);
+        .def_readwrite("tile_waves", &EngineConfig::tile_waves)
+        .def_readwrite("edge_cus", &EngineConfig::edge_cus)
+        .def_readwrite("force_split", &EngineConfig::force_split)
+        .def_readwrite("sched", &EngineConfig::sched);
 
     py::class_<Engine>(m, "Engine")
         .def_static(

@@ -112,6 +112,7 @@ void Engine::init(const PatternSpec& p) {
     stats_ = EngineStats{};
     stats_.depth = L_.R;
     stats_.kernel = backend_name() == "cpu" ? "cpu" : cfg_.kernel;
+    stats_.schedule = halo_items(L_.R).empty() ? "local" : "full";
     do_init(p);
     if (cfg_.compat) setup_compat();
 }

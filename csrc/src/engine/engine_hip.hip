@@ -2,8 +2,14 @@
 //
 // Board memory: two bit-packed tiles in HBM (hipMalloc, never managed memory — the reference
 // migrates managed pages host<->device every generation, gol-with-cuda.cu:35-51 + gol-main.c:97-100).
-// Streams: s_comp (kernels) and s_comm (halo exchange).  Per superstep with neighbours:
-//     s_comm:  wait(ev_ready) -> pack (2-D) -> RCCL group send/recv (or host staging) -> unpack -> ev_halo
+// Streams: s_comp (kernels) and s_comm (halo exchange).  Per superstep s with neighbours:
+//   edge mode (device transport, overlap; the default for multi-GPU RCCL runs) — s_comm owns a
+//   private CU partition (hipExtStreamCreateWithCUMask, GOL_EDGE_CUS):
+//     s_comp:  wait(B(s-1)) -> interior I(s) -> ev_int
+//     s_comm:  pack -> RCCL group send/recv H(s) -> unpack -> wait(I(s-1)) -> boundary B(s) -> ev_bnd
+//     so the exchange and the boundary bands run concurrently with the interior of the same superstep.
+//   otherwise (host-staged halos):
+//     s_comm:  wait(ev_ready) -> pack (2-D) -> host staging exchange -> unpack -> ev_halo
 //     s_comp:  interior kernel -> wait(ev_halo) -> boundary kernel -> ev_ready
 // With graphs on, G/(m*k) captures of m supersteps (m even => parity preserved) are replayed.
 #include <hip/hip_runtime.h>
@@ -84,18 +90,84 @@ class HipEngine : public Engine {
             HIP_CHECK(hipMemset(buf_[i], 0, bytes));
         }
         alloc_bytes_ = bytes;
-        HIP_CHECK(hipStreamCreateWithFlags(&s_comp_, hipStreamNonBlocking));
-        HIP_CHECK(hipStreamCreateWithFlags(&s_comm_, hipStreamNonBlocking));
+        device_transport_ = t_->device_buffers() && cfg_.transport != "host";
+        if (cfg_.transport == "device" && !t_->device_buffers())
+            throw Error("GOL_TRANSPORT=device needs a device transport (RCCL)");
+        // Edge-stream schedule (multi-GPU with a device transport): halo exchange + boundary bands
+        // run on their own stream, concurrently with the interior of the same superstep.
+        // Opt-in (GOL_EDGE_CUS > 0): measured on MI355X, a CU-masked compute stream runs the
+        // interior ~20% slower, which costs more than the partition saves (docs/PERFORMANCE.md).
+        for (auto& kk : kern_) kk = kernel_;
+        edge_mode_ = cfg_.edge_cus > 0 && cfg_.overlap && !cfg_.compat && !cfg_.profile && kernel_ != "lds" &&
+                     can_overlap() && !(self_x() && !L_.aligned()) &&
+                     ((device_transport_ && !halo_items(L_.R).empty()) || cfg_.force_split);
+        create_streams();
         HIP_CHECK(hipEventCreateWithFlags(&ev_ready_, hipEventDisableTiming));
         HIP_CHECK(hipEventCreateWithFlags(&ev_halo_, hipEventDisableTiming));
+        HIP_CHECK(hipEventCreateWithFlags(&ev_int_, hipEventDisableTiming));
+        HIP_CHECK(hipEventCreateWithFlags(&ev_bnd_, hipEventDisableTiming));
         if (cfg_.profile) {
             for (auto* e : {&ev_t0_, &ev_t1_, &ev_t2_, &ev_t3_}) HIP_CHECK(hipEventCreate(e));
         }
         HIP_CHECK(hipMalloc(&d_red_, 2 * sizeof(u64)));
         HIP_CHECK(hipHostMalloc(&h_red_, 2 * sizeof(u64), hipHostMallocDefault));
-        device_transport_ = t_->device_buffers() && cfg_.transport != "host";
-        if (cfg_.transport == "device" && !t_->device_buffers())
-            throw Error("GOL_TRANSPORT=device needs a device transport (RCCL)");
+    }
+
+    // The compute stream and the comm/edge stream.  In edge mode the edge stream gets a private
+    // partition of `edge_cus` CUs (hipExtStreamCreateWithCUMask) and the compute stream the rest:
+    // a one-round interior plan fills every VGPR slot of its CUs, so without a partition the RCCL
+    // kernels and the boundary bands could not become resident until the interior retires, and
+    // the exchange would serialise behind it.
+    void create_streams() {
+        comp_cus_ = cus_;
+        edge_cus_ = 0;
+        const int want = cfg_.edge_cus;
+        if (edge_mode_ && want > 0 && want <= cus_ / 4) {
+            // Workgroups are dispatched round-robin over the XCDs, so both partitions must span
+            // every XCD (a partition missing from one XCD makes that XCD the straggler).  Pick
+            // c = x*per + (per-1 - 8r - x) for XCD x and round r: one CU per XCD per round whether
+            // the mask numbers CUs XCD-major (c / per) or XCD-interleaved (c % 8).
+            const int xcds = 8, per = cus_ / xcds;
+            const int words = (cus_ + 31) / 32;
+            std::vector<uint32_t> mc(words, 0), me(words, 0);
+            std::vector<char> edge(cus_, 0);
+            int picked = 0;
+            for (int r = 0; picked < want && r < per / xcds; ++r)
+                for (int x = 0; x < xcds && picked < want; ++x, ++picked) edge[x * per + (per - 1 - 8 * r - x)] = 1;
+            if (cus_ % xcds) picked = 0;  // unexpected topology: fall back to the plain layout
+            for (int c = 0; c < cus_; ++c) (edge[c] ? me : mc)[c / 32] |= 1u << (c % 32);
+            if (picked != want) {
+                std::fill(me.begin(), me.end(), 0);
+                std::fill(mc.begin(), mc.end(), 0);
+                for (int c = 0; c < cus_; ++c) (c >= cus_ - want ? me : mc)[c / 32] |= 1u << (c % 32);
+            }
+            if (hipExtStreamCreateWithCUMask(&s_comp_, (uint32_t)words, mc.data()) == hipSuccess &&
+                hipExtStreamCreateWithCUMask(&s_comm_, (uint32_t)words, me.data()) == hipSuccess) {
+                comp_cus_ = cus_ - want;
+                edge_cus_ = want;
+                return;
+            }
+            hipGetLastError();
+            if (s_comp_) hipStreamDestroy(s_comp_);
+            s_comp_ = nullptr;
+            fprintf(stderr, "[gol] CU-masked streams unavailable; edge stream shares all CUs\n");
+        }
+        HIP_CHECK(hipStreamCreateWithFlags(&s_comp_, hipStreamNonBlocking));
+        HIP_CHECK(hipStreamCreateWithFlags(&s_comm_, hipStreamNonBlocking));
+    }
+
+    // CUs a plan of this kind runs on (resident-wave budget of its one-round balance).
+    int plan_cus(int kind) const {
+        if (kind == 2 && edge_mode_) return edge_cus_ > 0 ? edge_cus_ : cus_;
+        return comp_cus_;
+    }
+
+    // Every buffer-writing operation on the compute stream ends with this: the next superstep's
+    // waits (ready / interior / boundary) all see completed work.
+    void mark_ready() {
+        HIP_CHECK(hipEventRecord(ev_ready_, s_comp_));
+        HIP_CHECK(hipEventRecord(ev_int_, s_comp_));
+        HIP_CHECK(hipEventRecord(ev_bnd_, s_comp_));
     }
 
     ~HipEngine() override {
@@ -116,6 +188,8 @@ class HipEngine : public Engine {
         hipHostFree(h_red_);
         hipEventDestroy(ev_ready_);
         hipEventDestroy(ev_halo_);
+        hipEventDestroy(ev_int_);
+        hipEventDestroy(ev_bnd_);
         for (auto e : fence_ev_)
             if (e) hipEventDestroy(e);
         for (auto e : {ev_sync_comm_, ev_sync_comp_})
@@ -170,7 +244,7 @@ class HipEngine : public Engine {
         HIP_CHECK(hipMemcpy2D(buf_[cur_] + L_.index(0, 0), (size_t)L_.pitch * 8, m.data(), (size_t)L_.nw * 8,
                               (size_t)L_.nw * 8, (size_t)L_.h, hipMemcpyHostToDevice));
         post(buf_[cur_], s_comp_);
-        HIP_CHECK(hipEventRecord(ev_ready_, s_comp_));
+        mark_ready();
         synchronize();
     }
 
@@ -199,6 +273,9 @@ class HipEngine : public Engine {
                 trace::Range r("gol.graph_launch");
                 HIP_CHECK(hipGraphLaunch(exec, s_comp_));
             }
+            // Events recorded during capture are not re-recorded by replays: re-mark them after
+            // the graph so later eager supersteps (and the comm stream) wait for its work.
+            mark_ready();
             gen_ += per;
             generations -= per;
             stats_.generations += per;
@@ -239,14 +316,17 @@ class HipEngine : public Engine {
         }
         post(buf_[cur_], s_comp_);
         HIP_CHECK(hipGetLastError());
-        HIP_CHECK(hipEventRecord(ev_ready_, s_comp_));
+        mark_ready();
         synchronize();
         if (dcells) HIP_CHECK(hipFree(dcells));
-        if (cfg_.kernel == "auto" && !tuned_) {
-            autotune_kernel();
+        split_ = split_used() && (cfg_.sched == "auto" || cfg_.sched == "split");
+        if (!tuned_) {
+            if (cfg_.kernel == "auto") autotune_kernel();
+            autotune_schedule();
             tuned_ = true;
         }
-        stats_.kernel = kernel_;
+        stats_.kernel = split_ ? kern_[1] + "+boundary:" + kern_[2] : kern_[0];
+        stats_.schedule = split_ ? "split" : (halo_items(L_.R).empty() ? "local" : "full");
         // Build the plans for every depth a run can use (remainder supersteps included) now, so
         // neither graph capture nor a timed loop ever builds or uploads a plan.
         for (int k = 1; k <= (cfg_.compat ? 1 : L_.R); ++k)
@@ -258,12 +338,35 @@ class HipEngine : public Engine {
     }
 
     void do_superstep(int k) override {
+        run_superstep(k, split_);
+        cur_ ^= 1;
+    }
+
+    // One superstep buf[cur] -> buf[cur^1] (the caller flips the parity).  `split`: interior +
+    // boundary bands with the exchange overlapped (else exchange, then one full-tile kernel).
+    void run_superstep(int k, bool split) {
         prepare(k);
         u64* src = buf_[cur_];
         u64* dst = buf_[cur_ ^ 1];
         const std::vector<HaloItem>& items = items_for(k);
         const bool prof = cfg_.profile;
-        if (cfg_.compat || items.empty()) {
+        if (edge_mode_ && split) {
+            // I(s) interior on the compute stream, H(s) exchange + B(s) boundary on the edge
+            // stream, concurrently.  I(s) needs B(s-1) (its input rows and its output buffer);
+            // B(s) needs H(s) and I(s-1).  The waits are issued before this superstep re-records
+            // the events, so they refer to superstep s-1.
+            HIP_CHECK(hipStreamWaitEvent(s_comp_, ev_bnd_, 0));
+            launch(1, k, src, dst, s_comp_);
+            if (!items.empty()) exchange_device(k, items, cur_, s_comm_);
+            HIP_CHECK(hipStreamWaitEvent(s_comm_, ev_int_, 0));
+            launch(2, k, src, dst, s_comm_);
+            HIP_CHECK(hipEventRecord(ev_bnd_, s_comm_));
+            HIP_CHECK(hipEventRecord(ev_int_, s_comp_));
+            HIP_CHECK(hipStreamWaitEvent(s_comp_, ev_bnd_, 0));  // join: s_comp holds the whole board
+            HIP_CHECK(hipEventRecord(ev_ready_, s_comp_));
+            return;
+        }
+        if (cfg_.compat || (items.empty() && !cfg_.force_split)) {
             if (prof) HIP_CHECK(hipEventRecord(ev_t2_, s_comp_));
             launch(0, k, src, dst, s_comp_);
             post(dst, s_comp_);
@@ -274,8 +377,14 @@ class HipEngine : public Engine {
                 HIP_CHECK(hipEventElapsedTime(&ms, ev_t2_, ev_t3_));
                 stats_.t_compute_ms += ms;
             }
-        } else if (cfg_.overlap && can_overlap()) {
-            if (device_transport_) {
+        } else if (split) {
+            if (items.empty()) {
+                // GOL_FORCE_SPLIT on a rank without neighbours: the multi-GPU stream structure
+                // with an empty exchange (measures the split schedule's own cost on one GPU)
+                HIP_CHECK(hipStreamWaitEvent(s_comm_, ev_ready_, 0));
+                HIP_CHECK(hipEventRecord(ev_halo_, s_comm_));
+                launch(1, k, src, dst, s_comp_);
+            } else if (device_transport_) {
                 HIP_CHECK(hipStreamWaitEvent(s_comm_, ev_ready_, 0));
                 if (prof) HIP_CHECK(hipEventRecord(ev_t0_, s_comm_));
                 exchange_device(k, items, cur_, s_comm_);
@@ -310,8 +419,35 @@ class HipEngine : public Engine {
             post(dst, s_comp_);
             if (prof) record_profile(true);
         }
-        HIP_CHECK(hipEventRecord(ev_ready_, s_comp_));
-        cur_ ^= 1;
+        mark_ready();
+    }
+
+    // With neighbours, pick the superstep schedule by measurement: every rank times a few
+    // supersteps of each schedule on the scratch buffer (the exchange writes the same halo rows a
+    // real superstep would, the kernels write the scratch buffer; parity is not flipped), and the
+    // schedule with the smaller max-over-ranks time wins.  Split overlaps the exchange with the
+    // interior but pays a serial boundary kernel and cross-stream waits; full pays the exchange
+    // latency.  Which is cheaper depends on the tile size and the link latency.
+    void autotune_schedule() {
+        if (!split_ || halo_items(L_.R).empty() || cfg_.sched != "auto") return;
+        const int k = L_.R;
+        double t[2] = {0, 0};
+        for (int m = 0; m < 2; ++m) {
+            const bool sp = m == 0;
+            run_superstep(k, sp);  // warm-up: RCCL connections, plans, code objects
+            synchronize();
+            t_->barrier();
+            const auto t0 = std::chrono::steady_clock::now();
+            for (int i = 0; i < 4; ++i) run_superstep(k, sp);
+            synchronize();
+            const double dt = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+            t[m] = t_->allreduce_max(dt);
+        }
+        split_ = t[0] <= t[1];
+        sched_ms_[0] = t[0] * 250.0;  // ms per superstep
+        sched_ms_[1] = t[1] * 250.0;
+        stats_.exchanges = 0;  // the timing exchanges are not part of the run
+        stats_.halo_bytes = 0;
     }
 
     void do_set_compat_halos(const std::vector<u64>& above, const std::vector<u64>& below) override {
@@ -325,7 +461,7 @@ class HipEngine : public Engine {
                 hipk::launch_fill_ghost_cols(buf_[i], L_, L_.h, L_.h + 1, s_comp_);
             }
         }
-        HIP_CHECK(hipEventRecord(ev_ready_, s_comp_));
+        mark_ready();
         synchronize();
     }
 
@@ -356,38 +492,50 @@ class HipEngine : public Engine {
         return f;
     }
 
-    bool tile_kernel() const { return kernel_ == "tile"; }
+    bool tile_kernel(int kind) const { return kern_[kind] == "tile"; }
 
-    // GOL_KERNEL=auto: time one full-tile superstep of each candidate kernel (into the scratch
-    // buffer, so the board is untouched) and keep the faster one.  The register pipeline wins on
-    // big tiles; the LDS-resident tile kernel on small ones (its vertical halo is shared by a whole
-    // workgroup), e.g. a strong-scaled board's strips.
+    // Whether supersteps use the interior (kind 1) / boundary (kind 2) split.
+    bool split_used() const {
+        return !cfg_.compat && cfg_.overlap && can_overlap() && (!halo_items(L_.R).empty() || cfg_.force_split);
+    }
+
+    // GOL_KERNEL=auto: for every plan kind a run uses (full tile; interior + boundary bands when
+    // split), time one superstep of each candidate kernel (into the scratch buffer, so the board is
+    // untouched) and keep the faster one.  The register pipeline wins on big regions; the
+    // LDS-resident tile kernel on small ones — its vertical halo is shared by a whole workgroup and
+    // its dependency chains are short, which is what the k-row boundary bands need.
     void autotune_kernel() {
         const int k = cfg_.compat ? 1 : L_.R;
-        float best = 1e30f;
-        std::string pick = "temporal";
         hipEvent_t e0, e1;
         HIP_CHECK(hipEventCreate(&e0));
         HIP_CHECK(hipEventCreate(&e1));
-        for (const char* cand : {"temporal", "tile"}) {
-            kernel_ = cand;
-            if (kernel_ == "tile" && hipk::tile_max_rows(k) < 1) continue;
-            launch(0, k, buf_[cur_], buf_[cur_ ^ 1], s_comp_);  // warm-up (and plan build)
-            HIP_CHECK(hipEventRecord(e0, s_comp_));
-            for (int i = 0; i < 3; ++i) launch(0, k, buf_[cur_], buf_[cur_ ^ 1], s_comp_);
-            HIP_CHECK(hipEventRecord(e1, s_comp_));
-            HIP_CHECK(hipEventSynchronize(e1));
-            float ms = 0;
-            HIP_CHECK(hipEventElapsedTime(&ms, e0, e1));
-            tune_ms_[kernel_] = ms / 3;
-            if (ms < best) {
-                best = ms;
-                pick = kernel_;
+        std::vector<int> kinds = {0};
+        if (split_used()) kinds = {0, 1, 2};
+        for (int kind : kinds) {
+            float best = 1e30f;
+            std::string pick = "temporal";
+            hipStream_t s = (kind == 2 && edge_mode_) ? s_comm_ : s_comp_;
+            for (const char* cand : {"temporal", "tile"}) {
+                kern_[kind] = cand;
+                if (kern_[kind] == "tile" && hipk::tile_max_rows(k) < 1) continue;
+                launch(kind, k, buf_[cur_], buf_[cur_ ^ 1], s);  // warm-up (and plan build)
+                HIP_CHECK(hipEventRecord(e0, s));
+                for (int i = 0; i < 3; ++i) launch(kind, k, buf_[cur_], buf_[cur_ ^ 1], s);
+                HIP_CHECK(hipEventRecord(e1, s));
+                HIP_CHECK(hipEventSynchronize(e1));
+                float ms = 0;
+                HIP_CHECK(hipEventElapsedTime(&ms, e0, e1));
+                tune_ms_[strprintf("%d:%s", kind, cand)] = ms / 3;
+                if (ms < best) {
+                    best = ms;
+                    pick = cand;
+                }
             }
+            kern_[kind] = pick;
         }
         HIP_CHECK(hipEventDestroy(e0));
         HIP_CHECK(hipEventDestroy(e1));
-        kernel_ = pick;
+        kernel_ = kern_[0];
     }
 
     bool can_overlap() const {
@@ -418,20 +566,20 @@ class HipEngine : public Engine {
     }
 
     const DevPlan& plan(int kind, int k) {
-        const int key = (tile_kernel() ? 100000 : 0) + kind * 1000 + k;
+        const int key = (tile_kernel(kind) ? 100000 : 0) + kind * 1000 + k;
         auto it = plans_.find(key);
         if (it != plans_.end()) return it->second;
         std::vector<Region> rg = regions(kind, k);
         DevPlan p;
         i64 rows = cfg_.rows_per_wave;
-        if (tile_kernel()) {
+        if (tile_kernel(kind)) {
             // step_tile: one workgroup per plan wave, one tile per CU per round; rows are capped by
             // the 160 KiB of LDS (double-buffered tile + 2k halo rows), extra rounds beyond that
             const i64 rmax = hipk::tile_max_rows(k);
             if (rmax < 1) throw Error(strprintf("GOL_KERNEL=tile: depth %d leaves no LDS rows", k));
             if (rows > rmax) rows = rmax;
             for (i64 rounds = 1; rows <= 0; ++rounds) {
-                const i64 r = balanced_rows_per_chunk(rg, L_.nw, L_.h, k, rounds * cus_, 1, xwrap_by_plan());
+                const i64 r = balanced_rows_per_chunk(rg, L_.nw, L_.h, k, rounds * plan_cus(kind), 1, xwrap_by_plan());
                 if (r <= rmax) rows = r;
             }
         } else {
@@ -439,7 +587,7 @@ class HipEngine : public Engine {
                 rows = choose_rows_per_chunk(rg, k, cfg_.waves_target, 4 * (i64)k);
             if (rows <= 0) {
                 // one full round of resident waves (occupancy of this kernel instantiation)
-                const i64 resident = (i64)hipk::step_blocks_per_cu(k, step_flags()) * kWavesPerBlock * cus_;
+                const i64 resident = (i64)hipk::step_blocks_per_cu(k, step_flags()) * kWavesPerBlock * plan_cus(kind);
                 rows = balanced_rows_per_chunk(rg, L_.nw, L_.h, k, resident, 2 * (i64)k, xwrap_by_plan());
             }
         }
@@ -460,7 +608,7 @@ class HipEngine : public Engine {
             const DevPlan& p = plan(kind, k);
             if (p.st.out_words == 0) return;
             hipk::StepParams sp{L_.pitch, (i32)L_.h, (i32)L_.nw, L_.R, step_flags()};
-            if (tile_kernel())
+            if (tile_kernel(kind))
                 hipk::launch_step_tile(cfg_.tile_waves, k, src, dst, p.d, p.waves, p.rows, sp, s);
             else
                 hipk::launch_step(k, src, dst, p.d, p.waves, sp, s);
@@ -611,7 +759,7 @@ class HipEngine : public Engine {
         const int cur0 = cur_;
         try {
             HIP_CHECK(hipStreamBeginCapture(s_comp_, hipStreamCaptureModeRelaxed));
-            HIP_CHECK(hipEventRecord(ev_ready_, s_comp_));  // fork point for the comm stream
+            mark_ready();  // fork points for the comm stream, recorded inside the capture
             for (int i = 0; i < m; ++i) do_superstep(k);
             HIP_CHECK(hipStreamEndCapture(s_comp_, &graph));
             HIP_CHECK(hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0));
@@ -624,7 +772,7 @@ class HipEngine : public Engine {
             cur_ = cur0;
             graph_ok_ = false;
             fprintf(stderr, "[gol] hipGraph capture disabled: %s\n", e.what());
-            HIP_CHECK(hipEventRecord(ev_ready_, s_comp_));
+            mark_ready();
             return nullptr;
         }
         if (cur_ != cur0) throw Error("graph capture changed the buffer parity");
@@ -658,7 +806,14 @@ class HipEngine : public Engine {
     }
 
     int dev_ = 0, cus_ = 256;
+    bool edge_mode_ = false;       // exchange + boundary on the (CU-partitioned) edge stream
+    int comp_cus_ = 256, edge_cus_ = 0;
+    hipEvent_t ev_int_ = nullptr;  // interior of the last superstep done (compute stream)
+    hipEvent_t ev_bnd_ = nullptr;  // boundary of the last superstep done (edge stream)
     std::string kernel_;  // resolved kernel: temporal | tile | lds (auto resolves at init)
+    std::string kern_[3];  // per plan kind (full / interior / boundary), resolved by autotune
+    bool split_ = false;   // superstep schedule: interior/boundary split with overlapped exchange
+    double sched_ms_[2] = {0, 0};
     bool tuned_ = false;
     std::map<std::string, float> tune_ms_;
     hipEvent_t fence_ev_[kFenceDepth] = {};

@@ -154,6 +154,11 @@ EngineConfig engine_config(const Options& o, const std::string& backend, int dev
     c.profile = o.profile;
     c.graph_supersteps = (int)env_int("GOL_GRAPH_SUPERSTEPS", 0);
     c.watchdog_s = o.watchdog_s;
+    c.edge_cus = (int)env_int("GOL_EDGE_CUS", 0);
+    c.force_split = env_int("GOL_FORCE_SPLIT", 0) != 0;
+    c.sched = env_str("GOL_SCHEDULE", "auto");
+    if (c.sched != "auto" && c.sched != "split" && c.sched != "full")
+        throw Error("GOL_SCHEDULE must be auto, split or full (got " + c.sched + ")");
     return c;
 }
 
@@ -294,6 +299,7 @@ void write_metrics(const Options& o, Engine& eng, const CliArgs& a, double durat
     f << "  \"halo_bytes_rank0\": " << s.halo_bytes << ",\n";
     f << "  \"graph_launches\": " << s.graph_launches << ",\n";
     f << "  \"kernel\": \"" << s.kernel << "\",\n";
+    f << "  \"schedule\": \"" << s.schedule << "\",\n";
     f << "  \"plan_waves\": " << s.plan_waves << ",\n  \"lane_efficiency\": " << s.lane_efficiency << ",\n";
     f << "  \"t_exchange_ms\": " << s.t_exchange_ms << ",\n  \"t_compute_ms\": " << s.t_compute_ms << "\n";
     f << "}\n";

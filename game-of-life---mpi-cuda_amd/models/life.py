@@ -85,6 +85,9 @@ class Simulation:
         profile: bool = False,
         watchdog: float = float(os.environ.get("GOL_WATCHDOG", "0")),
         tile_waves: int = int(os.environ.get("GOL_TILE_WAVES", "8")),
+        edge_cus: int = int(os.environ.get("GOL_EDGE_CUS", "0")),
+        force_split: bool = os.environ.get("GOL_FORCE_SPLIT", "0") == "1",
+        schedule: str = os.environ.get("GOL_SCHEDULE", "auto"),
     ):
         self.transport = transport if transport is not None else _gol.SelfTransport()
         P, rank = self.transport.size(), self.transport.rank()
@@ -105,6 +108,9 @@ class Simulation:
         cfg.profile = profile
         cfg.watchdog_s = float(watchdog)
         cfg.tile_waves = int(tile_waves)
+        cfg.edge_cus = int(edge_cus)
+        cfg.force_split = bool(force_split)
+        cfg.sched = schedule
         if self.backend == "hip":
             n = _gol.hip_device_count()
             if n <= 0:

@@ -46,6 +46,9 @@ def _board(cwd, P):
         (4, {"GOL_GLOBAL": "1", "GOL_DECOMP": "2d", "GOL_GRID": "2x2"}),
         (2, {"GOL_GLOBAL": "1", "GOL_DECOMP": "2d", "GOL_GRID": "2x1", "GOL_OVERLAP": "0"}),
         (3, {"GOL_WATCHDOG": "60"}),
+        (3, {"GOL_SCHEDULE": "full"}),
+        (2, {"GOL_SCHEDULE": "split", "GOL_KERNEL": "tile"}),
+        (4, {"GOL_SCHEDULE": "split", "GOL_GLOBAL": "1", "GOL_DECOMP": "2d", "GOL_GRID": "2x2"}),
     ],
 )
 def test_threads_on_one_gpu_vs_oracle(gol_bin, tmp_path, P, env):

@@ -155,3 +155,16 @@ def test_auto_kernel_choice(gol, N):
     assert s.stats()["kernel"] in ("temporal", "tile")
     s.step(gens)
     assert np.array_equal(s.board(), numpy_step(initial_board(5, N, 1, True, N), gens))
+
+
+@pytest.mark.parametrize("kernel", ["temporal", "tile"])
+@pytest.mark.parametrize("graph", [True, False])
+@pytest.mark.parametrize("edge_cus", [8, 0])
+def test_edge_stream_schedule(gol, kernel, graph, edge_cus):
+    """Interior on the compute stream + boundary bands on the CU-partitioned edge stream
+    (the multi-GPU schedule, forced on one rank) is exact."""
+    N, gens = 1024, 8 * 36 + 5
+    s = _sim(gol, N, halo_depth=8, kernel=kernel, graph=graph, edge_cus=edge_cus, force_split=True)
+    s.init(5, seed=31)
+    s.step(gens)
+    assert np.array_equal(s.board(), numpy_step(initial_board(5, N, 1, True, 31), gens))
