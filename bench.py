@@ -60,7 +60,22 @@ def main() -> int:
     rank, P, local, cpu_group = init_distributed()
     if P > 1:
         control = torch_transport(cpu_group)
-        transport = rccl_transport(control, group=cpu_group) if backend == "hip" else control
+        transport = control
+        if backend == "hip":
+            import torch
+            import torch.distributed as dist
+
+            rccl = None
+            try:
+                rccl = rccl_transport(control, group=cpu_group)
+            except Exception as e:  # keep the run alive: halos staged through host memory instead
+                print(f"[bench] rank {rank}: RCCL transport unavailable ({e})", file=sys.stderr, flush=True)
+            ok = torch.tensor([1 if rccl is not None else 0], dtype=torch.int32)
+            dist.all_reduce(ok, op=dist.ReduceOp.MIN, group=cpu_group)  # every rank must agree
+            if int(ok.item()) == 1:
+                transport = rccl
+            elif rank == 0:
+                print("[bench] using host-staged halos on every rank", file=sys.stderr, flush=True)
     else:
         transport = native.SelfTransport()
 
@@ -146,7 +161,7 @@ def main() -> int:
     if P > 1:
         import torch.distributed as dist
 
-        dist.barrier()
+        dist.barrier(group=cpu_group)  # gloo: also fine when ranks share a GPU (rehearsal runs)
         dist.destroy_process_group()
     return 0
 
