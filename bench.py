@@ -35,7 +35,10 @@ def main() -> int:
     ap.add_argument("--size", type=int, default=32768, help="tile side per GPU (weak) / board side (strong)")
     ap.add_argument("--scaling", choices=["weak", "strong"], default="weak")
     ap.add_argument("--decomp", default="1d", help="1d | 2d | auto")
-    ap.add_argument("--halo-depth", type=int, default=int(os.environ.get("GOL_HALO_DEPTH", "8")))
+    ap.add_argument("--halo-depth", type=int, default=int(os.environ.get("GOL_HALO_DEPTH", "0")),
+                    help="generations per halo exchange (0 = auto: 8, or 32 for 1-D multi-GPU)")
+    ap.add_argument("--kernel-depth", type=int, default=int(os.environ.get("GOL_KERNEL_DEPTH", "0")),
+                    help="generations per kernel pass (0 = auto)")
     ap.add_argument("--kernel", default=os.environ.get("GOL_KERNEL", "auto"),
                     help="auto (timed at init) | temporal | tile | lds")
     ap.add_argument("--no-graph", action="store_true")
@@ -86,6 +89,7 @@ def main() -> int:
         global_mode=(args.scaling == "strong"),
         decomp=args.decomp,
         halo_depth=args.halo_depth,
+        kernel_depth=args.kernel_depth,
         graph=not args.no_graph,
         overlap=not args.no_overlap,
         kernel=args.kernel,
@@ -145,6 +149,7 @@ def main() -> int:
                 "parallelism": f"{'2d' if dec.Px > 1 else '1d'}-spatial p{P} ({dec.Px}x{dec.Py})",
                 "backend": backend,
                 "halo_depth": st["depth"],
+                "kernel_depth": st["kernel_depth"],
                 "kernel": st["kernel"],
                 "schedule": st["schedule"],
                 "graph_launches": st["graph_launches"],

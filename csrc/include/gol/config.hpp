@@ -33,7 +33,8 @@ struct Options {
     bool global_mode = false;       // GOL_GLOBAL    1: worldSize is the global board side (strong scaling)
     std::string decomp = "1d";      // GOL_DECOMP    1d | 2d | auto
     std::string grid = "";          // GOL_GRID      PxxPy, e.g. 4x2
-    int halo_depth = 8;             // GOL_HALO_DEPTH generations per halo exchange (temporal blocking)
+    int halo_depth = 0;             // GOL_HALO_DEPTH generations per halo exchange (0 = auto)
+    int kernel_depth = 0;           // GOL_KERNEL_DEPTH generations per kernel pass (0 = auto)
     bool graph = true;              // GOL_GRAPH     capture supersteps into hipGraphs
     bool overlap = true;            // GOL_OVERLAP   interior compute overlapped with the halo exchange
     u64 seed = 0x5EED;              // GOL_SEED      pattern 5 seed

@@ -31,7 +31,9 @@ namespace gol {
 
 struct EngineConfig {
     std::string backend = "cpu";      // cpu | hip
-    int halo_depth = 8;               // R: max generations per superstep (clamped to the geometry)
+    int halo_depth = 0;               // R: generations per halo exchange (0 = auto: 8 on one rank,
+                                      // 32 for 1-D multi-rank; clamped to the geometry)
+    int kernel_depth = 0;             // K: generations per kernel pass (0 = auto; HIP)
     bool overlap = true;              // interior/boundary split with comm-stream exchange
     bool graph = true;                // hipGraph capture of superstep pairs
     bool compat = false;              // reference halo quirks (Q1/Q2), 1-D only, k = 1
@@ -58,7 +60,8 @@ struct EngineStats {
     u64 exchanges = 0;
     u64 halo_bytes = 0;       // bytes sent by this rank
     u64 graph_launches = 0;
-    int depth = 0;            // R
+    int depth = 0;            // R (generations per halo exchange)
+    int kernel_depth = 0;     // K (generations per kernel pass)
     i64 plan_waves = 0;       // waves of the full-tile plan
     double lane_efficiency = 0;  // output words / (64 * input rows * waves) for the full plan
     double t_exchange_ms = 0;  // profile only

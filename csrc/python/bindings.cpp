@@ -104,6 +104,7 @@ py::dict stats_dict(const EngineStats& s) {
     d["t_compute_ms"] = s.t_compute_ms;
     d["kernel"] = s.kernel;
     d["schedule"] = s.schedule;
+    d["kernel_depth"] = s.kernel_depth;
     return d;
 }
 
@@ -245,7 +246,8 @@ PYBIND11_MODULE(_gol, m) {
         .def_readwrite("tile_waves", &EngineConfig::tile_waves)
         .def_readwrite("edge_cus", &EngineConfig::edge_cus)
         .def_readwrite("force_split", &EngineConfig::force_split)
-        .def_readwrite("sched", &EngineConfig::sched);
+        .def_readwrite("sched", &EngineConfig::sched)
+        .def_readwrite("kernel_depth", &EngineConfig::kernel_depth);
 
     py::class_<Engine>(m, "Engine")
         .def_static(

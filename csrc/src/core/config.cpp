@@ -64,6 +64,7 @@ Options options_from_env() {
     o.decomp = env_str("GOL_DECOMP", o.decomp);
     o.grid = env_str("GOL_GRID", o.grid);
     o.halo_depth = (int)env_int("GOL_HALO_DEPTH", o.halo_depth);
+    o.kernel_depth = (int)env_int("GOL_KERNEL_DEPTH", o.kernel_depth);
     o.graph = env_flag("GOL_GRAPH", o.graph);
     o.overlap = env_flag("GOL_OVERLAP", o.overlap);
     o.seed = (u64)env_int("GOL_SEED", (long long)o.seed);
@@ -83,7 +84,8 @@ Options options_from_env() {
     o.restart = env_str("GOL_RESTART", "");
     o.watchdog_s = (double)env_int("GOL_WATCHDOG", 0);
     o.verbose = env_flag("GOL_VERBOSE", false);
-    if (o.halo_depth < 1 || o.halo_depth > 64) throw Error("GOL_HALO_DEPTH must be in 1..64");
+    if (o.halo_depth < 0 || o.halo_depth > 64) throw Error("GOL_HALO_DEPTH must be in 1..64 (0 = auto)");
+    if (o.kernel_depth < 0 || o.kernel_depth > 64) throw Error("GOL_KERNEL_DEPTH must be in 1..64 (0 = auto)");
     return o;
 }
 

@@ -61,7 +61,8 @@ std::vector<std::vector<Item>> pack_waves(const std::vector<Region>& regions, i6
     for (const Region& rg : regions) {
         i64 rows = rg.r1 - rg.r0, words = rg.c1 - rg.c0;
         if (rows <= 0 || words <= 0) continue;
-        if (rg.r0 < 0 || rg.r1 > h || rg.c0 < 0 || rg.c1 > nw) throw Error("plan region outside the tile");
+        // rows may extend into the ghost rows (multi-pass supersteps: at most the 64-row halo)
+        if (rg.r0 < -64 || rg.r1 > h + 64 || rg.c0 < 0 || rg.c1 > nw) throw Error("plan region outside the tile");
         i64 nch = ceil_div(rows, rows_per_chunk);
         i64 base = rows / nch, extra = rows % nch;
         i64 r = rg.r0;

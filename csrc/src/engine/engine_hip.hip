@@ -70,17 +70,26 @@ class HipEngine : public Engine {
         cus_ = prop.multiProcessorCount;
         int R = L_.R;
         kernel_ = cfg_.kernel;
+        // Kernel pass depth K (generations per HBM pass) vs halo depth R (generations per
+        // exchange).  In 1-D (and on a single rank) a superstep of R generations runs as several
+        // passes of <= K, the earlier ones also producing the ghost rows the later ones read, so
+        // one exchange serves R generations (communication-avoiding deep halos).  Auto K: R when a
+        // kernel for it exists (<= 16), else 8, the measured optimum of the register pipeline.
+        multipass_ = !cfg_.compat && g_.dec.Px == 1 && kernel_ != "lds";
+        int K = cfg_.kernel_depth > 0 ? cfg_.kernel_depth : (R <= hipk::max_step_depth() ? R : 8);
+        K = std::min(K, R);
         if (kernel_ == "lds") {
-            R = 1;
+            R = K = 1;
         } else if (kernel_ == "tile") {
-            R = std::min(R, 32);  // any depth; LDS rows bound it (tile_max_rows)
+            K = std::min(K, 32);  // any depth; LDS rows bound it (tile_max_rows)
         } else if (kernel_ == "temporal" || kernel_ == "auto") {
             // auto: the depth must suit both candidates (instantiated temporal depths)
-            R = std::min(R, hipk::max_step_depth());
-            while (!hipk::step_depth_supported(R)) --R;
+            K = supported_kernel_depth(std::min(K, hipk::max_step_depth()));
         } else {
             throw Error("GOL_KERNEL must be auto, temporal, tile or lds (got '" + kernel_ + "')");
         }
+        if (!multipass_) R = std::min(R, K);
+        kdepth_ = K;
         if (R != L_.R) L_ = Layout(L_.h, L_.w, R);
         stats_.depth = R;
         // slack rows: the temporal kernel prefetches 3 rows past a segment's last input row
@@ -98,7 +107,8 @@ class HipEngine : public Engine {
         // Opt-in (GOL_EDGE_CUS > 0): measured on MI355X, a CU-masked compute stream runs the
         // interior ~20% slower, which costs more than the partition saves (docs/PERFORMANCE.md).
         for (auto& kk : kern_) kk = kernel_;
-        edge_mode_ = cfg_.edge_cus > 0 && cfg_.overlap && !cfg_.compat && !cfg_.profile && kernel_ != "lds" &&
+        edge_mode_ = cfg_.edge_cus > 0 && L_.R == kdepth_ && cfg_.overlap && !cfg_.compat && !cfg_.profile &&
+                     kernel_ != "lds" &&
                      can_overlap() && !(self_x() && !L_.aligned()) &&
                      ((device_transport_ && !halo_items(L_.R).empty()) || cfg_.force_split);
         create_streams();
@@ -291,7 +301,7 @@ class HipEngine : public Engine {
         Engine::run(generations);
     }
 
-    const DevPlan& full_plan_stats() { return plan(0, L_.R); }
+    const DevPlan& full_plan_stats() { return plan(0, pass_depths(L_.R)[0], ext_after(pass_depths(L_.R), 0)); }
 
    protected:
     void do_init(const PatternSpec& p) override {
@@ -327,39 +337,76 @@ class HipEngine : public Engine {
         }
         stats_.kernel = split_ ? kern_[1] + "+boundary:" + kern_[2] : kern_[0];
         stats_.schedule = split_ ? "split" : (halo_items(L_.R).empty() ? "local" : "full");
+        stats_.kernel_depth = kdepth_;
         // Build the plans for every depth a run can use (remainder supersteps included) now, so
         // neither graph capture nor a timed loop ever builds or uploads a plan.
         for (int k = 1; k <= (cfg_.compat ? 1 : L_.R); ++k)
             if (supported_depth(k) == k) prepare(k);
-        const DevPlan& fp = plan(0, cfg_.compat ? 1 : L_.R);
+        const DevPlan& fp = full_plan_stats();
         stats_.plan_waves = fp.waves;
         stats_.lane_efficiency =
             fp.st.lane_rows ? (double)fp.st.out_words / (double)fp.st.lane_rows : 0.0;
     }
 
     void do_superstep(int k) override {
-        run_superstep(k, split_);
+        const std::vector<int>& ps = pass_depths(k);
+        first_pass(k, ps[0], ext_after(ps, 0), split_);
         cur_ ^= 1;
+        for (size_t j = 1; j < ps.size(); ++j) {
+            // later passes need no halo: the ghost rows computed by the earlier passes carry the
+            // neighbours' cells forward (communication-avoiding deep halos)
+            const i64 e = ext_after(ps, j);
+            launch(0, ps[j], e, buf_[cur_], buf_[cur_ ^ 1], s_comp_);
+            post(buf_[cur_ ^ 1], s_comp_, e);
+            mark_ready();
+            cur_ ^= 1;
+        }
     }
 
-    // One superstep buf[cur] -> buf[cur^1] (the caller flips the parity).  `split`: interior +
-    // boundary bands with the exchange overlapped (else exchange, then one full-tile kernel).
-    void run_superstep(int k, bool split) {
-        prepare(k);
+    // Kernel passes of a superstep of k generations (each <= the kernel depth), and the rows beyond
+    // the tile each pass must still produce for the passes after it (0 when y wraps locally).
+    const std::vector<int>& pass_depths(int k) {
+        auto it = passes_.find(k);
+        if (it != passes_.end()) return it->second;
+        std::vector<int> ps;
+        for (int left = k; left > 0;) {
+            int d = std::min(left, kdepth_);
+            if (kern_[0] != "tile") d = supported_kernel_depth(d);
+            ps.push_back(d);
+            left -= d;
+        }
+        return passes_.emplace(k, ps).first->second;
+    }
+    i64 ext_after(const std::vector<int>& ps, size_t j) const {
+        if (self_y()) return 0;
+        i64 e = 0;
+        for (size_t i = j + 1; i < ps.size(); ++i) e += ps[i];
+        return e;
+    }
+    static int supported_kernel_depth(int want) {
+        while (want > 1 && !hipk::step_depth_supported(want)) --want;
+        return std::max(1, want);
+    }
+
+    // Exchange the kx-deep halo and run the first kernel pass (depth kp, output rows extended by e
+    // beyond the tile): buf[cur] -> buf[cur^1]; the caller flips the parity.  `split`: interior +
+    // boundary bands with the exchange overlapped (else exchange, then one full-region kernel).
+    void first_pass(int kx, int kp, i64 e, bool split) {
+        prepare(kx);
         u64* src = buf_[cur_];
         u64* dst = buf_[cur_ ^ 1];
-        const std::vector<HaloItem>& items = items_for(k);
+        const std::vector<HaloItem>& items = items_for(kx);
         const bool prof = cfg_.profile;
         if (edge_mode_ && split) {
             // I(s) interior on the compute stream, H(s) exchange + B(s) boundary on the edge
             // stream, concurrently.  I(s) needs B(s-1) (its input rows and its output buffer);
             // B(s) needs H(s) and I(s-1).  The waits are issued before this superstep re-records
-            // the events, so they refer to superstep s-1.
+            // the events, so they refer to superstep s-1.  (Single-pass supersteps only.)
             HIP_CHECK(hipStreamWaitEvent(s_comp_, ev_bnd_, 0));
-            launch(1, k, src, dst, s_comp_);
-            if (!items.empty()) exchange_device(k, items, cur_, s_comm_);
+            launch(1, kp, 0, src, dst, s_comp_);
+            if (!items.empty()) exchange_device(kx, items, cur_, s_comm_);
             HIP_CHECK(hipStreamWaitEvent(s_comm_, ev_int_, 0));
-            launch(2, k, src, dst, s_comm_);
+            launch(2, kp, e, src, dst, s_comm_);
             HIP_CHECK(hipEventRecord(ev_bnd_, s_comm_));
             HIP_CHECK(hipEventRecord(ev_int_, s_comp_));
             HIP_CHECK(hipStreamWaitEvent(s_comp_, ev_bnd_, 0));  // join: s_comp holds the whole board
@@ -368,8 +415,8 @@ class HipEngine : public Engine {
         }
         if (cfg_.compat || (items.empty() && !cfg_.force_split)) {
             if (prof) HIP_CHECK(hipEventRecord(ev_t2_, s_comp_));
-            launch(0, k, src, dst, s_comp_);
-            post(dst, s_comp_);
+            launch(0, kp, e, src, dst, s_comp_);
+            post(dst, s_comp_, e);
             if (prof) {
                 HIP_CHECK(hipEventRecord(ev_t3_, s_comp_));
                 HIP_CHECK(hipEventSynchronize(ev_t3_));
@@ -383,40 +430,40 @@ class HipEngine : public Engine {
                 // with an empty exchange (measures the split schedule's own cost on one GPU)
                 HIP_CHECK(hipStreamWaitEvent(s_comm_, ev_ready_, 0));
                 HIP_CHECK(hipEventRecord(ev_halo_, s_comm_));
-                launch(1, k, src, dst, s_comp_);
+                launch(1, kp, 0, src, dst, s_comp_);
             } else if (device_transport_) {
                 HIP_CHECK(hipStreamWaitEvent(s_comm_, ev_ready_, 0));
                 if (prof) HIP_CHECK(hipEventRecord(ev_t0_, s_comm_));
-                exchange_device(k, items, cur_, s_comm_);
+                exchange_device(kx, items, cur_, s_comm_);
                 if (prof) HIP_CHECK(hipEventRecord(ev_t1_, s_comm_));
                 HIP_CHECK(hipEventRecord(ev_halo_, s_comm_));
                 if (prof) HIP_CHECK(hipEventRecord(ev_t2_, s_comp_));
-                launch(1, k, src, dst, s_comp_);
+                launch(1, kp, 0, src, dst, s_comp_);
             } else {
                 if (prof) HIP_CHECK(hipEventRecord(ev_t2_, s_comp_));
-                launch(1, k, src, dst, s_comp_);  // interior first: runs while the host exchanges
+                launch(1, kp, 0, src, dst, s_comp_);  // interior first: runs while the host exchanges
                 HIP_CHECK(hipStreamWaitEvent(s_comm_, ev_ready_, 0));
                 if (prof) HIP_CHECK(hipEventRecord(ev_t0_, s_comm_));
-                exchange_staged(k, items, cur_, s_comm_);
+                exchange_staged(kx, items, cur_, s_comm_);
                 if (prof) HIP_CHECK(hipEventRecord(ev_t1_, s_comm_));
                 HIP_CHECK(hipEventRecord(ev_halo_, s_comm_));
             }
             HIP_CHECK(hipStreamWaitEvent(s_comp_, ev_halo_, 0));
-            launch(2, k, src, dst, s_comp_);
-            post(dst, s_comp_);
+            launch(2, kp, e, src, dst, s_comp_);
+            post(dst, s_comp_, e);
             if (prof) record_profile(true);
         } else {
             if (prof) HIP_CHECK(hipEventRecord(ev_t0_, s_comp_));
             if (device_transport_)
-                exchange_device(k, items, cur_, s_comp_);
+                exchange_device(kx, items, cur_, s_comp_);
             else
-                exchange_staged(k, items, cur_, s_comp_);
+                exchange_staged(kx, items, cur_, s_comp_);
             if (prof) {
                 HIP_CHECK(hipEventRecord(ev_t1_, s_comp_));
                 HIP_CHECK(hipEventRecord(ev_t2_, s_comp_));
             }
-            launch(0, k, src, dst, s_comp_);
-            post(dst, s_comp_);
+            launch(0, kp, e, src, dst, s_comp_);
+            post(dst, s_comp_, e);
             if (prof) record_profile(true);
         }
         mark_ready();
@@ -431,20 +478,23 @@ class HipEngine : public Engine {
     void autotune_schedule() {
         if (!split_ || halo_items(L_.R).empty() || cfg_.sched != "auto") return;
         const int k = L_.R;
+        const std::vector<int>& ps = pass_depths(k);
+        const i64 e0 = ext_after(ps, 0);
         double t[2] = {0, 0};
         for (int m = 0; m < 2; ++m) {
+            // only the exchange + first pass differ between the schedules; later passes are equal
             const bool sp = m == 0;
-            run_superstep(k, sp);  // warm-up: RCCL connections, plans, code objects
+            first_pass(k, ps[0], e0, sp);  // warm-up: RCCL connections, plans, code objects
             synchronize();
             t_->barrier();
             const auto t0 = std::chrono::steady_clock::now();
-            for (int i = 0; i < 4; ++i) run_superstep(k, sp);
+            for (int i = 0; i < 4; ++i) first_pass(k, ps[0], e0, sp);
             synchronize();
             const double dt = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
             t[m] = t_->allreduce_max(dt);
         }
         split_ = t[0] <= t[1];
-        sched_ms_[0] = t[0] * 250.0;  // ms per superstep
+        sched_ms_[0] = t[0] * 250.0;  // ms per (exchange + first pass)
         sched_ms_[1] = t[1] * 250.0;
         stats_.exchanges = 0;  // the timing exchanges are not part of the run
         stats_.halo_bytes = 0;
@@ -476,9 +526,8 @@ class HipEngine : public Engine {
         // Depends on the CONFIGURED kernel only: every rank must cut the same supersteps (the halo
         // exchange sizes follow k), even when GOL_KERNEL=auto resolves differently per rank.
         if (cfg_.kernel == "lds") return 1;
-        if (cfg_.kernel == "tile") return std::max(1, want);
-        while (want > 1 && !hipk::step_depth_supported(want)) --want;
-        return std::max(1, want);
+        if (cfg_.kernel == "tile" || multipass_) return std::max(1, want);  // any depth: passes
+        return supported_kernel_depth(want);
     }
 
    private:
@@ -505,7 +554,7 @@ class HipEngine : public Engine {
     // LDS-resident tile kernel on small ones — its vertical halo is shared by a whole workgroup and
     // its dependency chains are short, which is what the k-row boundary bands need.
     void autotune_kernel() {
-        const int k = cfg_.compat ? 1 : L_.R;
+        const int k = cfg_.compat ? 1 : kdepth_;
         hipEvent_t e0, e1;
         HIP_CHECK(hipEventCreate(&e0));
         HIP_CHECK(hipEventCreate(&e1));
@@ -518,9 +567,9 @@ class HipEngine : public Engine {
             for (const char* cand : {"temporal", "tile"}) {
                 kern_[kind] = cand;
                 if (kern_[kind] == "tile" && hipk::tile_max_rows(k) < 1) continue;
-                launch(kind, k, buf_[cur_], buf_[cur_ ^ 1], s);  // warm-up (and plan build)
+                launch(kind, k, 0, buf_[cur_], buf_[cur_ ^ 1], s);  // warm-up (and plan build)
                 HIP_CHECK(hipEventRecord(e0, s));
-                for (int i = 0; i < 3; ++i) launch(kind, k, buf_[cur_], buf_[cur_ ^ 1], s);
+                for (int i = 0; i < 3; ++i) launch(kind, k, 0, buf_[cur_], buf_[cur_ ^ 1], s);
                 HIP_CHECK(hipEventRecord(e1, s));
                 HIP_CHECK(hipEventSynchronize(e1));
                 float ms = 0;
@@ -545,15 +594,18 @@ class HipEngine : public Engine {
         return true;
     }
 
-    std::vector<Region> regions(int kind, int k) const {
+    // Output regions of a pass of depth k whose output rows extend e rows beyond the tile (into
+    // the ghost rows, 1-D multi-pass supersteps): kind 0 full, 1 interior, 2 boundary bands.
+    std::vector<Region> regions(int kind, int k, i64 e = 0) const {
         const i64 h = L_.h, nw = L_.nw;
         const bool two_d = g_.dec.Px > 1;
-        if (kind == 0 || h <= 2 * (i64)k) return kind == 1 ? std::vector<Region>{} : std::vector<Region>{{0, h, 0, nw}};
+        if (kind == 0 || h <= 2 * (i64)k)
+            return kind == 1 ? std::vector<Region>{} : std::vector<Region>{{-e, h + e, 0, nw}};
         if (kind == 1) {
             if (two_d) return nw > 2 ? std::vector<Region>{{k, h - k, 1, nw - 1}} : std::vector<Region>{};
             return {{k, h - k, 0, nw}};
         }
-        std::vector<Region> r = {{0, k, 0, nw}, {h - k, h, 0, nw}};
+        std::vector<Region> r = {{-e, k, 0, nw}, {h - k, h + e, 0, nw}};
         if (two_d) {
             if (nw > 2) {
                 r.push_back({k, h - k, 0, 1});
@@ -565,11 +617,11 @@ class HipEngine : public Engine {
         return r;
     }
 
-    const DevPlan& plan(int kind, int k) {
-        const int key = (tile_kernel(kind) ? 100000 : 0) + kind * 1000 + k;
+    const DevPlan& plan(int kind, int k, i64 e = 0) {
+        const int key = (tile_kernel(kind) ? 1000000 : 0) + kind * 100000 + (int)e * 100 + k;
         auto it = plans_.find(key);
         if (it != plans_.end()) return it->second;
-        std::vector<Region> rg = regions(kind, k);
+        std::vector<Region> rg = regions(kind, k, e);
         DevPlan p;
         i64 rows = cfg_.rows_per_wave;
         if (tile_kernel(kind)) {
@@ -599,13 +651,13 @@ class HipEngine : public Engine {
         return plans_.emplace(key, p).first->second;
     }
 
-    void launch(int kind, int k, const u64* src, u64* dst, hipStream_t s) {
+    void launch(int kind, int k, i64 e, const u64* src, u64* dst, hipStream_t s) {
         if (kernel_ == "lds") {
             // full-row bands only (the LDS variant is never split by columns: can_overlap)
             for (const Region& r : regions(kind, 1))
                 if (r.c0 == 0) hipk::launch_step_lds(src, dst, L_, r.r0, r.r1, step_flags(), s);
         } else {
-            const DevPlan& p = plan(kind, k);
+            const DevPlan& p = plan(kind, k, e);
             if (p.st.out_words == 0) return;
             hipk::StepParams sp{L_.pitch, (i32)L_.h, (i32)L_.nw, L_.R, step_flags()};
             if (tile_kernel(kind))
@@ -617,8 +669,8 @@ class HipEngine : public Engine {
     }
 
     // Ghost words for widths that are not a multiple of 64 when the tile is its own E/W neighbour.
-    void post(u64* buf, hipStream_t s) {
-        if (self_x() && !L_.aligned()) hipk::launch_fill_ghost_cols(buf, L_, 0, L_.h, s);
+    void post(u64* buf, hipStream_t s, i64 e = 0) {
+        if (self_x() && !L_.aligned()) hipk::launch_fill_ghost_cols(buf, L_, -e, L_.h + e, s);
     }
 
     // ----- halo exchange -----
@@ -629,11 +681,13 @@ class HipEngine : public Engine {
     }
 
     void prepare(int k) {
-        plan(0, k);
+        const std::vector<int>& ps = pass_depths(k);
+        plan(0, ps[0], ext_after(ps, 0));
         if (can_overlap()) {
-            plan(1, k);
-            plan(2, k);
+            plan(1, ps[0]);
+            plan(2, ps[0], ext_after(ps, 0));
         }
+        for (size_t j = 1; j < ps.size(); ++j) plan(0, ps[j], ext_after(ps, j));
         const std::vector<HaloItem>& items = items_for(k);
         if (items.empty()) return;
         // staging buffers sized for the deepest halo (k = R)
@@ -812,6 +866,9 @@ class HipEngine : public Engine {
     hipEvent_t ev_bnd_ = nullptr;  // boundary of the last superstep done (edge stream)
     std::string kernel_;  // resolved kernel: temporal | tile | lds (auto resolves at init)
     std::string kern_[3];  // per plan kind (full / interior / boundary), resolved by autotune
+    int kdepth_ = 8;       // kernel pass depth K (<= halo depth R)
+    bool multipass_ = false;
+    std::map<int, std::vector<int>> passes_;
     bool split_ = false;   // superstep schedule: interior/boundary split with overlapped exchange
     double sched_ms_[2] = {0, 0};
     bool tuned_ = false;

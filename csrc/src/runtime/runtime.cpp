@@ -140,6 +140,7 @@ EngineConfig engine_config(const Options& o, const std::string& backend, int dev
     EngineConfig c;
     c.backend = backend;
     c.halo_depth = o.halo_depth;
+    c.kernel_depth = o.kernel_depth;
     c.overlap = o.overlap;
     c.graph = o.graph;
     c.compat = o.compat;
@@ -295,6 +296,7 @@ void write_metrics(const Options& o, Engine& eng, const CliArgs& a, double durat
     f << "  \"backend\": \"" << eng.backend_name() << "\",\n";
     f << "  \"transport\": \"" << eng.transport().name() << "\",\n";
     f << "  \"halo_depth\": " << s.depth << ",\n";
+    f << "  \"kernel_depth\": " << s.kernel_depth << ",\n";
     f << "  \"supersteps\": " << s.supersteps << ",\n  \"exchanges\": " << s.exchanges << ",\n";
     f << "  \"halo_bytes_rank0\": " << s.halo_bytes << ",\n";
     f << "  \"graph_launches\": " << s.graph_launches << ",\n";

@@ -57,7 +57,9 @@ class Simulation:
     transport:    a ``_gol.Transport``; defaults to a single-rank transport.  See
                   :mod:`gol_amd.parallel` for torch.distributed / RCCL / thread transports.
     backend:      ``"hip"``, ``"cpu"`` or ``"auto"``.
-    halo_depth:   generations per halo exchange (temporal blocking depth, <= 64; HIP caps at 16).
+    halo_depth:   generations per halo exchange (<= 64; 0 = auto: 8, or 32 for 1-D multi-rank).
+    kernel_depth: generations per kernel pass (HIP; 0 = auto).  A superstep of halo_depth
+                  generations runs as several kernel passes in 1-D (communication-avoiding halos).
     decomp/grid:  ``"1d"`` row strips (reference) or ``"2d"`` blocks, optional ``"PxxPy"`` grid.
     compat:       reproduce the reference's halo quirks (frozen gen-0 halos, P<=2 swap).
     watchdog:     seconds without progress before the job is aborted (0 = off; GOL_WATCHDOG).
@@ -72,7 +74,8 @@ class Simulation:
         global_mode: bool = False,
         decomp: str = "1d",
         grid: str = "",
-        halo_depth: int = 8,
+        halo_depth: int = int(os.environ.get("GOL_HALO_DEPTH", "0")),
+        kernel_depth: int = int(os.environ.get("GOL_KERNEL_DEPTH", "0")),
         overlap: bool = True,
         graph: bool = True,
         compat: bool = False,
@@ -97,6 +100,7 @@ class Simulation:
         cfg = _gol.EngineConfig()
         cfg.backend = self.backend
         cfg.halo_depth = halo_depth
+        cfg.kernel_depth = kernel_depth
         cfg.overlap = overlap
         cfg.graph = graph
         cfg.compat = compat

@@ -81,3 +81,22 @@ def test_tile_kernel_multi_rank(gol_bin, tmp_path, env):
     assert r.returncode == 0, r.stderr
     glob = env.get("GOL_GLOBAL") == "1"
     assert np.array_equal(_board(tmp_path, P), numpy_step(initial_board(5, N, P, not glob), gens))
+
+
+@pytest.mark.parametrize(
+    "N,env",
+    [
+        (256, {"GOL_HALO_DEPTH": "32", "GOL_KERNEL_DEPTH": "8"}),
+        (256, {"GOL_HALO_DEPTH": "24", "GOL_KERNEL_DEPTH": "5", "GOL_KERNEL": "tile"}),
+        (200, {"GOL_HALO_DEPTH": "20", "GOL_KERNEL_DEPTH": "6", "GOL_SCHEDULE": "split"}),
+        (200, {"GOL_HALO_DEPTH": "17", "GOL_KERNEL_DEPTH": "4", "GOL_SCHEDULE": "full", "GOL_GRAPH": "0"}),
+        (130, {}),
+    ],
+)
+def test_multipass_deep_halos(gol_bin, tmp_path, N, env):
+    """1-D supersteps of R generations run as several kernel passes that also compute the ghost
+    rows (one exchange per R generations); remainders and unaligned widths included."""
+    P, gens = 3, 101
+    r = _run(gol_bin, [5, N, gens, 256, 1], tmp_path, P, env)
+    assert r.returncode == 0, r.stderr
+    assert np.array_equal(_board(tmp_path, P), numpy_step(initial_board(5, N, P, True), gens))

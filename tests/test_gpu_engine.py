@@ -168,3 +168,12 @@ def test_edge_stream_schedule(gol, kernel, graph, edge_cus):
     s.init(5, seed=31)
     s.step(gens)
     assert np.array_equal(s.board(), numpy_step(initial_board(5, N, 1, True, 31), gens))
+
+
+@pytest.mark.parametrize("R,K", [(32, 8), (24, 6), (13, 4)])
+def test_single_rank_multipass(gol, R, K):
+    N, gens = 512, 3 * R + 7
+    s = _sim(gol, N, halo_depth=R, kernel_depth=K).init(5, seed=R)
+    assert s.stats()["depth"] == R and s.stats()["kernel_depth"] <= K
+    s.step(gens)
+    assert np.array_equal(s.board(), numpy_step(initial_board(5, N, 1, True, R), gens))
