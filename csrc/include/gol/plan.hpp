@@ -15,6 +15,7 @@
 // remainder of a row), so lane utilisation stays high for any width.
 #pragma once
 
+#include <string>
 #include <vector>
 
 #include "gol/common.hpp"
@@ -56,6 +57,12 @@ struct PlanStats {
 // lanes right of word nw-1 stream word 0, so no ghost words are needed.
 std::vector<LaneDesc> build_plan(const std::vector<Region>& regions, i64 nw, i64 h, i64 rows_per_chunk, int k,
                                  bool xwrap, PlanStats* stats = nullptr);
+
+// Bounds check of a plan before it is uploaded (a bad plan would fault the GPU): every lane's word
+// column lies in [-1, nw]; without y-wrap its input rows [row0-k, row0+nrows+k) lie in the
+// allocated rows [-R, h+R); store lanes write rows inside [-R, h+R) and columns in [0, nw).
+// Returns an empty string when the plan is safe, else a description of the first violation.
+std::string validate_plan(const std::vector<LaneDesc>& lanes, i64 nw, i64 h, int R, int k, bool wrap_y);
 
 // Number of waves (padded to whole workgroups) of the plan, without materialising lanes.
 i64 plan_waves(const std::vector<Region>& regions, i64 nw, i64 h, i64 rows_per_chunk);

@@ -149,4 +149,28 @@ std::vector<LaneDesc> build_plan(const std::vector<Region>& regions, i64 nw, i64
     return lanes;
 }
 
+std::string validate_plan(const std::vector<LaneDesc>& lanes, i64 nw, i64 h, int R, int k, bool wrap_y) {
+    if (lanes.size() % kWaveLanes) return "lane count is not a multiple of 64";
+    for (size_t w = 0; w < lanes.size() / kWaveLanes; ++w) {
+        const LaneDesc* L = &lanes[w * kWaveLanes];
+        for (int l = 0; l < kWaveLanes; ++l) {
+            const LaneDesc& d = L[l];
+            if (d.nrows != L[0].nrows) return strprintf("wave %zu: nrows differs between lanes", w);
+            if (d.nrows <= 0) continue;  // padding wave
+            auto bad = [&](const char* what) {
+                return strprintf("wave %zu lane %d (row0 %d col %d nrows %d): %s", w, l, d.row0, d.col, d.nrows, what);
+            };
+            if (d.col < -1 || d.col > nw) return bad("word column outside [-1, nw]");
+            if (!wrap_y && (d.row0 - k < -R || (i64)d.row0 + d.nrows + k > h + R))
+                return bad("input rows outside the allocated halo rows");
+            if (wrap_y && (d.row0 < 0 || (i64)d.row0 + d.nrows > h)) return bad("y-wrapped rows outside the tile");
+            if (d.flags & LANE_STORE) {
+                if (d.col < 0 || d.col >= nw) return bad("store lane outside words [0, nw)");
+                if (d.row0 < -R || (i64)d.row0 + d.nrows > h + R) return bad("store rows outside [-R, h+R)");
+            }
+        }
+    }
+    return "";
+}
+
 }  // namespace gol

@@ -644,6 +644,9 @@ class HipEngine : public Engine {
             }
         }
         std::vector<LaneDesc> lanes = build_plan(rg, L_.nw, L_.h, rows, k, xwrap_by_plan(), &p.st);
+        const std::string bad = validate_plan(lanes, L_.nw, L_.h, L_.R, k, (step_flags() & hipk::STEP_WRAP_Y) != 0);
+        if (!bad.empty()) throw Error(strprintf("refusing to launch an unsafe plan (kind %d, k %d, e %lld): %s", kind, k,
+                                                (long long)e, bad.c_str()));
         p.waves = (i64)lanes.size() / kWaveLanes;
         p.rows = rows;
         HIP_CHECK(hipMalloc(&p.d, lanes.size() * sizeof(LaneDesc)));

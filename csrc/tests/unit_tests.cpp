@@ -128,8 +128,22 @@ static void test_plan() {
             bool all1 = true;
             for (int c : cover) all1 &= c == 1;
             CHECK(all1);
+            CHECK(validate_plan(lanes, nw, 40, 2, 2, false).empty());
         }
     }
+    // multi-pass extension: output rows [-e, h+e) with k-deep inputs inside the R-row halo
+    for (int R : {8, 32}) {
+        for (int k : {1, 4, 8}) {
+            const i64 e = R - k, h = 100, nw = 70;
+            auto lanes = build_plan({{-e, h + e, 0, nw}}, nw, h, 13, k, true);
+            CHECK(validate_plan(lanes, nw, h, R, k, false).empty());
+            CHECK(!validate_plan(lanes, nw, h, R - 1, k, false).empty());  // one row too deep
+        }
+    }
+    // a corrupted lane is reported
+    auto lanes = build_plan({{0, 10, 0, 5}}, 5, 10, 10, 1, false);
+    lanes[3].col = 9;
+    CHECK(!validate_plan(lanes, 5, 10, 1, 1, false).empty());
 }
 
 static void test_cpu_step() {

@@ -1,0 +1,16 @@
+#!/bin/bash
+# Host sanitizer runs of the native core (CPU paths: engines, thread/TCP transports, planner, I/O,
+# watchdog).  GPU sanitizers are not used on this pool; the HIP sources are compiled without them.
+#   bash tools/sanitize_check.sh [address|thread ...]
+set -e
+cd "$(dirname "$0")/.."
+for san in "${@:-address thread}"; do
+  for s in $san; do
+    b=build-san-$s
+    cmake -S . -B $b -DGOL_SANITIZE=$s -DGOL_WITH_PYTHON=OFF -DGOL_WITH_MPI=OFF -DCMAKE_BUILD_TYPE=RelWithDebInfo > $b.log 2>&1
+    cmake --build $b -j8 --target gol_unit >> $b.log 2>&1
+    echo "== $s"
+    if [ $s = thread ]; then export OMP_NUM_THREADS=1 TSAN_OPTIONS="halt_on_error=1"; else export ASAN_OPTIONS="detect_leaks=1"; fi
+    GOL_BACKEND=cpu ./$b/gol_unit | tail -1
+  done
+done
