@@ -247,7 +247,8 @@ PYBIND11_MODULE(_gol, m) {
         .def_readwrite("edge_cus", &EngineConfig::edge_cus)
         .def_readwrite("force_split", &EngineConfig::force_split)
         .def_readwrite("sched", &EngineConfig::sched)
-        .def_readwrite("kernel_depth", &EngineConfig::kernel_depth);
+        .def_readwrite("kernel_depth", &EngineConfig::kernel_depth)
+        .def_readwrite("graph_rccl", &EngineConfig::graph_rccl);
 
     py::class_<Engine>(m, "Engine")
         .def_static(

@@ -275,6 +275,9 @@ class HipEngine : public Engine {
         const u64 per = (u64)m * (u64)k;
         bool local = cfg_.compat || halo_items(k).empty();
         if (!local && !device_transport_) return;  // host-staged exchange cannot be captured
+        // RCCL inside captured graphs is opt-in: with R-deep supersteps (hundreds of us each) the
+        // eager launch cost is negligible, and an eager exchange keeps RCCL's own error handling.
+        if (!local && !cfg_.graph_rccl) return;
         while (generations >= per && graph_ok_) {
             hipGraphExec_t exec = graph_for(k, m);
             if (!exec) break;

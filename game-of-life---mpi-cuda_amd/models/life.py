@@ -115,6 +115,7 @@ class Simulation:
         cfg.edge_cus = int(edge_cus)
         cfg.force_split = bool(force_split)
         cfg.sched = schedule
+        cfg.graph_rccl = os.environ.get("GOL_GRAPH_RCCL", "0") == "1"
         if self.backend == "hip":
             n = _gol.hip_device_count()
             if n <= 0:
