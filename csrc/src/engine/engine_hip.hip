@@ -546,6 +546,17 @@ class HipEngine : public Engine {
 
     bool tile_kernel(int kind) const { return kern_[kind] == "tile"; }
 
+    // Rounds of one-tile-per-CU the LDS tile kernel needs for a plan (cheap estimate, no plan).
+    // Plans are explicit (one descriptor row per tile), so huge boards are left to step_temporal.
+    static constexpr i64 kMaxTileRounds = 16;
+    i64 tile_rounds(int kind, int k, i64 e) const {
+        const i64 rmax = std::max<i64>(1, hipk::tile_max_rows(k));
+        i64 tiles = 0;
+        for (const Region& r : regions(kind, k, e))
+            tiles += ceil_div(r.r1 - r.r0, rmax) * ceil_div(r.c1 - r.c0, (i64)kSegWords);
+        return ceil_div(tiles, (i64)plan_cus(kind));
+    }
+
     // Whether supersteps use the interior (kind 1) / boundary (kind 2) split.
     bool split_used() const {
         return !cfg_.compat && cfg_.overlap && can_overlap() && (!halo_items(L_.R).empty() || cfg_.force_split);
@@ -569,7 +580,8 @@ class HipEngine : public Engine {
             hipStream_t s = (kind == 2 && edge_mode_) ? s_comm_ : s_comp_;
             for (const char* cand : {"temporal", "tile"}) {
                 kern_[kind] = cand;
-                if (kern_[kind] == "tile" && hipk::tile_max_rows(k) < 1) continue;
+                if (kern_[kind] == "tile" && (hipk::tile_max_rows(k) < 1 || tile_rounds(kind, k, 0) > kMaxTileRounds))
+                    continue;  // LDS tiles only pay off for small regions (docs/PERFORMANCE.md)
                 launch(kind, k, 0, buf_[cur_], buf_[cur_ ^ 1], s);  // warm-up (and plan build)
                 HIP_CHECK(hipEventRecord(e0, s));
                 for (int i = 0; i < 3; ++i) launch(kind, k, 0, buf_[cur_], buf_[cur_ ^ 1], s);
@@ -633,9 +645,16 @@ class HipEngine : public Engine {
             const i64 rmax = hipk::tile_max_rows(k);
             if (rmax < 1) throw Error(strprintf("GOL_KERNEL=tile: depth %d leaves no LDS rows", k));
             if (rows > rmax) rows = rmax;
-            for (i64 rounds = 1; rows <= 0; ++rounds) {
-                const i64 r = balanced_rows_per_chunk(rg, L_.nw, L_.h, k, rounds * plan_cus(kind), 1, xwrap_by_plan());
-                if (r <= rmax) rows = r;
+            if (tile_rounds(kind, k, e) > kMaxTileRounds)
+                throw Error(strprintf("GOL_KERNEL=tile: this tile needs %lld rounds of LDS tiles; use the temporal "
+                                      "kernel for boards this large",
+                                      (long long)tile_rounds(kind, k, e)));
+            if (rows <= 0) {
+                const i64 r1 = balanced_rows_per_chunk(rg, L_.nw, L_.h, k, plan_cus(kind), 1, xwrap_by_plan());
+                const i64 rounds = ceil_div(r1, rmax);
+                rows = rounds <= 1 ? r1
+                                   : std::min(rmax, balanced_rows_per_chunk(rg, L_.nw, L_.h, k, rounds * plan_cus(kind), 1,
+                                                                            xwrap_by_plan()));
             }
         } else {
             if (rows <= 0 && cfg_.waves_target > 0)
