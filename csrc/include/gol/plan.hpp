@@ -60,7 +60,8 @@ std::vector<LaneDesc> build_plan(const std::vector<Region>& regions, i64 nw, i64
 
 // Bounds check of a plan before it is uploaded (a bad plan would fault the GPU): every lane's word
 // column lies in [-1, nw]; without y-wrap its input rows [row0-k, row0+nrows+k) lie in the
-// allocated rows [-R, h+R); store lanes write rows inside [-R, h+R) and columns in [0, nw).
+// allocated rows [-R, h+R); store lanes write rows inside [-R, h+R) and columns in [-1, nw]
+// (ghost words are outputs of the earlier passes of a 2-D multi-pass superstep).
 // Returns an empty string when the plan is safe, else a description of the first violation.
 std::string validate_plan(const std::vector<LaneDesc>& lanes, i64 nw, i64 h, int R, int k, bool wrap_y);
 

@@ -61,8 +61,9 @@ std::vector<std::vector<Item>> pack_waves(const std::vector<Region>& regions, i6
     for (const Region& rg : regions) {
         i64 rows = rg.r1 - rg.r0, words = rg.c1 - rg.c0;
         if (rows <= 0 || words <= 0) continue;
-        // rows may extend into the ghost rows (multi-pass supersteps: at most the 64-row halo)
-        if (rg.r0 < -64 || rg.r1 > h + 64 || rg.c0 < 0 || rg.c1 > nw) throw Error("plan region outside the tile");
+        // rows may extend into the ghost rows and columns into the ghost words (multi-pass
+        // supersteps: at most the 64-row halo and the one-word column halo)
+        if (rg.r0 < -64 || rg.r1 > h + 64 || rg.c0 < -1 || rg.c1 > nw + 1) throw Error("plan region outside the tile");
         i64 nch = ceil_div(rows, rows_per_chunk);
         i64 base = rows / nch, extra = rows % nch;
         i64 r = rg.r0;
@@ -138,6 +139,12 @@ std::vector<LaneDesc> build_plan(const std::vector<Region>& regions, i64 nw, i64
                 }
                 if (xwrap && col == -1) col = nw - 1;
                 if (xwrap && col == nw) col = 0;
+                // halo lanes of a segment that includes a ghost word (2-D multi-pass) have no
+                // word further out: stream the ghost word itself.  Its outer bits are garbage
+                // and spread inwards one column per generation, so word 0 / nw-1 stay exact for
+                // supersteps of < 64 generations.
+                if (col < -1) col = -1;
+                if (col > nw) col = nw;
                 L[l] = {(i32)it.r0, (i32)col, f, (i32)nrows};
             }
         }
@@ -165,7 +172,7 @@ std::string validate_plan(const std::vector<LaneDesc>& lanes, i64 nw, i64 h, int
                 return bad("input rows outside the allocated halo rows");
             if (wrap_y && (d.row0 < 0 || (i64)d.row0 + d.nrows > h)) return bad("y-wrapped rows outside the tile");
             if (d.flags & LANE_STORE) {
-                if (d.col < 0 || d.col >= nw) return bad("store lane outside words [0, nw)");
+                if (d.col < -1 || d.col > nw) return bad("store lane outside words [-1, nw]");
                 if (d.row0 < -R || (i64)d.row0 + d.nrows > h + R) return bad("store rows outside [-R, h+R)");
             }
         }

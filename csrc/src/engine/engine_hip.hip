@@ -75,7 +75,7 @@ class HipEngine : public Engine {
         // passes of <= K, the earlier ones also producing the ghost rows the later ones read, so
         // one exchange serves R generations (communication-avoiding deep halos).  Auto K: R when a
         // kernel for it exists (<= 16), else 8, the measured optimum of the register pipeline.
-        multipass_ = !cfg_.compat && g_.dec.Px == 1 && kernel_ != "lds";
+        multipass_ = !cfg_.compat && kernel_ != "lds";
         int K = cfg_.kernel_depth > 0 ? cfg_.kernel_depth : (R <= hipk::max_step_depth() ? R : 8);
         K = std::min(K, R);
         if (kernel_ == "lds") {
@@ -380,8 +380,9 @@ class HipEngine : public Engine {
         }
         return passes_.emplace(k, ps).first->second;
     }
+    // Generations still to run after pass j of a superstep (the "extension" of pass j's output:
+    // that many ghost rows when y has neighbours, plus the ghost words when x has neighbours).
     i64 ext_after(const std::vector<int>& ps, size_t j) const {
-        if (self_y()) return 0;
         i64 e = 0;
         for (size_t i = j + 1; i < ps.size(); ++i) e += ps[i];
         return e;
@@ -611,22 +612,26 @@ class HipEngine : public Engine {
 
     // Output regions of a pass of depth k whose output rows extend e rows beyond the tile (into
     // the ghost rows, 1-D multi-pass supersteps): kind 0 full, 1 interior, 2 boundary bands.
-    std::vector<Region> regions(int kind, int k, i64 e = 0) const {
+    std::vector<Region> regions(int kind, int k, i64 rem = 0) const {
         const i64 h = L_.h, nw = L_.nw;
         const bool two_d = g_.dec.Px > 1;
+        // multi-pass: earlier passes also produce the ghost rows (y neighbours) and the ghost
+        // words, columns -1 and nw (x neighbours), that later passes read
+        const i64 e = self_y() ? 0 : rem;
+        const i64 xe = (!self_x() && rem > 0) ? 1 : 0;
         if (kind == 0 || h <= 2 * (i64)k)
-            return kind == 1 ? std::vector<Region>{} : std::vector<Region>{{-e, h + e, 0, nw}};
+            return kind == 1 ? std::vector<Region>{} : std::vector<Region>{{-e, h + e, -xe, nw + xe}};
         if (kind == 1) {
             if (two_d) return nw > 2 ? std::vector<Region>{{k, h - k, 1, nw - 1}} : std::vector<Region>{};
             return {{k, h - k, 0, nw}};
         }
-        std::vector<Region> r = {{-e, k, 0, nw}, {h - k, h + e, 0, nw}};
+        std::vector<Region> r = {{-e, k, -xe, nw + xe}, {h - k, h + e, -xe, nw + xe}};
         if (two_d) {
             if (nw > 2) {
-                r.push_back({k, h - k, 0, 1});
-                r.push_back({k, h - k, nw - 1, nw});
+                r.push_back({k, h - k, -xe, 1});
+                r.push_back({k, h - k, nw - 1, nw + xe});
             } else {
-                r.push_back({k, h - k, 0, nw});
+                r.push_back({k, h - k, -xe, nw + xe});
             }
         }
         return r;
@@ -694,7 +699,8 @@ class HipEngine : public Engine {
     }
 
     // Ghost words for widths that are not a multiple of 64 when the tile is its own E/W neighbour.
-    void post(u64* buf, hipStream_t s, i64 e = 0) {
+    void post(u64* buf, hipStream_t s, i64 rem = 0) {
+        const i64 e = self_y() ? 0 : rem;
         if (self_x() && !L_.aligned()) hipk::launch_fill_ghost_cols(buf, L_, -e, L_.h + e, s);
     }
 

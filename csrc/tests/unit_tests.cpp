@@ -228,6 +228,12 @@ static void test_engines() {
         for (int g = 0; g < 9; ++g) b = byte_step(b, d.H, d.W);
         CHECK(got == pack(b, d.H, d.W));
     }
+    // deep 2-D supersteps (ghost words recomputed inside a superstep, up to 63 generations)
+    {
+        auto ref = run_engines(256, 1, true, "1d", "", 1, 5, 70, false);
+        CHECK(run_engines(256, 4, true, "2d", "2x2", 63, 5, 70, false) == ref);
+        CHECK(run_engines(256, 2, true, "2d", "2x1", 32, 5, 70, false) == ref);
+    }
     // fingerprint invariance across decompositions
     u64 f1 = 0, f2 = 0, f3 = 0;
     run_engines(256, 1, true, "1d", "", 8, 5, 20, false, &f1);

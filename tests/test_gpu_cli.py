@@ -100,3 +100,23 @@ def test_multipass_deep_halos(gol_bin, tmp_path, N, env):
     r = _run(gol_bin, [5, N, gens, 256, 1], tmp_path, P, env)
     assert r.returncode == 0, r.stderr
     assert np.array_equal(_board(tmp_path, P), numpy_step(initial_board(5, N, P, True), gens))
+
+
+@pytest.mark.parametrize(
+    "N,P,grid,env",
+    [
+        (256, 4, "2x2", {"GOL_HALO_DEPTH": "32", "GOL_KERNEL_DEPTH": "8", "GOL_SCHEDULE": "split"}),
+        (256, 4, "2x2", {"GOL_HALO_DEPTH": "63", "GOL_KERNEL_DEPTH": "8", "GOL_SCHEDULE": "full"}),
+        (256, 2, "2x1", {"GOL_HALO_DEPTH": "24", "GOL_KERNEL_DEPTH": "6"}),
+        (200, 4, "2x2", {"GOL_HALO_DEPTH": "20", "GOL_KERNEL_DEPTH": "4", "GOL_KERNEL": "tile"}),
+        (384, 6, "3x2", {}),
+    ],
+)
+def test_multipass_2d(gol_bin, tmp_path, N, P, grid, env):
+    """2-D supersteps of R generations as several passes: earlier passes also compute the ghost
+    rows and ghost words (one 8-message exchange per R generations)."""
+    gens = 131
+    e = dict(env, GOL_GLOBAL="1", GOL_DECOMP="2d", GOL_GRID=grid)
+    r = _run(gol_bin, [5, N, gens, 256, 1], tmp_path, P, e)
+    assert r.returncode == 0, r.stderr
+    assert np.array_equal(_board(tmp_path, P), numpy_step(initial_board(5, N, P, False), gens))
