@@ -30,6 +30,7 @@ enum : u32 {
     STEP_WRAP_Y = 1u << 1,  // tile is its own N/S neighbour: rows are read modulo h, no ghost rows
     STEP_PF_LDS = 1u << 2,  // temporal kernel: prefetch rows through a per-wave LDS ring (DMA)
     STEP_SKEW = 1u << 3,    // temporal kernel: skewed level pipeline (K independent chains per row)
+    STEP_TILE_L2 = 1u << 4, // tile kernel: two generations per LDS pass (half the barriers)
 };
 
 // Rows the HIP engine allocates past the bottom halo: prefetch / flush overrun (skewed pipeline:

@@ -2,16 +2,14 @@
 //
 // Board memory: two bit-packed tiles in HBM (hipMalloc, never managed memory — the reference
 // migrates managed pages host<->device every generation, gol-with-cuda.cu:35-51 + gol-main.c:97-100).
-// Streams: s_comp (kernels) and s_comm (halo exchange).  Per superstep s with neighbours:
-//   edge mode (device transport, overlap; the default for multi-GPU RCCL runs) — s_comm owns a
-//   private CU partition (hipExtStreamCreateWithCUMask, GOL_EDGE_CUS):
-//     s_comp:  wait(B(s-1)) -> interior I(s) -> ev_int
-//     s_comm:  pack -> RCCL group send/recv H(s) -> unpack -> wait(I(s-1)) -> boundary B(s) -> ev_bnd
-//     so the exchange and the boundary bands run concurrently with the interior of the same superstep.
-//   otherwise (host-staged halos):
-//     s_comm:  wait(ev_ready) -> pack (2-D) -> host staging exchange -> unpack -> ev_halo
-//     s_comp:  interior kernel -> wait(ev_halo) -> boundary kernel -> ev_ready
-// With graphs on, G/(m*k) captures of m supersteps (m even => parity preserved) are replayed.
+// Streams: s_comp (kernels) and s_comm (halo exchange).  A superstep of R generations = one halo
+// exchange + R/K kernel passes (the earlier passes also compute the ghost rows/words the later
+// ones read).  With neighbours, the first pass runs one of two schedules (chosen by measurement):
+//   split:  s_comm:  wait(ev_ready) -> pack (2-D) -> RCCL group send/recv (or host staging) -> unpack -> ev_halo
+//           s_comp:  interior kernel -> wait(ev_halo) -> boundary kernel -> later passes -> ev_ready
+//   full:   s_comp:  exchange -> full-region kernel -> later passes
+//   (opt-in edge mode: boundary bands on a CU-partitioned s_comm, concurrently with the interior)
+// With graphs on, G/(m*R) captures of m supersteps (even pass count => parity preserved) are replayed.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -73,10 +71,11 @@ class HipEngine : public Engine {
         // Kernel pass depth K (generations per HBM pass) vs halo depth R (generations per
         // exchange).  In 1-D (and on a single rank) a superstep of R generations runs as several
         // passes of <= K, the earlier ones also producing the ghost rows the later ones read, so
-        // one exchange serves R generations (communication-avoiding deep halos).  Auto K: R when a
-        // kernel for it exists (<= 16), else 8, the measured optimum of the register pipeline.
+        // one exchange serves R generations (communication-avoiding deep halos).
         multipass_ = !cfg_.compat && kernel_ != "lds";
-        int K = cfg_.kernel_depth > 0 ? cfg_.kernel_depth : (R <= hipk::max_step_depth() ? R : 8);
+        // auto K: 8, the measured optimum of the register pipeline (3 waves/SIMD at 163 VGPRs);
+        // GOL_KERNEL=auto may raise it for the LDS tile kernel (autotune_kernel)
+        int K = cfg_.kernel_depth > 0 ? cfg_.kernel_depth : 8;
         K = std::min(K, R);
         if (kernel_ == "lds") {
             R = K = 1;
@@ -374,7 +373,7 @@ class HipEngine : public Engine {
         std::vector<int> ps;
         for (int left = k; left > 0;) {
             int d = std::min(left, kdepth_);
-            if (kern_[0] != "tile") d = supported_kernel_depth(d);
+            if (cfg_.kernel != "tile") d = supported_kernel_depth(d);  // every kind may be temporal
             ps.push_back(d);
             left -= d;
         }
@@ -542,6 +541,7 @@ class HipEngine : public Engine {
         if (xwrap_by_plan()) f |= hipk::STEP_WRAP_X;
         if (cfg_.prefetch == "lds") f |= hipk::STEP_PF_LDS;
         if (cfg_.pipeline == "skew") f |= hipk::STEP_SKEW;
+        if (tile_l2_) f |= hipk::STEP_TILE_L2;  // tile kernel: 2 generations per LDS pass
         return f;
     }
 
@@ -569,34 +569,59 @@ class HipEngine : public Engine {
     // LDS-resident tile kernel on small ones — its vertical halo is shared by a whole workgroup and
     // its dependency chains are short, which is what the k-row boundary bands need.
     void autotune_kernel() {
-        const int k = cfg_.compat ? 1 : kdepth_;
         hipEvent_t e0, e1;
         HIP_CHECK(hipEventCreate(&e0));
         HIP_CHECK(hipEventCreate(&e1));
-        std::vector<int> kinds = {0};
-        if (split_used()) kinds = {0, 1, 2};
-        for (int kind : kinds) {
-            float best = 1e30f;
-            std::string pick = "temporal";
+        // time one pass of kernel `kern` at depth k on plan `kind`; returns ms per generation
+        auto time_pass = [&](int kind, const char* kern, int k) -> float {
+            kern_[kind] = kern;
+            if (kern_[kind] == "tile" && (hipk::tile_max_rows(k) < 1 || tile_rounds(kind, k, 0) > kMaxTileRounds))
+                return 1e30f;  // LDS tiles only pay off for small regions (docs/PERFORMANCE.md)
+            if (kern_[kind] == "temporal" && !hipk::step_depth_supported(k)) return 1e30f;
             hipStream_t s = (kind == 2 && edge_mode_) ? s_comm_ : s_comp_;
-            for (const char* cand : {"temporal", "tile"}) {
-                kern_[kind] = cand;
-                if (kern_[kind] == "tile" && (hipk::tile_max_rows(k) < 1 || tile_rounds(kind, k, 0) > kMaxTileRounds))
-                    continue;  // LDS tiles only pay off for small regions (docs/PERFORMANCE.md)
-                launch(kind, k, 0, buf_[cur_], buf_[cur_ ^ 1], s);  // warm-up (and plan build)
-                HIP_CHECK(hipEventRecord(e0, s));
-                for (int i = 0; i < 3; ++i) launch(kind, k, 0, buf_[cur_], buf_[cur_ ^ 1], s);
-                HIP_CHECK(hipEventRecord(e1, s));
-                HIP_CHECK(hipEventSynchronize(e1));
-                float ms = 0;
-                HIP_CHECK(hipEventElapsedTime(&ms, e0, e1));
-                tune_ms_[strprintf("%d:%s", kind, cand)] = ms / 3;
-                if (ms < best) {
-                    best = ms;
-                    pick = cand;
-                }
+            launch(kind, k, 0, buf_[cur_], buf_[cur_ ^ 1], s);  // warm-up (and plan build)
+            HIP_CHECK(hipEventRecord(e0, s));
+            for (int i = 0; i < 3; ++i) launch(kind, k, 0, buf_[cur_], buf_[cur_ ^ 1], s);
+            HIP_CHECK(hipEventRecord(e1, s));
+            HIP_CHECK(hipEventSynchronize(e1));
+            float ms = 0;
+            HIP_CHECK(hipEventElapsedTime(&ms, e0, e1));
+            const float per_gen = ms / 3 / (float)k;
+            tune_ms_[strprintf("%d:%s@%d", kind, kern, k)] = per_gen;
+            return per_gen;
+        };
+        // full-tile kernel and pass depth: the register pipeline at the auto depth, the LDS tile
+        // kernel at that depth and (deeper passes amortise its staging) twice that depth
+        const int k0 = cfg_.compat ? 1 : kdepth_;
+        std::vector<std::pair<const char*, int>> cands = {{"temporal", k0}, {"tile", k0}};
+        const int k2 = supported_kernel_depth(std::min({2 * k0, L_.R, 32}));
+        if (!cfg_.compat && cfg_.kernel_depth == 0 && k2 > k0) cands.push_back({"tile", k2});
+        float best = 1e30f;
+        std::pair<const char*, int> pick = cands[0];
+        for (const auto& c : cands) {
+            const float t = time_pass(0, c.first, c.second);
+            if (t < best) {
+                best = t;
+                pick = c;
             }
-            kern_[kind] = pick;
+        }
+        kern_[0] = pick.first;
+        kdepth_ = pick.second;
+        passes_.clear();
+        // interior / boundary plans of split supersteps, at the chosen pass depth
+        if (split_used()) {
+            for (int kind : {1, 2}) {
+                float bk = 1e30f;
+                const char* pk = "temporal";
+                for (const char* c : {"temporal", "tile"}) {
+                    const float t = time_pass(kind, c, kdepth_);
+                    if (t < bk) {
+                        bk = t;
+                        pk = c;
+                    }
+                }
+                kern_[kind] = pk;
+            }
         }
         HIP_CHECK(hipEventDestroy(e0));
         HIP_CHECK(hipEventDestroy(e1));
@@ -898,6 +923,7 @@ class HipEngine : public Engine {
     std::string kernel_;  // resolved kernel: temporal | tile | lds (auto resolves at init)
     std::string kern_[3];  // per plan kind (full / interior / boundary), resolved by autotune
     int kdepth_ = 8;       // kernel pass depth K (<= halo depth R)
+    bool tile_l2_ = env_int("GOL_TILE_LEVELS", 2) == 2;  // tile kernel: generations per LDS pass
     bool multipass_ = false;
     std::map<int, std::vector<int>> passes_;
     bool split_ = false;   // superstep schedule: interior/boundary split with overlapped exchange

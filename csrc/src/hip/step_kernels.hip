@@ -369,19 +369,29 @@ struct BandSink {
     }
 };
 
-// Stream input rows in[0 .. n) (n >= 3) through a one-level window; outputs rows 1 .. n-2.
-template <bool LAST>
+// Stream input rows in[0 .. n) (n >= 2*LV+1) through an LV-level register window (LV generations
+// per LDS pass); outputs rows LV .. n-LV-1.
+template <bool LAST, int LV>
 __device__ __forceinline__ void tile_band(const u32* __restrict__ in, int n, BandSink<LAST>& out, int lane) {
-    Pipe<1> P;
+    Pipe<LV> P;
     u32 lo, hi;
 #define GOL_TILE_ROW(PH, GUARD, IDX)                                   \
     lo = in[(IDX) * kTileRowU32 + lane];                               \
     hi = in[(IDX) * kTileRowU32 + 64 + lane];                          \
-    if (advance<1, PH, GUARD>(P, lo, hi, (IDX))) out.put(lo, hi);
-    GOL_TILE_ROW(0, true, 0)
-    GOL_TILE_ROW(1, true, 1)
-    GOL_TILE_ROW(2, true, 2)
-    int i = 3;
+    if (advance<LV, PH, GUARD>(P, lo, hi, (IDX))) out.put(lo, hi);
+    constexpr int i0 = ((2 * LV + 2) / 3) * 3;  // first multiple of 3 with the window full
+    int i = 0;
+    for (; i < i0; i += 3) {
+        if (i < n) {
+            GOL_TILE_ROW(0, true, i)
+        }
+        if (i + 1 < n) {
+            GOL_TILE_ROW(1, true, i + 1)
+        }
+        if (i + 2 < n) {
+            GOL_TILE_ROW(2, true, i + 2)
+        }
+    }
     for (; i + 3 <= n; i += 3) {
         // hoist the triple's LDS reads above its compute (stores to the other buffer do not alias)
         const u32 l0 = in[i * kTileRowU32 + lane], h0 = in[i * kTileRowU32 + 64 + lane];
@@ -389,11 +399,11 @@ __device__ __forceinline__ void tile_band(const u32* __restrict__ in, int n, Ban
         const u32 l2 = in[(i + 2) * kTileRowU32 + lane], h2 = in[(i + 2) * kTileRowU32 + 64 + lane];
         __builtin_amdgcn_sched_barrier(0);
         lo = l0, hi = h0;
-        if (advance<1, 0, false>(P, lo, hi, i)) out.put(lo, hi);
+        if (advance<LV, 0, false>(P, lo, hi, i)) out.put(lo, hi);
         lo = l1, hi = h1;
-        if (advance<1, 1, false>(P, lo, hi, i + 1)) out.put(lo, hi);
+        if (advance<LV, 1, false>(P, lo, hi, i + 1)) out.put(lo, hi);
         lo = l2, hi = h2;
-        if (advance<1, 2, false>(P, lo, hi, i + 2)) out.put(lo, hi);
+        if (advance<LV, 2, false>(P, lo, hi, i + 2)) out.put(lo, hi);
     }
     if (i < n) {
         GOL_TILE_ROW(0, false, i)
@@ -404,7 +414,31 @@ __device__ __forceinline__ void tile_band(const u32* __restrict__ in, int n, Ban
 #undef GOL_TILE_ROW
 }
 
-template <int NW, bool WRAPY>
+// One LDS pass of `lv` generations: wave `wv` streams its band of the pass's output rows.
+template <int NW, int LV>
+__device__ __forceinline__ void tile_pass(const u32* A, u32* B, u64* dst, const LaneDesc& d, const StepParams& p,
+                                          int K, int g, int n_in, int wv, int lane) {
+    const int lo_r = g + LV, cnt = n_in - 2 * g - 2 * LV;
+    const int b = (cnt + NW - 1) / NW;
+    const int r0 = lo_r + wv * b;
+    const int r1 = min(r0 + b, lo_r + cnt);
+    if (r1 <= r0) return;
+    const u32* in = A + (r0 - LV) * kTileRowU32;
+    const int n = r1 - r0 + 2 * LV;
+    if (g + LV < K) {
+        BandSink<false> s{B, nullptr, 0, r0, lane};
+        tile_band<false, LV>(in, n, s, lane);
+    } else {
+        // tile row r0 is output row row0 + r0 - K; halo/idle lanes write the trash row
+        const bool out_lane = d.flags & LANE_STORE;
+        const i64 srow = out_lane ? (i64)(d.row0 + r0 - K + p.R) : (i64)(p.h + 2 * p.R + kSlackRows - 1);
+        BandSink<true> s{nullptr, reinterpret_cast<uint2*>(dst + srow * p.pitch + (d.col + 1)), out_lane ? p.pitch : 0,
+                         0, lane};
+        tile_band<true, LV>(in, n, s, lane);
+    }
+}
+
+template <int NW, bool WRAPY, int LV>
 __global__ __launch_bounds__(64 * NW) void step_tile(const u64* __restrict__ src, u64* __restrict__ dst,
                                                      const LaneDesc* __restrict__ plan, StepParams p, int K) {
     extern __shared__ __attribute__((aligned(16))) u32 tile_lds[];
@@ -429,26 +463,16 @@ __global__ __launch_bounds__(64 * NW) void step_tile(const u64* __restrict__ src
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
 
-    // 2. K generations; generation g computes tile rows [g+1, n_in-g-1)
-    const bool out_lane = d.flags & LANE_STORE;
-    for (int g = 0; g < K; ++g) {
-        const int lo_r = g + 1, cnt = n_in - 2 * g - 2;
-        const int b = (cnt + NW - 1) / NW;
-        const int r0 = lo_r + wv * b;
-        const int r1 = min(r0 + b, lo_r + cnt);
-        if (r1 > r0) {
-            if (g + 1 < K) {
-                BandSink<false> s{B, nullptr, 0, r0, lane};
-                tile_band<false>(A + (r0 - 1) * kTileRowU32, r1 - r0 + 2, s, lane);
-            } else {
-                // tile row r0 is output row row0 + r0 - K; halo/idle lanes write the trash row
-                const i64 srow = out_lane ? (i64)(d.row0 + r0 - K + p.R) : (i64)(p.h + 2 * p.R + kSlackRows - 1);
-                BandSink<true> s{nullptr, reinterpret_cast<uint2*>(dst + srow * p.pitch + (d.col + 1)),
-                                 out_lane ? p.pitch : 0, 0, lane};
-                tile_band<true>(A + (r0 - 1) * kTileRowU32, r1 - r0 + 2, s, lane);
-            }
-        }
-        if (g + 1 < K) {
+    // 2. K generations in passes of LV (a final odd generation runs a one-level pass); the pass
+    // starting at generation g computes tile rows [g+lv, n_in-g-lv)
+    for (int g = 0; g < K;) {
+        const int lv = (LV == 2 && g + 2 <= K) ? 2 : 1;
+        if (lv == 2)
+            tile_pass<NW, (LV == 2 ? 2 : 1)>(A, B, dst, d, p, K, g, n_in, wv, lane);
+        else
+            tile_pass<NW, 1>(A, B, dst, d, p, K, g, n_in, wv, lane);
+        g += lv;
+        if (g < K) {
             __syncthreads();
             u32* t = A;
             A = B;
@@ -462,7 +486,9 @@ inline size_t tile_lds_bytes(i64 rows, int k) { return (size_t)(2 * (rows + 2 * 
 
 template <int NW>
 const void* tile_kernel(u32 flags) {
-    return (flags & STEP_WRAP_Y) ? (const void*)step_tile<NW, true> : (const void*)step_tile<NW, false>;
+    if (flags & STEP_TILE_L2)
+        return (flags & STEP_WRAP_Y) ? (const void*)step_tile<NW, true, 2> : (const void*)step_tile<NW, false, 2>;
+    return (flags & STEP_WRAP_Y) ? (const void*)step_tile<NW, true, 1> : (const void*)step_tile<NW, false, 1>;
 }
 
 const void* tile_kernel_for(int nw_per_wg, u32 flags) {
@@ -571,7 +597,7 @@ static const void* tile_kernel_checked(int nw_per_wg, u32 flags) {
     const void* f = tile_kernel_for(nw_per_wg, flags);
     if (!f) throw Error(strprintf("step_tile: unsupported waves per workgroup %d (4, 8 or 16)", nw_per_wg));
     static bool attr_set[64] = {};
-    const int key = (nw_per_wg & 31) * 2 + ((flags & STEP_WRAP_Y) ? 1 : 0);
+    const int key = ((nw_per_wg & 15) * 2 + ((flags & STEP_WRAP_Y) ? 1 : 0)) * 2 + ((flags & STEP_TILE_L2) ? 1 : 0);
     if (!attr_set[key]) {  // allow the full 160 KiB of dynamic LDS
         hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kMaxLdsBytes);
         if (e != hipSuccess) throw Error(strprintf("step_tile: hipFuncSetAttribute: %s", hipGetErrorString(e)));

@@ -29,9 +29,9 @@ def test_random_board_vs_numpy(gol, N):
 @pytest.mark.parametrize("depth", [1, 2, 3, 4, 6, 8, 12, 16])
 def test_every_depth(gol, depth):
     N, gens = 192, 37
-    s = _sim(gol, N, halo_depth=depth).init(5, seed=3)
+    s = _sim(gol, N, halo_depth=depth, kernel_depth=depth, kernel="temporal").init(5, seed=3)
     s.step(gens)
-    assert s.stats()["depth"] == depth
+    assert s.stats()["depth"] == depth and s.stats()["kernel_depth"] == depth
     assert np.array_equal(s.board(), numpy_step(initial_board(5, N, 1, True, 3), gens))
 
 
@@ -107,7 +107,8 @@ def test_naive_yardstick(gol):
 @pytest.mark.parametrize("depth", [1, 3, 8, 16])
 def test_kernel_variants(gol, pipeline, prefetch, depth):
     N, gens = 700, 3 * depth + 5
-    s = _sim(gol, N, halo_depth=depth, pipeline=pipeline, prefetch=prefetch).init(5, seed=depth)
+    s = _sim(gol, N, halo_depth=depth, kernel_depth=depth, kernel="temporal", pipeline=pipeline,
+             prefetch=prefetch).init(5, seed=depth)
     s.step(gens)
     assert np.array_equal(s.board(), numpy_step(initial_board(5, N, 1, True, depth), gens))
 
@@ -126,7 +127,7 @@ def test_watchdog_fenced_run(gol, graph):
 def test_tile_kernel_depths(gol, tile_waves, depth):
     """LDS-resident temporal kernel (any runtime depth) vs numpy."""
     N, gens = 700, 3 * depth + 5
-    s = _sim(gol, N, halo_depth=depth, kernel="tile", tile_waves=tile_waves).init(5, seed=depth)
+    s = _sim(gol, N, halo_depth=depth, kernel_depth=depth, kernel="tile", tile_waves=tile_waves).init(5, seed=depth)
     s.step(gens)
     assert np.array_equal(s.board(), numpy_step(initial_board(5, N, 1, True, depth), gens))
 
