@@ -152,6 +152,7 @@ def main() -> int:
                 "kernel_depth": st["kernel_depth"],
                 "kernel": st["kernel"],
                 "schedule": st["schedule"],
+                "autotune": st["tuning"],
                 "graph_launches": st["graph_launches"],
                 "plan_waves": st["plan_waves"],
                 "lane_efficiency": round(st["lane_efficiency"], 4),

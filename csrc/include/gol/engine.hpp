@@ -69,6 +69,7 @@ struct EngineStats {
     double t_compute_ms = 0;   // profile only
     std::string kernel;        // stencil kernel in use (HIP: temporal | tile | lds; CPU: cpu)
     std::string schedule;      // superstep schedule: local (no neighbours) | split | full
+    std::string tuning;        // init-time measurements behind the auto choices (HIP)
 };
 
 class Engine {

@@ -105,6 +105,7 @@ py::dict stats_dict(const EngineStats& s) {
     d["kernel"] = s.kernel;
     d["schedule"] = s.schedule;
     d["kernel_depth"] = s.kernel_depth;
+    d["tuning"] = s.tuning;
     return d;
 }
 

@@ -340,6 +340,11 @@ class HipEngine : public Engine {
         stats_.kernel = split_ ? kern_[1] + "+boundary:" + kern_[2] : kern_[0];
         stats_.schedule = split_ ? "split" : (halo_items(L_.R).empty() ? "local" : "full");
         stats_.kernel_depth = kdepth_;
+        std::string tn;
+        for (const auto& kv : tune_ms_) tn += strprintf("%s%s=%.3fus/gen", tn.empty() ? "" : " ", kv.first.c_str(), kv.second * 1e3);
+        if (sched_ms_[0] > 0)
+            tn += strprintf("%ssplit=%.3fms full=%.3fms", tn.empty() ? "" : " ", sched_ms_[0], sched_ms_[1]);
+        stats_.tuning = tn;
         // Build the plans for every depth a run can use (remainder supersteps included) now, so
         // neither graph capture nor a timed loop ever builds or uploads a plan.
         for (int k = 1; k <= (cfg_.compat ? 1 : L_.R); ++k)
@@ -478,6 +483,7 @@ class HipEngine : public Engine {
     // schedule with the smaller max-over-ranks time wins.  Split overlaps the exchange with the
     // interior but pays a serial boundary kernel and cross-stream waits; full pays the exchange
     // latency.  Which is cheaper depends on the tile size and the link latency.
+    static constexpr int kSchedReps = 8;
     void autotune_schedule() {
         if (!split_ || halo_items(L_.R).empty() || cfg_.sched != "auto") return;
         const int k = L_.R;
@@ -491,14 +497,14 @@ class HipEngine : public Engine {
             synchronize();
             t_->barrier();
             const auto t0 = std::chrono::steady_clock::now();
-            for (int i = 0; i < 4; ++i) first_pass(k, ps[0], e0, sp);
+            for (int i = 0; i < kSchedReps; ++i) first_pass(k, ps[0], e0, sp);
             synchronize();
             const double dt = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
             t[m] = t_->allreduce_max(dt);
         }
         split_ = t[0] <= t[1];
-        sched_ms_[0] = t[0] * 250.0;  // ms per (exchange + first pass)
-        sched_ms_[1] = t[1] * 250.0;
+        sched_ms_[0] = t[0] * 1e3 / kSchedReps;  // ms per (exchange + first pass)
+        sched_ms_[1] = t[1] * 1e3 / kSchedReps;
         stats_.exchanges = 0;  // the timing exchanges are not part of the run
         stats_.halo_bytes = 0;
     }
