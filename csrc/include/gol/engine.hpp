@@ -40,6 +40,7 @@ struct EngineConfig {
     int device = -1;                  // HIP device (-1: current)
     i64 rows_per_wave = 0;            // plan segment height override (0 = auto)
     int waves_target = 0;             // plan wave-count target (0 = auto)
+    int plan_xcds = 8;                // XCD-aware plan order (workgroup b runs on XCD b % n; 1 = off)
     std::string kernel = "auto";      // auto (timed at init) | temporal (register pipeline) |
                                       // tile (LDS-resident) | lds (1 gen, reference-class LDS tile)
     int tile_waves = 8;               // tile kernel: waves per workgroup (4, 8, 16)

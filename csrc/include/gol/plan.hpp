@@ -55,8 +55,11 @@ struct PlanStats {
 // (only used to account for the 2k extra input rows per segment in the stats).  With `xwrap` the
 // tile is its own E/W neighbour (w % 64 == 0): halo lanes left of word 0 stream word nw-1 and halo
 // lanes right of word nw-1 stream word 0, so no ghost words are needed.
+// Waves are ordered for L2 locality: column-major, and whole workgroups of `wg_waves` waves
+// permuted so each of the `xcds` XCDs (workgroup b runs on XCD b % xcds) gets a contiguous stretch.
 std::vector<LaneDesc> build_plan(const std::vector<Region>& regions, i64 nw, i64 h, i64 rows_per_chunk, int k,
-                                 bool xwrap, PlanStats* stats = nullptr);
+                                 bool xwrap, PlanStats* stats = nullptr, int wg_waves = kWavesPerBlock,
+                                 int xcds = 8);
 
 // Bounds check of a plan before it is uploaded (a bad plan would fault the GPU): every lane's word
 // column lies in [-1, nw]; without y-wrap its input rows [row0-k, row0+nrows+k) lie in the

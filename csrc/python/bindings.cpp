@@ -249,7 +249,8 @@ PYBIND11_MODULE(_gol, m) {
         .def_readwrite("force_split", &EngineConfig::force_split)
         .def_readwrite("sched", &EngineConfig::sched)
         .def_readwrite("kernel_depth", &EngineConfig::kernel_depth)
-        .def_readwrite("graph_rccl", &EngineConfig::graph_rccl);
+        .def_readwrite("graph_rccl", &EngineConfig::graph_rccl)
+        .def_readwrite("plan_xcds", &EngineConfig::plan_xcds);
 
     py::class_<Engine>(m, "Engine")
         .def_static(

@@ -113,15 +113,39 @@ i64 plan_waves(const std::vector<Region>& regions, i64 nw, i64 h, i64 rows_per_c
 }
 
 std::vector<LaneDesc> build_plan(const std::vector<Region>& regions, i64 nw, i64 h, i64 rows_per_chunk, int k,
-                                 bool xwrap, PlanStats* stats) {
-    std::vector<std::vector<Item>> waves = pack_waves(regions, nw, h, rows_per_chunk);
-    i64 nwaves = round_up(std::max<i64>(1, (i64)waves.size()), kWavesPerBlock);
+                                 bool xwrap, PlanStats* stats, int wg_waves, int xcds) {
+    std::vector<std::vector<Item>> packed = pack_waves(regions, nw, h, rows_per_chunk);
+    i64 nwaves = round_up(std::max<i64>(1, (i64)packed.size()), kWavesPerBlock);
+    // XCD-aware order.  Vertically adjacent segments of a column share 2k input rows, so the
+    // full-width segments are ordered column-major (narrow, packed waves stay last); then whole
+    // workgroups are permuted so that XCD x — workgroup b is dispatched to XCD b % xcds — runs a
+    // contiguous stretch of that order and the shared rows are hits in its own L2.
+    std::stable_sort(packed.begin(), packed.end(), [](const std::vector<Item>& a, const std::vector<Item>& b) {
+        const bool fa = a.size() == 1 && a[0].lanes() == kWaveLanes, fb = b.size() == 1 && b[0].lanes() == kWaveLanes;
+        if (fa != fb) return fa;
+        if (!fa) return false;
+        return a[0].c0 != b[0].c0 ? a[0].c0 < b[0].c0 : a[0].r0 < b[0].r0;
+    });
+    std::vector<std::vector<Item>> waves((size_t)nwaves);
+    if (wg_waves < 1 || nwaves % wg_waves) wg_waves = 1;
+    const i64 nwg = nwaves / wg_waves;
+    std::vector<i64> order((size_t)nwg);
+    for (i64 b = 0; b < nwg; ++b) order[(size_t)b] = b;
+    if (xcds > 1)
+        std::stable_sort(order.begin(), order.end(), [xcds](i64 a, i64 b) {
+            return a % xcds != b % xcds ? a % xcds < b % xcds : a / xcds < b / xcds;
+        });
+    for (i64 s = 0; s < nwg; ++s)
+        for (int i = 0; i < wg_waves; ++i) {
+            const size_t src = (size_t)(s * wg_waves + i);
+            if (src < packed.size()) waves[(size_t)(order[(size_t)s] * wg_waves + i)] = std::move(packed[src]);
+        }
     std::vector<LaneDesc> lanes((size_t)(nwaves * kWaveLanes));
     PlanStats st;
     st.waves = nwaves;
     for (size_t wi = 0; wi < (size_t)nwaves; ++wi) {
         LaneDesc* L = &lanes[wi * kWaveLanes];
-        if (wi >= waves.size()) {
+        if (waves[wi].empty()) {
             for (int l = 0; l < kWaveLanes; ++l) L[l] = {0, 0, 0u, 0};
             continue;
         }

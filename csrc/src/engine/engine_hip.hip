@@ -701,7 +701,8 @@ class HipEngine : public Engine {
                 rows = balanced_rows_per_chunk(rg, L_.nw, L_.h, k, resident, 2 * (i64)k, xwrap_by_plan());
             }
         }
-        std::vector<LaneDesc> lanes = build_plan(rg, L_.nw, L_.h, rows, k, xwrap_by_plan(), &p.st);
+        std::vector<LaneDesc> lanes = build_plan(rg, L_.nw, L_.h, rows, k, xwrap_by_plan(), &p.st,
+                                                 tile_kernel(kind) ? 1 : kWavesPerBlock, cfg_.plan_xcds);
         const std::string bad = validate_plan(lanes, L_.nw, L_.h, L_.R, k, (step_flags() & hipk::STEP_WRAP_Y) != 0);
         if (!bad.empty()) throw Error(strprintf("refusing to launch an unsafe plan (kind %d, k %d, e %lld): %s", kind, k,
                                                 (long long)e, bad.c_str()));

@@ -158,6 +158,7 @@ EngineConfig engine_config(const Options& o, const std::string& backend, int dev
     c.edge_cus = (int)env_int("GOL_EDGE_CUS", 0);
     c.force_split = env_int("GOL_FORCE_SPLIT", 0) != 0;
     c.graph_rccl = env_int("GOL_GRAPH_RCCL", 0) != 0;
+    c.plan_xcds = (int)env_int("GOL_PLAN_XCDS", 8);
     c.sched = env_str("GOL_SCHEDULE", "auto");
     if (c.sched != "auto" && c.sched != "split" && c.sched != "full")
         throw Error("GOL_SCHEDULE must be auto, split or full (got " + c.sched + ")");

@@ -116,6 +116,7 @@ class Simulation:
         cfg.force_split = bool(force_split)
         cfg.sched = schedule
         cfg.graph_rccl = os.environ.get("GOL_GRAPH_RCCL", "0") == "1"
+        cfg.plan_xcds = int(os.environ.get("GOL_PLAN_XCDS", "8"))
         if self.backend == "hip":
             n = _gol.hip_device_count()
             if n <= 0:

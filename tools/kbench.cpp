@@ -61,7 +61,8 @@ int main(int argc, char** argv) {
         rows = balanced_rows_per_chunk(rg, L.nw, N, K, resident, 2 * K, true);
     }
     PlanStats st;
-    std::vector<LaneDesc> lanes = build_plan(rg, L.nw, N, rows, K, true, &st);
+    const int xcds = getenv("KB_XCDS") ? atoi(getenv("KB_XCDS")) : 8;  // 1: plain row-major order
+    std::vector<LaneDesc> lanes = build_plan(rg, L.nw, N, rows, K, true, &st, tile_nw > 0 ? 1 : kWavesPerBlock, xcds);
     LaneDesc* dplan;
     CK(hipMalloc(&dplan, lanes.size() * sizeof(LaneDesc)));
     CK(hipMemcpy(dplan, lanes.data(), lanes.size() * sizeof(LaneDesc), hipMemcpyHostToDevice));
