@@ -296,8 +296,15 @@ struct WaveRunner {
 };
 
 // MODE bit 0: PF_LDS prefetch ring; bit 1: skewed level pipeline.
+// GOL_TEMPORAL_WAVES_PER_EU (build-time experiment knob): minimum waves per SIMD the register
+// allocator must fit (e.g. 4 caps K=8 at 128 VGPRs instead of its natural 163).
+#ifdef GOL_TEMPORAL_WAVES_PER_EU
+#define GOL_TEMPORAL_OCC __attribute__((amdgpu_waves_per_eu(GOL_TEMPORAL_WAVES_PER_EU)))
+#else
+#define GOL_TEMPORAL_OCC
+#endif
 template <int K, bool WRAPY, int MODE>
-__global__ __launch_bounds__(256) void step_temporal(const u64* __restrict__ src, u64* __restrict__ dst,
+__global__ __launch_bounds__(256) GOL_TEMPORAL_OCC void step_temporal(const u64* __restrict__ src, u64* __restrict__ dst,
                                                      const LaneDesc* __restrict__ plan, StepParams p) {
     const int wv = threadIdx.x >> 6;
     const i64 wave = (i64)blockIdx.x * kWavesPerBlock + wv;
