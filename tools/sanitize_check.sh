@@ -6,7 +6,7 @@ set -e
 cd "$(dirname "$0")/.."
 for san in "${@:-address thread}"; do
   for s in $san; do
-    b=build-san-$s
+    b=${GOL_SAN_BUILD_DIR:-/tmp}/gol-san-$s
     cmake -S . -B $b -DGOL_SANITIZE=$s -DGOL_WITH_PYTHON=OFF -DGOL_WITH_MPI=OFF -DCMAKE_BUILD_TYPE=RelWithDebInfo > $b.log 2>&1
     cmake --build $b -j8 --target gol_unit >> $b.log 2>&1
     echo "== $s"
