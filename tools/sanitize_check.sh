@@ -11,6 +11,6 @@ for san in "${@:-address thread}"; do
     cmake --build $b -j8 --target gol_unit >> $b.log 2>&1
     echo "== $s"
     if [ $s = thread ]; then export OMP_NUM_THREADS=1 TSAN_OPTIONS="halt_on_error=1"; else export ASAN_OPTIONS="detect_leaks=1"; fi
-    GOL_BACKEND=cpu ./$b/gol_unit | tail -1
+    GOL_BACKEND=cpu $b/gol_unit | tail -1
   done
 done
