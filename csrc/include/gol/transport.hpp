@@ -89,12 +89,18 @@ class ThreadTransport : public Transport {
     void send_bytes(int peer, const void* buf, size_t n) override;
     void recv_bytes(int peer, void* buf, size_t n) override;
     [[noreturn]] void abort(int code) override;
+    const void* group_key() const { return g_.get(); }  // identifies the ranks of one group
 
    private:
     std::shared_ptr<ThreadGroup> g_;
     int rank_;
 };
 std::shared_ptr<ThreadGroup> make_thread_group(int nranks);
+
+// RCCL-semantics data plane for thread-mode ranks sharing one GPU (device buffers, stream-ordered
+// rendezvous copies, per-peer FIFO matching): exercises the device-transport engine paths without
+// a second GPU.  `control` must be a ThreadTransport.
+std::shared_ptr<Transport> make_p2p_emulation_transport(std::shared_ptr<Transport> control);
 
 // Torchrun-style rendezvous over TCP: rank 0 listens on MASTER_ADDR:MASTER_PORT, every rank
 // connects to every other rank (full mesh of sockets, P <= a few dozen).

@@ -126,6 +126,7 @@ static bool devices_distinct(Transport& control, int device) {
 std::shared_ptr<Transport> make_data_transport(std::shared_ptr<Transport> control, const std::string& backend,
                                                const Options& o, int device) {
     if (backend != "hip" || control->size() == 1 || o.transport == "host") return control;
+    if (o.transport == "p2p") return make_p2p_emulation_transport(control);  // RCCL semantics, one GPU
     if (!devices_distinct(*control, device)) {
         if (o.transport == "rccl")
             throw Error("GOL_TRANSPORT=rccl needs one rank per GPU, but ranks share a device");
@@ -151,7 +152,7 @@ EngineConfig engine_config(const Options& o, const std::string& backend, int dev
     c.tile_waves = (int)env_int("GOL_TILE_WAVES", 8);
     c.prefetch = env_str("GOL_PREFETCH", "reg");
     c.pipeline = env_str("GOL_PIPELINE", "chain");
-    c.transport = o.transport == "rccl" ? "device" : o.transport;
+    c.transport = (o.transport == "rccl" || o.transport == "p2p") ? "device" : o.transport;
     c.profile = o.profile;
     c.graph_supersteps = (int)env_int("GOL_GRAPH_SUPERSTEPS", 0);
     c.watchdog_s = o.watchdog_s;

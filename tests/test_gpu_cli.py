@@ -120,3 +120,29 @@ def test_multipass_2d(gol_bin, tmp_path, N, P, grid, env):
     r = _run(gol_bin, [5, N, gens, 256, 1], tmp_path, P, e)
     assert r.returncode == 0, r.stderr
     assert np.array_equal(_board(tmp_path, P), numpy_step(initial_board(5, N, P, False), gens))
+
+
+@pytest.mark.parametrize(
+    "N,P,env",
+    [
+        (256, 2, {}),
+        (256, 3, {"GOL_SCHEDULE": "split"}),
+        (256, 4, {"GOL_SCHEDULE": "full"}),
+        (200, 3, {"GOL_SCHEDULE": "split", "GOL_HALO_DEPTH": "20", "GOL_KERNEL_DEPTH": "6"}),
+        (256, 4, {"GOL_GLOBAL": "1", "GOL_DECOMP": "2d", "GOL_GRID": "2x2", "GOL_SCHEDULE": "split"}),
+        (256, 4, {"GOL_GLOBAL": "1", "GOL_DECOMP": "2d", "GOL_GRID": "2x2", "GOL_SCHEDULE": "full"}),
+        (384, 6, {"GOL_GLOBAL": "1", "GOL_DECOMP": "2d", "GOL_GRID": "3x2"}),
+        (256, 2, {"GOL_KERNEL": "tile", "GOL_SCHEDULE": "split"}),
+        (256, 3, {"GOL_WATCHDOG": "60", "GOL_SCHEDULE": "split"}),
+    ],
+)
+def test_device_transport_emulated(gol_bin, tmp_path, N, P, env):
+    """GOL_TRANSPORT=p2p: thread ranks on one GPU with RCCL's semantics (device buffers, stream-
+    ordered rendezvous copies, per-peer FIFO matching) — the device-transport engine paths that the
+    multi-GPU RCCL runs take (device halos, split schedule, 2-D pack/unpack, collective autotune)."""
+    gens = 101
+    r = _run(gol_bin, [5, N, gens, 256, 1], tmp_path, P, dict(env, GOL_TRANSPORT="p2p"))
+    assert r.returncode == 0, r.stderr
+    assert "p2p-emulation" in r.stderr  # GOL_VERBOSE describes the transport
+    glob = env.get("GOL_GLOBAL") == "1"
+    assert np.array_equal(_board(tmp_path, P), numpy_step(initial_board(5, N, P, not glob), gens))
