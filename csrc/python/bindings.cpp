@@ -209,6 +209,12 @@ PYBIND11_MODULE(_gol, m) {
         for (int r = 0; r < P; ++r) v.push_back(std::make_shared<ThreadTransport>(g, r));
         return v;
     });
+    m.def("make_p2p_transports", [](int P) {
+        auto g = make_thread_group(P);
+        std::vector<std::shared_ptr<Transport>> v;
+        for (int r = 0; r < P; ++r) v.push_back(make_p2p_emulation_transport(std::make_shared<ThreadTransport>(g, r)));
+        return v;
+    });
     py::class_<PyTransport, Transport, std::shared_ptr<PyTransport>>(m, "PyTransport")
         .def(py::init<int, int, py::function, py::function, py::object, py::object>(), py::arg("rank"),
              py::arg("size"), py::arg("send"), py::arg("recv"), py::arg("exchange") = py::none(),

@@ -93,10 +93,7 @@ class HipEngine : public Engine {
         stats_.depth = R;
         // slack rows: the temporal kernel prefetches 3 rows past a segment's last input row
         const size_t bytes = (size_t)(L_.words() + hipk::kSlackRows * L_.pitch) * 8;
-        for (int i = 0; i < 2; ++i) {
-            HIP_CHECK(hipMalloc(&buf_[i], bytes));
-            HIP_CHECK(hipMemset(buf_[i], 0, bytes));
-        }
+        for (int i = 0; i < 2; ++i) HIP_CHECK(hipMalloc(&buf_[i], bytes));
         alloc_bytes_ = bytes;
         device_transport_ = t_->device_buffers() && cfg_.transport != "host";
         if (cfg_.transport == "device" && !t_->device_buffers())
@@ -111,6 +108,11 @@ class HipEngine : public Engine {
                      can_overlap() && !(self_x() && !L_.aligned()) &&
                      ((device_transport_ && !halo_items(L_.R).empty()) || cfg_.force_split);
         create_streams();
+        // All device memory work is ordered on the engine's own streams.  (They are non-blocking:
+        // null-stream calls such as hipMemset, or a pageable hipMemcpy whose DMA may still be in
+        // flight when it returns, would NOT be ordered before their kernels.)
+        for (int i = 0; i < 2; ++i) HIP_CHECK(hipMemsetAsync(buf_[i], 0, bytes, s_comp_));
+        HIP_CHECK(hipStreamSynchronize(s_comp_));
         HIP_CHECK(hipEventCreateWithFlags(&ev_ready_, hipEventDisableTiming));
         HIP_CHECK(hipEventCreateWithFlags(&ev_halo_, hipEventDisableTiming));
         HIP_CHECK(hipEventCreateWithFlags(&ev_int_, hipEventDisableTiming));
@@ -163,6 +165,12 @@ class HipEngine : public Engine {
         }
         HIP_CHECK(hipStreamCreateWithFlags(&s_comp_, hipStreamNonBlocking));
         HIP_CHECK(hipStreamCreateWithFlags(&s_comm_, hipStreamNonBlocking));
+    }
+
+    // Host -> device copy ordered on the compute stream; returns when the data is in HBM.
+    void upload(void* dst, const void* src, size_t n) {
+        HIP_CHECK(hipMemcpyAsync(dst, src, n, hipMemcpyHostToDevice, s_comp_));
+        HIP_CHECK(hipStreamSynchronize(s_comp_));
     }
 
     // CUs a plan of this kind runs on (resident-wave budget of its one-round balance).
@@ -250,8 +258,9 @@ class HipEngine : public Engine {
                 u64& x = m[(size_t)(r * L_.nw + c)];
                 x = split_word(x & L_.mask(c));
             }
-        HIP_CHECK(hipMemcpy2D(buf_[cur_] + L_.index(0, 0), (size_t)L_.pitch * 8, m.data(), (size_t)L_.nw * 8,
-                              (size_t)L_.nw * 8, (size_t)L_.h, hipMemcpyHostToDevice));
+        HIP_CHECK(hipMemcpy2DAsync(buf_[cur_] + L_.index(0, 0), (size_t)L_.pitch * 8, m.data(), (size_t)L_.nw * 8,
+                                   (size_t)L_.nw * 8, (size_t)L_.h, hipMemcpyHostToDevice, s_comp_));
+        HIP_CHECK(hipStreamSynchronize(s_comp_));  // m is pageable and goes out of scope
         post(buf_[cur_], s_comp_);
         mark_ready();
         synchronize();
@@ -512,9 +521,8 @@ class HipEngine : public Engine {
     void do_set_compat_halos(const std::vector<u64>& above, const std::vector<u64>& below) override {
         synchronize();
         for (int i = 0; i < 2; ++i) {
-            HIP_CHECK(hipMemcpy(buf_[i] + L_.index(-1, -1), above.data(), (size_t)L_.pitch * 8, hipMemcpyHostToDevice));
-            HIP_CHECK(hipMemcpy(buf_[i] + L_.index(L_.h, -1), below.data(), (size_t)L_.pitch * 8,
-                                hipMemcpyHostToDevice));
+            upload(buf_[i] + L_.index(-1, -1), above.data(), (size_t)L_.pitch * 8);
+            upload(buf_[i] + L_.index(L_.h, -1), below.data(), (size_t)L_.pitch * 8);
             if (self_x() && !L_.aligned()) {
                 hipk::launch_fill_ghost_cols(buf_[i], L_, -1, 0, s_comp_);
                 hipk::launch_fill_ghost_cols(buf_[i], L_, L_.h, L_.h + 1, s_comp_);
@@ -709,7 +717,7 @@ class HipEngine : public Engine {
         p.waves = (i64)lanes.size() / kWaveLanes;
         p.rows = rows;
         HIP_CHECK(hipMalloc(&p.d, lanes.size() * sizeof(LaneDesc)));
-        HIP_CHECK(hipMemcpy(p.d, lanes.data(), lanes.size() * sizeof(LaneDesc), hipMemcpyHostToDevice));
+        upload(p.d, lanes.data(), lanes.size() * sizeof(LaneDesc));
         return plans_.emplace(key, p).first->second;
     }
 
@@ -795,9 +803,9 @@ class HipEngine : public Engine {
         dc.nunpack = (int)up.size();
         if (!pk.empty()) {
             HIP_CHECK(hipMalloc(&dc.pack, pk.size() * sizeof(hipk::CopyDesc)));
-            HIP_CHECK(hipMemcpy(dc.pack, pk.data(), pk.size() * sizeof(hipk::CopyDesc), hipMemcpyHostToDevice));
+            upload(dc.pack, pk.data(), pk.size() * sizeof(hipk::CopyDesc));
             HIP_CHECK(hipMalloc(&dc.unpack, up.size() * sizeof(hipk::CopyDesc)));
-            HIP_CHECK(hipMemcpy(dc.unpack, up.data(), up.size() * sizeof(hipk::CopyDesc), hipMemcpyHostToDevice));
+            upload(dc.unpack, up.data(), up.size() * sizeof(hipk::CopyDesc));
         }
         return copies_.emplace(key, dc).first->second;
     }

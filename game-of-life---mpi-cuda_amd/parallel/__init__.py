@@ -3,6 +3,7 @@ ranks, one process per GPU, RCCL halo exchange over xGMI (see :mod:`.dist`)."""
 from .dist import (  # noqa: F401
     env_rank,
     init_distributed,
+    p2p_thread_transports,
     rccl_transport,
     tcp_transport,
     thread_transports,

@@ -178,3 +178,33 @@ def test_single_rank_multipass(gol, R, K):
     assert s.stats()["depth"] == R and s.stats()["kernel_depth"] <= K
     s.step(gens)
     assert np.array_equal(s.board(), numpy_step(initial_board(5, N, 1, True, R), gens))
+
+
+@pytest.mark.parametrize("decomp,grid,P", [("1d", "", 3), ("2d", "2x2", 4)])
+def test_python_threads_device_transport(gol, decomp, grid, P):
+    """Simulation API, one Python thread per rank, RCCL-semantics transport on one GPU."""
+    import threading
+
+    N, gens = 256, 77
+    ts = gol.parallel.p2p_thread_transports(P)
+    out, errs = [None] * P, []
+
+    def rank_main(r):
+        try:
+            s = gol.Simulation(N, ts[r], backend="hip", device=0, global_mode=True, decomp=decomp, grid=grid)
+            s.init(5, seed=9)
+            s.step(gens)
+            out[r] = (s.geometry.row0, s.geometry.col0, s.board())
+        except Exception as e:  # pragma: no cover - reported below
+            errs.append(repr(e))
+
+    th = [threading.Thread(target=rank_main, args=(r,)) for r in range(P)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=300)
+    assert not errs, errs
+    board = np.zeros((N, N), dtype=np.uint8)
+    for r0, c0, b in out:
+        board[r0 : r0 + b.shape[0], c0 : c0 + b.shape[1]] = b
+    assert np.array_equal(board, numpy_step(initial_board(5, N, 1, True, 9), gens))
