@@ -76,7 +76,7 @@ def test_dump_bytes(gol_bin, tmp_path):
 
 
 @pytest.mark.parametrize("pattern", [0, 1, 2, 3, 4, 5])
-@pytest.mark.parametrize("P", [1, 2, 3, 4])
+@pytest.mark.parametrize("P", [1, 2, 3, 4, 8])
 def test_patterns_multi_rank_threads(gol_bin, tmp_path, pattern, P):
     N, gens = 140, 7
     r = run(gol_bin, [pattern, N, gens, 256, 1], tmp_path, nranks=P)

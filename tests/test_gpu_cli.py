@@ -146,3 +146,13 @@ def test_device_transport_emulated(gol_bin, tmp_path, N, P, env):
     assert "p2p-emulation" in r.stderr  # GOL_VERBOSE describes the transport
     glob = env.get("GOL_GLOBAL") == "1"
     assert np.array_equal(_board(tmp_path, P), numpy_step(initial_board(5, N, P, not glob), gens))
+
+
+@pytest.mark.parametrize("env", [{}, {"GOL_GLOBAL": "1", "GOL_DECOMP": "2d", "GOL_GRID": "4x2"}])
+def test_eight_ranks_one_gpu(gol_bin, tmp_path, env):
+    """8 ranks (the node size of the scaling runs) with the RCCL-semantics data plane."""
+    P, N, gens = 8, 256, 70
+    r = _run(gol_bin, [5, N, gens, 256, 1], tmp_path, P, dict(env, GOL_TRANSPORT="p2p"))
+    assert r.returncode == 0, r.stderr
+    glob = env.get("GOL_GLOBAL") == "1"
+    assert np.array_equal(_board(tmp_path, P), numpy_step(initial_board(5, N, P, not glob), gens))

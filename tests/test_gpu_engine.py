@@ -208,3 +208,25 @@ def test_python_threads_device_transport(gol, decomp, grid, P):
     for r0, c0, b in out:
         board[r0 : r0 + b.shape[0], c0 : c0 + b.shape[1]] = b
     assert np.array_equal(board, numpy_step(initial_board(5, N, 1, True, 9), gens))
+
+
+@pytest.mark.parametrize("kernel", ["temporal", "tile"])
+def test_known_physics_gpu(gol, kernel):
+    """Blinker period 2, block still life, glider back home after 4N generations on an N x N torus,
+    all-ones board dies in one generation — on the HIP kernels."""
+    N = 128
+    s = _sim(gol, N, kernel=kernel).init(0)
+    b = np.zeros((N, N), np.uint8)
+    b[5, 4:7] = 1
+    b[60:62, 60:62] = 1
+    s.set_board(b)
+    s.step(2)
+    assert np.array_equal(s.board(), b)
+    g = np.zeros((N, N), np.uint8)
+    g[1, 2] = g[2, 3] = g[3, 1] = g[3, 2] = g[3, 3] = 1
+    s.set_board(g)
+    s.step(4 * N)
+    assert np.array_equal(s.board(), g)
+    s.set_board(np.ones((N, N), np.uint8))
+    s.step(1)
+    assert s.population() == 0
