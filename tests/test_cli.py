@@ -213,3 +213,17 @@ def test_roctx_ranges_enabled(gol_bin, tmp_path):
     assert r.returncode == 0, r.stderr
     assert "no roctx library" not in r.stderr
     assert r.stdout.endswith(BANNER)
+
+
+def test_metrics_json(gol_bin, tmp_path):
+    """GOL_METRICS_JSON: machine-readable run metrics on rank 0 (stdout contract unchanged)."""
+    import json
+
+    path = tmp_path / "m.json"
+    r = run(gol_bin, [5, 128, 40, 256, 0], tmp_path, nranks=2, env={"GOL_METRICS_JSON": str(path)})
+    assert r.returncode == 0, r.stderr
+    assert r.stdout.endswith(BANNER)
+    m = json.loads(path.read_text())
+    assert m["ranks"] == 2 and m["generations"] == 40 and m["board"] == [256, 128]
+    assert m["cell_updates"] == 2 * 128 * 128 * 40 and m["cell_updates_per_sec"] > 0
+    assert m["backend"] == "cpu" and m["exchanges"] > 0 and m["halo_depth"] >= 1

@@ -156,3 +156,16 @@ def test_eight_ranks_one_gpu(gol_bin, tmp_path, env):
     assert r.returncode == 0, r.stderr
     glob = env.get("GOL_GLOBAL") == "1"
     assert np.array_equal(_board(tmp_path, P), numpy_step(initial_board(5, N, P, not glob), gens))
+
+
+def test_profile_and_metrics_on_gpu(gol_bin, tmp_path):
+    """GOL_PROFILE=1 per-phase event timing + GOL_METRICS_JSON on the HIP backend."""
+    import json
+
+    path = tmp_path / "m.json"
+    r = _run(gol_bin, [5, 512, 64, 256, 0], tmp_path, 2,
+             {"GOL_PROFILE": "1", "GOL_METRICS_JSON": str(path), "GOL_ROCTX": "1"})
+    assert r.returncode == 0, r.stderr
+    m = json.loads(path.read_text())
+    assert m["backend"] == "hip" and m["t_compute_ms"] > 0 and m["t_exchange_ms"] >= 0
+    assert m["kernel"] and m["schedule"] in ("split", "full")
