@@ -41,6 +41,10 @@ std::shared_ptr<Transport> make_data_transport(std::shared_ptr<Transport> contro
 
 EngineConfig engine_config(const Options& o, const std::string& backend, int device);
 
+// CLI threadsPerBlock as a hint: the LDS tile kernel's workgroup size (T/64 waves).  Values that
+// are not a multiple of 64 in 64..1024 warn on stderr (when `report`) and keep the default.
+void apply_threads_hint(EngineConfig& c, unsigned threads, bool report);
+
 // The `gol` program: ./gol <pattern> <worldSize> <iterations> <threadsPerBlock> <output_on_off>.
 // Returns the process exit status.
 int run_cli(int argc, char** argv);

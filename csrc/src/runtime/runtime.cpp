@@ -137,6 +137,23 @@ std::shared_ptr<Transport> make_data_transport(std::shared_ptr<Transport> contro
     return make_rccl_transport(control);
 }
 
+// threadsPerBlock (CLI argument 4): the reference's CUDA block size, which also decided whether its
+// launch failed (blocks = W*H/T, T > 1024 invalid; survey Q6).  Here it is validated and used as a
+// hint only: the workgroup size of the LDS tile kernel (T/64 waves; 512 -> 8, the default), unless
+// GOL_TILE_WAVES is set.  Invalid values warn on stderr and keep the default.
+void apply_threads_hint(EngineConfig& c, unsigned threads, bool report) {
+    if (getenv("GOL_TILE_WAVES")) return;
+    const bool ok = threads >= 64 && threads <= 1024 && threads % 64 == 0;
+    if (!ok) {
+        if (report)
+            fprintf(stderr, "[gol] threadsPerBlock=%u is not a multiple of 64 in 64..1024; using the default "
+                            "workgroup size\n", threads);
+        return;
+    }
+    const int waves = (int)threads / 64;
+    c.tile_waves = waves >= 16 ? 16 : (waves >= 8 ? 8 : 4);
+}
+
 EngineConfig engine_config(const Options& o, const std::string& backend, int device) {
     EngineConfig c;
     c.backend = backend;
@@ -336,7 +353,9 @@ int run_rank(const CliArgs& a, const Options& o, const LaunchInfo& li, std::shar
         Geometry g = make_geometry(dec, rank);
         PatternSpec pat = make_pattern(a.pattern, dec, o.seed);
         std::shared_ptr<Transport> t = make_data_transport(control, backend, o, device);
-        std::unique_ptr<Engine> eng = Engine::create(g, engine_config(o, backend, device), t);
+        EngineConfig ec = engine_config(o, backend, device);
+        apply_threads_hint(ec, a.threads, rank == 0);
+        std::unique_ptr<Engine> eng = Engine::create(g, ec, t);
         if (o.verbose && rank == 0) fprintf(stderr, "[gol] %s\n", eng->describe().c_str());
         eng->init(pat);
         u64 done = 0;

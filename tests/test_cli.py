@@ -66,6 +66,17 @@ def test_report_lines(gol_bin, tmp_path):
     assert not list(tmp_path.glob("Rank_*"))  # on_off != 1 writes nothing
 
 
+@pytest.mark.parametrize("threads,warns", [(64, False), (1024, False), (100, True), (0, True), (2048, True)])
+def test_threads_per_block_hint(gol_bin, tmp_path, threads, warns):
+    """threadsPerBlock is a hint (survey Q6): invalid values warn on stderr, the run and stdout are unchanged."""
+    r = run(gol_bin, [5, 64, 10, threads, 1], tmp_path)
+    assert r.returncode == 0, r.stderr
+    assert r.stdout.endswith(", number of cell updates = 40960\n" + BANNER)
+    assert ("threadsPerBlock=%d" % threads in r.stderr) == warns
+    _, _, cells = read_dump(os.path.join(tmp_path, "Rank_0_of_1.txt"))
+    assert np.array_equal(cells, numpy_step(initial_board(5, 64, 1, True), 10))
+
+
 def test_dump_bytes(gol_bin, tmp_path):
     r = run(gol_bin, [4, 6, 0, 64, 1], tmp_path)
     assert r.returncode == 0
