@@ -73,9 +73,10 @@ std::unique_ptr<Engine> Engine::create(const Geometry& g, const EngineConfig& c,
 }
 
 std::string Engine::describe() const {
-    return strprintf("%s backend, %s, rank %d tile %lldx%lld at (%lld,%lld), halo depth %d, transport %s%s",
+    const std::string wg = cfg_.backend == "hip" ? strprintf(", tile workgroup %d waves", cfg_.tile_waves) : "";
+    return strprintf("%s backend, %s, rank %d tile %lldx%lld at (%lld,%lld), halo depth %d, transport %s%s%s",
                      backend_name().c_str(), g_.dec.describe().c_str(), g_.rank, (long long)g_.h, (long long)g_.w,
-                     (long long)g_.row0, (long long)g_.col0, L_.R, t_->name().c_str(),
+                     (long long)g_.row0, (long long)g_.col0, L_.R, t_->name().c_str(), wg.c_str(),
                      cfg_.compat ? ", compat=reference" : "");
 }
 

@@ -169,3 +169,30 @@ def test_profile_and_metrics_on_gpu(gol_bin, tmp_path):
     m = json.loads(path.read_text())
     assert m["backend"] == "hip" and m["t_compute_ms"] > 0 and m["t_exchange_ms"] >= 0
     assert m["kernel"] and m["schedule"] in ("split", "full")
+
+
+@pytest.mark.parametrize("threads,waves", [(256, 4), (512, 8), (1024, 16), (100, 8)])
+def test_threads_per_block_selects_tile_workgroup(gol_bin, tmp_path, threads, waves):
+    """threadsPerBlock is the LDS tile kernel's workgroup size (T/64 waves); invalid -> default 8."""
+    N, gens = 512, 37
+    r = _run(gol_bin, [5, N, gens, threads, 1], tmp_path, 1, {"GOL_KERNEL": "tile"})
+    assert r.returncode == 0, r.stderr
+    assert f"tile workgroup {waves} waves" in r.stderr
+    assert ("threadsPerBlock=100" in r.stderr) == (threads == 100)
+    assert np.array_equal(_board(tmp_path, 1), numpy_step(initial_board(5, N, 1, True), gens))
+
+
+def test_perf_smoke_8192(gol_bin, tmp_path):
+    """SURVEY §4.3 perf smoke: 8192^2 x 1000 generations through the CLI, cell-updates/s above a floor.
+
+    Measured ≈3.6e13/s on one MI355X (docs/PERFORMANCE.md); the floor (1e13) catches a fallback to a
+    slow path (e.g. the yardstick byte kernel runs at ≈4e11) without flaking on a shared box."""
+    import re
+
+    r = _run(gol_bin, [5, 8192, 1000, 512, 0], tmp_path, 1)
+    assert r.returncode == 0, r.stderr
+    m = re.match(r"TOTAL DURATION : ([0-9.]+), number of cell updates = (\d+)\n", r.stdout)
+    assert m, r.stdout
+    secs, updates = float(m.group(1)), int(m.group(2))
+    assert updates == 8192 * 8192 * 1000
+    assert updates / secs > 1e13, f"{updates / secs:.3e} cell-updates/s"
