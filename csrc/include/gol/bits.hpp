@@ -8,10 +8,14 @@
 //   1. per row, the horizontal sum h = left + centre + right  (2 bits: s0 = xor3, s1 = maj)
 //   2. T = h(row-1) + h(row) + h(row+1):
 //        x0 = xor3(s0's), cy = maj(s0's), u0 = xor3(s1's), u1 = maj(s1's)
-//        T  = x0 + 2*(cy + u0 + 2*u1) = x0 + 2*y
-//      T == 3  <=>  x0 & (y == 1)  <=>  x0 & ~u1 & (u0 ^ cy)
-//      T == 4  <=> ~x0 & (y == 2)  <=> ~x0 & (u1 ? ~u0 & ~cy : u0 & cy)
-// Every step is a 3-input boolean function, i.e. one v_bitop3_b32 on gfx950.
+//        T  = x0 + 2*(cy + u0 + 2*u1)
+//   3. next = [T in {3,4}] & (x0 | alive)   (T == 3 is the odd one), where, in two 3-input steps,
+//        g1 = exactly one of (x0, cy, u1)
+//        [T in {3,4}] = (u0, u1, g1) in {(0,0,0), (0,1,1), (1,0,1)}
+//      (an exhaustive search over 3-input gate circuits; it uses the don't-care "alive with T = 0",
+//      impossible because T counts the centre.  The textbook form needs 4 steps here.)
+// Every step is a 3-input boolean function, i.e. one v_bitop3_b32 on gfx950: 7 per word-half for
+// the vertical sum and the rule, 2 for the row's horizontal sum.
 #pragma once
 
 #include "gol/common.hpp"
@@ -34,12 +38,14 @@ constexpr unsigned lut3(F f) {
 
 constexpr unsigned kLutXor3 = 0x96;  // a ^ b ^ c
 constexpr unsigned kLutMaj = 0xE8;   // majority(a, b, c)
-constexpr unsigned kLutY1 = lut3([](unsigned u1, unsigned u0, unsigned cy) { return ~u1 & (u0 ^ cy); });
-constexpr unsigned kLutY2 = lut3([](unsigned u1, unsigned u0, unsigned cy) {
-    return (u1 & ~u0 & ~cy) | (~u1 & u0 & cy);
+constexpr unsigned kLutOne3 = lut3([](unsigned x0, unsigned cy, unsigned u1) {
+    return (x0 & ~cy & ~u1) | (~x0 & cy & ~u1) | (~x0 & ~cy & u1);
 });
-constexpr unsigned kLutBorn4 = lut3([](unsigned x0, unsigned x, unsigned y2) { return ~x0 & x & y2; });
-constexpr unsigned kLutOut = lut3([](unsigned x0, unsigned y1, unsigned t) { return (x0 & y1) | t; });
+constexpr unsigned kLutT34 = lut3([](unsigned u0, unsigned u1, unsigned g1) {
+    return (~u0 & ~u1 & ~g1) | (~u0 & u1 & g1) | (u0 & ~u1 & g1);
+});
+constexpr unsigned kLutNext = lut3([](unsigned x0, unsigned alive, unsigned t34) { return t34 & (x0 | alive); });
+static_assert(kLutOne3 == 0x16 && kLutT34 == 0x29 && kLutNext == 0xA8, "rule LUTs");
 
 // Host/reference evaluation of a 3-input LUT on 64-bit words.
 GOL_HD u64 bitop3_ref(u64 a, u64 b, u64 c, unsigned lut) {
@@ -110,9 +116,9 @@ GOL_HD u64 rule64(u64 a0, u64 a1, u64 b0, u64 b1, u64 c0, u64 c1, u64 x) {
     u64 cy = (a0 & b0) | (a0 & c0) | (b0 & c0);
     u64 u0 = a1 ^ b1 ^ c1;
     u64 u1 = (a1 & b1) | (a1 & c1) | (b1 & c1);
-    u64 y1 = ~u1 & (u0 ^ cy);
-    u64 y2 = (u1 & ~u0 & ~cy) | (~u1 & u0 & cy);
-    return (x0 & y1) | (~x0 & x & y2);
+    u64 g1 = (x0 ^ cy ^ u1) & ~(x0 & cy & u1);    // kLutOne3
+    u64 t34 = (g1 & (u0 ^ u1)) | ~(g1 | u0 | u1);  // kLutT34
+    return t34 & (x0 | x);                          // kLutNext
 }
 
 // Word accessors for the bit-level helpers below: natural words as stored, or split-format

@@ -275,17 +275,37 @@ class HipEngine : public Engine {
         return {h_red_[0], h_red_[1]};
     }
 
-    void run_graphed(u64& generations) {
-        const int k = cfg_.compat ? 1 : L_.R;
-        int m = cfg_.graph_supersteps;
+    // Graph shape of run(): m supersteps of k generations per replay; false when run() stays eager.
+    bool graph_shape(int& k, int& m) {
+        if (!cfg_.graph || cfg_.profile) return false;
+        k = cfg_.compat ? 1 : L_.R;
+        m = cfg_.graph_supersteps;
         if (m <= 0) m = k >= 8 ? 16 : 32;
         m += m & 1;  // even: the graph returns to the same buffer parity
-        const u64 per = (u64)m * (u64)k;
         bool local = cfg_.compat || halo_items(k).empty();
-        if (!local && !device_transport_) return;  // host-staged exchange cannot be captured
+        if (!local && !device_transport_) return false;  // host-staged exchange cannot be captured
         // RCCL inside captured graphs is opt-in: with R-deep supersteps (hundreds of us each) the
         // eager launch cost is negligible, and an eager exchange keeps RCCL's own error handling.
-        if (!local && !cfg_.graph_rccl) return;
+        if (!local && !cfg_.graph_rccl) return false;
+        return true;
+    }
+
+    // Capture, instantiate and upload the replay graph at init, so no timed run() ever pays for
+    // stream capture or graph instantiation (a 16-superstep capture costs milliseconds: more than
+    // a whole 8192^2 x 1000 run).
+    void prewarm_graph() {
+        int k = 0, m = 0;
+        if (!graph_shape(k, m)) return;
+        hipGraphExec_t exec = graph_for(k, m);
+        if (exec) HIP_CHECK(hipGraphUpload(exec, s_comp_));
+        mark_ready();
+        synchronize();
+    }
+
+    void run_graphed(u64& generations) {
+        int k = 0, m = 0;
+        if (!graph_shape(k, m)) return;
+        const u64 per = (u64)m * (u64)k;
         while (generations >= per && graph_ok_) {
             hipGraphExec_t exec = graph_for(k, m);
             if (!exec) break;
@@ -308,7 +328,7 @@ class HipEngine : public Engine {
 
     void run(u64 generations) override {
         Armed armed(wd_.get());
-        if (cfg_.graph && !cfg_.profile) run_graphed(generations);
+        run_graphed(generations);
         Engine::run(generations);
     }
 
@@ -358,6 +378,7 @@ class HipEngine : public Engine {
         // neither graph capture nor a timed loop ever builds or uploads a plan.
         for (int k = 1; k <= (cfg_.compat ? 1 : L_.R); ++k)
             if (supported_depth(k) == k) prepare(k);
+        prewarm_graph();
         const DevPlan& fp = full_plan_stats();
         stats_.plan_waves = fp.waves;
         stats_.lane_efficiency =
@@ -875,7 +896,9 @@ class HipEngine : public Engine {
 
     // ----- graphs -----
     hipGraphExec_t graph_for(int k, int m) {
-        const int key = k * 1000 + m;
+        // the captured kernels bake in the buffer pointers, so a replay must start at the parity
+        // it was captured at (an odd-pass remainder superstep flips it between run() calls)
+        const int key = (k * 1000 + m) * 2 + cur_;
         auto it = graphs_.find(key);
         if (it != graphs_.end()) return it->second;
         prepare(k);

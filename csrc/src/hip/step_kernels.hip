@@ -12,8 +12,8 @@
 //    are shifted: the previous lane's hi (v_mov_b32_dpp wave_shr:1) funnelled into hi, and the next
 //    lane's lo (wave_shl:1) funnelled into lo, one v_alignbit_b32 each — no LDS, no barriers.
 //  * Bit-sliced counting: per row the horizontal 3-sum (xor3 / maj = 1 v_bitop3 each), then the
-//    vertical 3-sum of those 2-bit sums and the rule in 8 more v_bitop3 (bits.hpp): 12 VALU ops per
-//    32 cells per generation (13 with natural bit order, which needs 4 funnel shifts per word).
+//    vertical 3-sum of those 2-bit sums and the rule in 7 more v_bitop3 (bits.hpp): 11 VALU ops per
+//    32 cells per generation (12 with natural bit order, which needs 4 funnel shifts per word).
 //  * Temporal blocking: K generation levels are chained in registers.  Level l keeps a 3-row
 //    window (horizontal sums of rows r-2, r-1 and its centre row); when a row arrives at level l it
 //    emits row r-1 of generation l+1 to level l+1.  One HBM pass = K generations, so the kernel is
@@ -56,10 +56,9 @@ __device__ __forceinline__ u32 rule32(u32 a0, u32 a1, u32 b0, u32 b1, u32 c0, u3
     const u32 cy = b3<kLutMaj>(a0, b0, c0);
     const u32 u0 = b3<kLutXor3>(a1, b1, c1);
     const u32 u1 = b3<kLutMaj>(a1, b1, c1);
-    const u32 y1 = b3<kLutY1>(u1, u0, cy);
-    const u32 y2 = b3<kLutY2>(u1, u0, cy);
-    const u32 t = b3<kLutBorn4>(x0, x, y2);
-    return b3<kLutOut>(x0, y1, t);
+    const u32 g1 = b3<kLutOne3>(x0, cy, u1);
+    const u32 t34 = b3<kLutT34>(u0, u1, g1);
+    return b3<kLutNext>(x0, x, t34);
 }
 
 // Horizontal 3-sums of one split-format word (bits.hpp: lo = even columns, hi = odd columns).

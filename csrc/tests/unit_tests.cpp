@@ -281,7 +281,7 @@ static void test_dump() {
 }
 
 static void test_bits() {
-    CHECK(bitop3_ref(0xF0, 0xCC, 0xAA, kLutXor3) == (0xF0ull ^ 0xCC ^ 0xAA) && kLutY1 != kLutY2);
+    CHECK(bitop3_ref(0xF0, 0xCC, 0xAA, kLutXor3) == (0xF0ull ^ 0xCC ^ 0xAA) && kLutOne3 != kLutT34);
     std::vector<u64> row = {0x8000000000000001ull};
     CHECK(wrap64(row.data(), 64, -64) == row[0] && wrap64(row.data(), 64, 1) == ((row[0] >> 1) | (row[0] << 63)));
     std::vector<u64> r5 = {0b10011ull};  // width 5: periodic 1 1 0 0 1

@@ -60,6 +60,19 @@ def test_graph_replay(gol, graph):
     assert np.array_equal(s.board(), numpy_step(initial_board(5, N, 1, True, 11), gens))
 
 
+def test_graph_replay_after_parity_flip(gol):
+    """Replays are keyed by buffer parity: a remainder superstep with an odd pass count (8 of R=16,
+    K=8) between two graphed runs must not replay a graph captured at the other parity."""
+    N = 512
+    s = _sim(gol, N, halo_depth=16, kernel_depth=8, kernel="temporal").init(5, seed=12)
+    total = 0
+    for gens in (16 * 16, 8, 16 * 16, 8, 16 * 16 + 3):
+        s.step(gens)
+        total += gens
+    assert s.stats()["graph_launches"] >= 3
+    assert np.array_equal(s.board(), numpy_step(initial_board(5, N, 1, True, 12), total))
+
+
 def test_large_board_vs_torch_conv(gol):
     import torch
 

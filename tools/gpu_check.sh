@@ -17,7 +17,7 @@ step() {  # step <name> <timeout> <cmd...>
 rocminfo 2>/dev/null | grep -m3 -E "Marketing|gfx950|Compute Unit" > gpurun_out/rocminfo.txt
 for s in "$@"; do
   case $s in
-    tests)  step pytest_gpu 600 python -m pytest tests -x -q -m gpu ;;
+    tests)  step pytest_gpu 900 python -u -m pytest tests -x -v -m gpu --timeout 120 --timeout-method thread ;;
     smoke)  step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench)  step bench 600 python bench.py --steps 2000 --warmup 200 --yardstick ;;
     prof)   step prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o prof --output-format csv -- python3 bench.py --steps 400 --warmup 40 ;;
