@@ -108,6 +108,7 @@ class HipEngine : public Engine {
                      can_overlap() && !(self_x() && !L_.aligned()) &&
                      ((device_transport_ && !halo_items(L_.R).empty()) || cfg_.force_split);
         create_streams();
+        events_needed_ = edge_mode_ || cfg_.force_split || !halo_items(L_.R).empty();
         // All device memory work is ordered on the engine's own streams.  (They are non-blocking:
         // null-stream calls such as hipMemset, or a pageable hipMemcpy whose DMA may still be in
         // flight when it returns, would NOT be ordered before their kernels.)
@@ -182,6 +183,10 @@ class HipEngine : public Engine {
     // Every buffer-writing operation on the compute stream ends with this: the next superstep's
     // waits (ready / interior / boundary) all see completed work.
     void mark_ready() {
+        // Nothing waits on these when the compute stream is the only stream (no exchange, no
+        // split schedule): skip them — an event record between two kernels costs ~15 us on the
+        // GPU (a release fence), measured between eager supersteps on one MI355X.
+        if (!events_needed_) return;
         HIP_CHECK(hipEventRecord(ev_ready_, s_comp_));
         HIP_CHECK(hipEventRecord(ev_int_, s_comp_));
         HIP_CHECK(hipEventRecord(ev_bnd_, s_comp_));
@@ -201,6 +206,7 @@ class HipEngine : public Engine {
         for (auto& v : {&hstage_s_, &hstage_r_})
             for (u64* p : *v) hipHostFree(p);
         for (int i = 0; i < 2; ++i) hipFree(buf_[i]);
+        for (void* p : deferred_free_) hipFree(p);
         hipFree(d_red_);
         hipHostFree(h_red_);
         hipEventDestroy(ev_ready_);
@@ -238,8 +244,11 @@ class HipEngine : public Engine {
     std::vector<u64> tile_words() override {
         synchronize();
         std::vector<u64> d((size_t)(L_.h * L_.nw));
-        HIP_CHECK(hipMemcpy2D(d.data(), (size_t)L_.nw * 8, buf_[cur_] + L_.index(0, 0), (size_t)L_.pitch * 8,
-                              (size_t)L_.nw * 8, (size_t)L_.h, hipMemcpyDeviceToHost));
+        // stream-ordered (never the legacy null stream: in thread mode another rank's engine may be
+        // capturing a graph, and a null-stream copy would have to depend on the capturing stream)
+        HIP_CHECK(hipMemcpy2DAsync(d.data(), (size_t)L_.nw * 8, buf_[cur_] + L_.index(0, 0), (size_t)L_.pitch * 8,
+                                   (size_t)L_.nw * 8, (size_t)L_.h, hipMemcpyDeviceToHost, s_comp_));
+        HIP_CHECK(hipStreamSynchronize(s_comp_));
         // device storage is split-format (bits.hpp); the API is natural-order words
         for (i64 r = 0; r < L_.h; ++r)
             for (i64 c = 0; c < L_.nw; ++c) {
@@ -290,41 +299,64 @@ class HipEngine : public Engine {
         return true;
     }
 
-    // Capture, instantiate and upload the replay graph at init, so no timed run() ever pays for
+    // Capture and instantiate the replay graphs at init, so no timed run() ever pays for
     // stream capture or graph instantiation (a 16-superstep capture costs milliseconds: more than
     // a whole 8192^2 x 1000 run).
     void prewarm_graph() {
-        int k = 0, m = 0;
-        if (!graph_shape(k, m)) return;
-        hipGraphExec_t exec = graph_for(k, m);
-        if (exec) HIP_CHECK(hipGraphUpload(exec, s_comp_));
+        int k = 0, M = 0;
+        if (!graph_shape(k, M)) return;
+        for (int m : {M, 4, 1}) {
+            if (m > M) continue;
+            // both parities: a remainder graph of odd pass count leaves the other one current
+            for (int par = 0; par < 2; ++par) {
+                const int cur0 = cur_;
+                cur_ = par;
+                graph_for(k, m);
+                cur_ = cur0;
+            }
+        }
         mark_ready();
         synchronize();
     }
 
+    // Replays: graphs of m supersteps, then of 4 and 1 for the remainder (eager launches of a
+    // superstep cost ~15 us of GPU idle each; graph replays none), every size captured at init.
     void run_graphed(u64& generations) {
-        int k = 0, m = 0;
-        if (!graph_shape(k, m)) return;
+        int k = 0, M = 0;
+        if (!graph_shape(k, M)) return;
+        for (int m : {M, 4, 1}) {
+            if (m > M) continue;
+            const u64 per = (u64)m * (u64)k;
+            while (generations >= per && graph_ok_) {
+                hipGraphExec_t exec = graph_for(k, m);
+                if (!exec) return;
+                replay(exec, k, m);
+                generations -= per;
+            }
+        }
+    }
+
+    void replay(hipGraphExec_t exec, int k, int m) {
         const u64 per = (u64)m * (u64)k;
-        while (generations >= per && graph_ok_) {
-            hipGraphExec_t exec = graph_for(k, m);
-            if (!exec) break;
+        {
             maybe_inject_fault();
             {
                 trace::Range r("gol.graph_launch");
                 HIP_CHECK(hipGraphLaunch(exec, s_comp_));
             }
+            cur_ ^= graph_flip(k, m);
             // Events recorded during capture are not re-recorded by replays: re-mark them after
             // the graph so later eager supersteps (and the comm stream) wait for its work.
             mark_ready();
             gen_ += per;
-            generations -= per;
             stats_.generations += per;
             stats_.supersteps += (u64)m;
             stats_.graph_launches += 1;
             progress("graph");
         }
     }
+    // Buffer-parity flip of m supersteps of k generations (one flip per kernel pass).
+    int graph_flip(int k, int m) { return (int)((pass_depths(k).size() * (size_t)m) & 1); }
 
     void run(u64 generations) override {
         Armed armed(wd_.get());
@@ -359,9 +391,10 @@ class HipEngine : public Engine {
         HIP_CHECK(hipGetLastError());
         mark_ready();
         synchronize();
-        if (dcells) HIP_CHECK(hipFree(dcells));
+        if (dcells) deferred_free_.push_back(dcells);  // hipFree may synchronise the whole device
         split_ = split_used() && (cfg_.sched == "auto" || cfg_.sched == "split");
         if (!tuned_) {
+            spin_up();
             if (cfg_.kernel == "auto") autotune_kernel();
             autotune_schedule();
             tuned_ = true;
@@ -395,9 +428,9 @@ class HipEngine : public Engine {
             const i64 e = ext_after(ps, j);
             launch(0, ps[j], e, buf_[cur_], buf_[cur_ ^ 1], s_comp_);
             post(buf_[cur_ ^ 1], s_comp_, e);
-            mark_ready();
             cur_ ^= 1;
         }
+        if (ps.size() > 1) mark_ready();  // the next exchange reads what the last pass wrote
     }
 
     // Kernel passes of a superstep of k generations (each <= the kernel depth), and the rows beyond
@@ -507,6 +540,26 @@ class HipEngine : public Engine {
         mark_ready();
     }
 
+    // Bring the GPU to its steady clock before anything is timed.  From idle, sclk ramps up over
+    // the first ~20-30 ms of load (measured on MI355X: 32768^2 passes shrink from ~97 to ~87 us
+    // while rocm-smi shows sclk rising to 2.4 GHz), which would bias the kernel autotune towards
+    // whichever candidate runs last and make the first generations of a run slower than the rest.
+    // The full-board kernel runs on the scratch buffer (the board is untouched) for GOL_SPINUP_MS
+    // (default 100 ms for boards of >= 2^24 cells, 20 ms below; 0 = off).
+    void spin_up() {
+        const bool big = (double)L_.h * (double)L_.w >= (double)(1 << 24);
+        const double budget_ms = (double)env_int("GOL_SPINUP_MS", big ? 100 : 20);
+        if (budget_ms <= 0 || cfg_.compat || kernel_ == "lds") return;
+        const int k = tile_kernel(0) ? kdepth_ : supported_kernel_depth(std::min(kdepth_, hipk::max_step_depth()));
+        const auto t0 = std::chrono::steady_clock::now();
+        for (int it = 0; it < 100000; ++it) {
+            for (int j = 0; j < 4; ++j) launch(0, k, 0, buf_[cur_], buf_[cur_ ^ 1], s_comp_);
+            HIP_CHECK(hipStreamSynchronize(s_comp_));
+            const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+            if (ms >= budget_ms) break;
+        }
+    }
+
     // With neighbours, pick the superstep schedule by measurement: every rank times a few
     // supersteps of each schedule on the scratch buffer (the exchange writes the same halo rows a
     // real superstep would, the kernels write the scratch buffer; parity is not flipped), and the
@@ -556,7 +609,9 @@ class HipEngine : public Engine {
     std::vector<u64> read_row(i64 r) override {
         synchronize();
         std::vector<u64> row((size_t)L_.pitch);
-        HIP_CHECK(hipMemcpy(row.data(), buf_[cur_] + L_.index(r, -1), (size_t)L_.pitch * 8, hipMemcpyDeviceToHost));
+        HIP_CHECK(hipMemcpyAsync(row.data(), buf_[cur_] + L_.index(r, -1), (size_t)L_.pitch * 8, hipMemcpyDeviceToHost,
+                                 s_comp_));
+        HIP_CHECK(hipStreamSynchronize(s_comp_));
         return row;
     }
 
@@ -923,7 +978,7 @@ class HipEngine : public Engine {
             mark_ready();
             return nullptr;
         }
-        if (cur_ != cur0) throw Error("graph capture changed the buffer parity");
+        cur_ = cur0;  // capture does not execute: the replay flips the parity (graph_flip)
         graphs_[key] = exec;
         return exec;
     }
@@ -982,6 +1037,8 @@ class HipEngine : public Engine {
     u64* h_red_ = nullptr;
     bool device_transport_ = false;
     bool graph_ok_ = true;
+    bool events_needed_ = true;
+    std::vector<void*> deferred_free_;  // another stream waits on ev_ready_ / ev_int_ / ev_bnd_
     std::map<int, DevPlan> plans_;
     std::map<int, DevCopies> copies_;
     std::map<int, std::vector<HaloItem>> items_;

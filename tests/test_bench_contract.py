@@ -1,0 +1,48 @@
+"""bench.py driver contract on CPU: exactly one JSON line from rank 0 with the BASELINE.json metric,
+for a single process and for a 2-rank torch.distributed.run (gloo) launch — the same launch line the
+driver uses on an 8-GPU node."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+KEYS = {"metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+        "vs_baseline", "dtype", "data", "config"}
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _run(cmd):
+    env = dict(os.environ, OMP_NUM_THREADS="1")
+    r = subprocess.run(cmd, cwd=REPO, env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    out = json.loads(lines[0])
+    assert KEYS <= set(out), sorted(KEYS - set(out))
+    with open(os.path.join(REPO, "BASELINE.json")) as f:
+        assert out["metric"] == json.load(f)["metric"]
+    assert out["value"] > 0 and out["higher_is_better"] is True
+    assert out["steps"] == 20 and out["warmup"] == 2
+    return out
+
+
+def test_bench_single_process():
+    out = _run([sys.executable, "bench.py", "--steps", "20", "--warmup", "2"])
+    assert out["config"]["parallelism"].endswith("p1 (1x1)")
+
+
+def test_bench_torchrun_two_ranks():
+    out = _run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), "bench.py", "--gpus", "2",
+                "--steps", "20", "--warmup", "2"])
+    cfg = out["config"]
+    assert cfg["parallelism"].endswith("p2 (1x2)")
+    # weak scaling: every rank owns a full tile, the global board grows with the rank count
+    assert cfg["board"][0] == 2 * cfg["tile_per_rank"][0]

@@ -60,16 +60,17 @@ def test_graph_replay(gol, graph):
     assert np.array_equal(s.board(), numpy_step(initial_board(5, N, 1, True, 11), gens))
 
 
-def test_graph_replay_after_parity_flip(gol):
-    """Replays are keyed by buffer parity: a remainder superstep with an odd pass count (8 of R=16,
-    K=8) between two graphed runs must not replay a graph captured at the other parity."""
+@pytest.mark.parametrize("R,K", [(16, 8), (8, 8), (24, 8)])
+def test_graph_replay_after_parity_flip(gol, R, K):
+    """Replays are keyed by buffer parity and track it: graphs of 16, 4 and 1 supersteps (1 or 3
+    passes per superstep flip the parity per superstep) interleaved with eager remainders."""
     N = 512
-    s = _sim(gol, N, halo_depth=16, kernel_depth=8, kernel="temporal").init(5, seed=12)
+    s = _sim(gol, N, halo_depth=R, kernel_depth=K, kernel="temporal").init(5, seed=12)
     total = 0
-    for gens in (16 * 16, 8, 16 * 16, 8, 16 * 16 + 3):
+    for gens in (R * 16, 8, R * 21 + 3, 5, R * 16 + R * 4 + R + 7, 2 * R + 1):
         s.step(gens)
         total += gens
-    assert s.stats()["graph_launches"] >= 3
+    assert s.stats()["graph_launches"] >= 6
     assert np.array_equal(s.board(), numpy_step(initial_board(5, N, 1, True, 12), total))
 
 
