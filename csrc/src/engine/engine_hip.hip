@@ -394,7 +394,6 @@ class HipEngine : public Engine {
         if (dcells) deferred_free_.push_back(dcells);  // hipFree may synchronise the whole device
         split_ = split_used() && (cfg_.sched == "auto" || cfg_.sched == "split");
         if (!tuned_) {
-            spin_up();
             if (cfg_.kernel == "auto") autotune_kernel();
             autotune_schedule();
             tuned_ = true;
@@ -412,6 +411,7 @@ class HipEngine : public Engine {
         for (int k = 1; k <= (cfg_.compat ? 1 : L_.R); ++k)
             if (supported_depth(k) == k) prepare(k);
         prewarm_graph();
+        spin_up();  // init ends with the GPU at its steady clock (plan building and captures idle it)
         const DevPlan& fp = full_plan_stats();
         stats_.plan_waves = fp.waves;
         stats_.lane_efficiency =
@@ -550,6 +550,8 @@ class HipEngine : public Engine {
         const bool big = (double)L_.h * (double)L_.w >= (double)(1 << 24);
         const double budget_ms = (double)env_int("GOL_SPINUP_MS", big ? 100 : 20);
         if (budget_ms <= 0 || cfg_.compat || kernel_ == "lds") return;
+        const std::string saved = kern_[0];
+        if (cfg_.kernel != "tile") kern_[0] = "temporal";  // the register kernel runs on any board
         const int k = tile_kernel(0) ? kdepth_ : supported_kernel_depth(std::min(kdepth_, hipk::max_step_depth()));
         const auto t0 = std::chrono::steady_clock::now();
         for (int it = 0; it < 100000; ++it) {
@@ -558,6 +560,7 @@ class HipEngine : public Engine {
             const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
             if (ms >= budget_ms) break;
         }
+        kern_[0] = saved;
     }
 
     // With neighbours, pick the superstep schedule by measurement: every rank times a few
@@ -663,11 +666,18 @@ class HipEngine : public Engine {
         HIP_CHECK(hipEventCreate(&e0));
         HIP_CHECK(hipEventCreate(&e1));
         // time one pass of kernel `kern` at depth k on plan `kind`; returns ms per generation
-        auto time_pass = [&](int kind, const char* kern, int k) -> float {
+        // build_only: construct (and upload) the plan only.  Every plan of a tuning round is built
+        // before the GPU is spun up and the kernels are timed: building a tile plan for a large
+        // board is ~0.1 s of host work, long enough for the clock to drop again.
+        auto time_pass = [&](int kind, const char* kern, int k, bool build_only = false) -> float {
             kern_[kind] = kern;
             if (kern_[kind] == "tile" && (hipk::tile_max_rows(k) < 1 || tile_rounds(kind, k, 0) > kMaxTileRounds))
                 return 1e30f;  // LDS tiles only pay off for small regions (docs/PERFORMANCE.md)
             if (kern_[kind] == "temporal" && !hipk::step_depth_supported(k)) return 1e30f;
+            if (build_only) {
+                plan(kind, k, 0);
+                return 0.f;
+            }
             hipStream_t s = (kind == 2 && edge_mode_) ? s_comm_ : s_comp_;
             launch(kind, k, 0, buf_[cur_], buf_[cur_ ^ 1], s);  // warm-up (and plan build)
             HIP_CHECK(hipEventRecord(e0, s));
@@ -686,6 +696,8 @@ class HipEngine : public Engine {
         std::vector<std::pair<const char*, int>> cands = {{"temporal", k0}, {"tile", k0}};
         const int k2 = supported_kernel_depth(std::min({2 * k0, L_.R, 32}));
         if (!cfg_.compat && cfg_.kernel_depth == 0 && k2 > k0) cands.push_back({"tile", k2});
+        for (const auto& c : cands) time_pass(0, c.first, c.second, true);
+        spin_up();
         float best = 1e30f;
         std::pair<const char*, int> pick = cands[0];
         for (const auto& c : cands) {
@@ -700,6 +712,9 @@ class HipEngine : public Engine {
         passes_.clear();
         // interior / boundary plans of split supersteps, at the chosen pass depth
         if (split_used()) {
+            for (int kind : {1, 2})
+                for (const char* c : {"temporal", "tile"}) time_pass(kind, c, kdepth_, true);
+            spin_up();
             for (int kind : {1, 2}) {
                 float bk = 1e30f;
                 const char* pk = "temporal";
