@@ -151,6 +151,7 @@ def main() -> int:
                 "halo_depth": st["depth"],
                 "kernel_depth": st["kernel_depth"],
                 "kernel": st["kernel"],
+                "tile_waves": st["tile_waves"],
                 "schedule": st["schedule"],
                 "autotune": st["tuning"],
                 "graph_launches": st["graph_launches"],

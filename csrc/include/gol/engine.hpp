@@ -44,6 +44,7 @@ struct EngineConfig {
     std::string kernel = "auto";      // auto (timed at init) | temporal (register pipeline) |
                                       // tile (LDS-resident) | lds (1 gen, reference-class LDS tile)
     int tile_waves = 8;               // tile kernel: waves per workgroup (4, 8, 16)
+    bool tune_tile_waves = true;      // GOL_KERNEL=auto may also try 8 waves (false: GOL_TILE_WAVES set)
     std::string prefetch = "reg";     // temporal kernel row prefetch: reg (pinned triple) | lds (DMA ring)
     std::string pipeline = "chain";   // temporal kernel level pipeline: chain | skew (ILP variant)
     std::string transport = "auto";   // auto | device | host  (host = stage halos through host memory)
@@ -64,6 +65,7 @@ struct EngineStats {
     u64 graph_launches = 0;
     int depth = 0;            // R (generations per halo exchange)
     int kernel_depth = 0;     // K (generations per kernel pass)
+    int tile_waves = 0;       // HIP: workgroup size of the LDS tile kernel (waves)
     i64 plan_waves = 0;       // waves of the full-tile plan
     double lane_efficiency = 0;  // output words / (64 * input rows * waves) for the full plan
     double t_exchange_ms = 0;  // profile only

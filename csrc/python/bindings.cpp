@@ -105,6 +105,7 @@ py::dict stats_dict(const EngineStats& s) {
     d["kernel"] = s.kernel;
     d["schedule"] = s.schedule;
     d["kernel_depth"] = s.kernel_depth;
+    d["tile_waves"] = s.tile_waves;
     d["tuning"] = s.tuning;
     return d;
 }
@@ -251,6 +252,7 @@ PYBIND11_MODULE(_gol, m) {
         .def_readwrite("graph_supersteps", &EngineConfig::graph_supersteps)
         .def_readwrite("watchdog_s", &EngineConfig::watchdog_s)
         .def_readwrite("tile_waves", &EngineConfig::tile_waves)
+        .def_readwrite("tune_tile_waves", &EngineConfig::tune_tile_waves)
         .def_readwrite("edge_cus", &EngineConfig::edge_cus)
         .def_readwrite("force_split", &EngineConfig::force_split)
         .def_readwrite("sched", &EngineConfig::sched)

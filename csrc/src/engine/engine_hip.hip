@@ -401,6 +401,7 @@ class HipEngine : public Engine {
         stats_.kernel = split_ ? kern_[1] + "+boundary:" + kern_[2] : kern_[0];
         stats_.schedule = split_ ? "split" : (halo_items(L_.R).empty() ? "local" : "full");
         stats_.kernel_depth = kdepth_;
+        stats_.tile_waves = cfg_.tile_waves;
         std::string tn;
         for (const auto& kv : tune_ms_) tn += strprintf("%s%s=%.3fus/gen", tn.empty() ? "" : " ", kv.first.c_str(), kv.second * 1e3);
         if (sched_ms_[0] > 0)
@@ -678,6 +679,7 @@ class HipEngine : public Engine {
                 plan(kind, k, 0);
                 return 0.f;
             }
+            const bool tile = kern_[kind] == "tile";
             hipStream_t s = (kind == 2 && edge_mode_) ? s_comm_ : s_comp_;
             launch(kind, k, 0, buf_[cur_], buf_[cur_ ^ 1], s);  // warm-up (and plan build)
             HIP_CHECK(hipEventRecord(e0, s));
@@ -687,28 +689,43 @@ class HipEngine : public Engine {
             float ms = 0;
             HIP_CHECK(hipEventElapsedTime(&ms, e0, e1));
             const float per_gen = ms / 3 / (float)k;
-            tune_ms_[strprintf("%d:%s@%d", kind, kern, k)] = per_gen;
+            tune_ms_[tile ? strprintf("%d:%s@%dx%dw", kind, kern, k, cfg_.tile_waves) : strprintf("%d:%s@%d", kind, kern, k)] =
+                per_gen;
             return per_gen;
         };
         // full-tile kernel and pass depth: the register pipeline at the auto depth, the LDS tile
         // kernel at that depth and (deeper passes amortise its staging) twice that depth
+        // The tile workgroup size (the threadsPerBlock hint, or GOL_TILE_WAVES) is a candidate
+        // dimension too unless GOL_TILE_WAVES fixed it: the measured default, 8 waves, is also tried.
+        struct Cand {
+            const char* kern;
+            int k, nw;
+        };
         const int k0 = cfg_.compat ? 1 : kdepth_;
-        std::vector<std::pair<const char*, int>> cands = {{"temporal", k0}, {"tile", k0}};
+        const int nw0 = cfg_.tile_waves;
+        std::vector<int> nws = {nw0};
+        if (cfg_.tune_tile_waves && nw0 != 8) nws.push_back(8);
+        std::vector<Cand> cands = {{"temporal", k0, nw0}};
         const int k2 = supported_kernel_depth(std::min({2 * k0, L_.R, 32}));
-        if (!cfg_.compat && cfg_.kernel_depth == 0 && k2 > k0) cands.push_back({"tile", k2});
-        for (const auto& c : cands) time_pass(0, c.first, c.second, true);
+        for (int nw : nws) {
+            cands.push_back({"tile", k0, nw});
+            if (!cfg_.compat && cfg_.kernel_depth == 0 && k2 > k0) cands.push_back({"tile", k2, nw});
+        }
+        for (const auto& c : cands) time_pass(0, c.kern, c.k, true);
         spin_up();
         float best = 1e30f;
-        std::pair<const char*, int> pick = cands[0];
+        Cand pick = cands[0];
         for (const auto& c : cands) {
-            const float t = time_pass(0, c.first, c.second);
+            cfg_.tile_waves = c.nw;
+            const float t = time_pass(0, c.kern, c.k);
             if (t < best) {
                 best = t;
                 pick = c;
             }
         }
-        kern_[0] = pick.first;
-        kdepth_ = pick.second;
+        kern_[0] = pick.kern;
+        kdepth_ = pick.k;
+        cfg_.tile_waves = pick.nw;
         passes_.clear();
         // interior / boundary plans of split supersteps, at the chosen pass depth
         if (split_used()) {

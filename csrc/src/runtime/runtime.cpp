@@ -167,6 +167,7 @@ EngineConfig engine_config(const Options& o, const std::string& backend, int dev
     c.waves_target = o.waves_target;
     c.kernel = env_str("GOL_KERNEL", "auto");
     c.tile_waves = (int)env_int("GOL_TILE_WAVES", 8);
+    c.tune_tile_waves = getenv("GOL_TILE_WAVES") == nullptr;
     c.prefetch = env_str("GOL_PREFETCH", "reg");
     c.pipeline = env_str("GOL_PIPELINE", "chain");
     c.transport = (o.transport == "rccl" || o.transport == "p2p") ? "device" : o.transport;

@@ -112,6 +112,7 @@ class Simulation:
         cfg.profile = profile
         cfg.watchdog_s = float(watchdog)
         cfg.tile_waves = int(tile_waves)
+        cfg.tune_tile_waves = "GOL_TILE_WAVES" not in os.environ
         cfg.edge_cus = int(edge_cus)
         cfg.force_split = bool(force_split)
         cfg.sched = schedule
