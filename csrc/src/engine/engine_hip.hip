@@ -114,10 +114,14 @@ class HipEngine : public Engine {
         // flight when it returns, would NOT be ordered before their kernels.)
         for (int i = 0; i < 2; ++i) HIP_CHECK(hipMemsetAsync(buf_[i], 0, bytes, s_comp_));
         HIP_CHECK(hipStreamSynchronize(s_comp_));
-        HIP_CHECK(hipEventCreateWithFlags(&ev_ready_, hipEventDisableTiming));
-        HIP_CHECK(hipEventCreateWithFlags(&ev_halo_, hipEventDisableTiming));
-        HIP_CHECK(hipEventCreateWithFlags(&ev_int_, hipEventDisableTiming));
-        HIP_CHECK(hipEventCreateWithFlags(&ev_bnd_, hipEventDisableTiming));
+        // Stream-ordering events (never read by the host).  GOL_EVENT_SCOPE=device asks for a
+        // device-scope release instead of the default system-scope fence (measurement knob).
+        const unsigned evf = hipEventDisableTiming |
+                             (env_str("GOL_EVENT_SCOPE", "system") == "device" ? hipEventReleaseToDevice : 0u);
+        HIP_CHECK(hipEventCreateWithFlags(&ev_ready_, evf));
+        HIP_CHECK(hipEventCreateWithFlags(&ev_halo_, evf));
+        HIP_CHECK(hipEventCreateWithFlags(&ev_int_, evf));
+        HIP_CHECK(hipEventCreateWithFlags(&ev_bnd_, evf));
         if (cfg_.profile) {
             for (auto* e : {&ev_t0_, &ev_t1_, &ev_t2_, &ev_t3_}) HIP_CHECK(hipEventCreate(e));
         }
@@ -188,6 +192,7 @@ class HipEngine : public Engine {
         // GPU (a release fence), measured between eager supersteps on one MI355X.
         if (!events_needed_) return;
         HIP_CHECK(hipEventRecord(ev_ready_, s_comp_));
+        if (!edge_mode_) return;  // ev_int_ / ev_bnd_ order the edge-stream schedule only
         HIP_CHECK(hipEventRecord(ev_int_, s_comp_));
         HIP_CHECK(hipEventRecord(ev_bnd_, s_comp_));
     }
@@ -1069,8 +1074,8 @@ class HipEngine : public Engine {
     u64* h_red_ = nullptr;
     bool device_transport_ = false;
     bool graph_ok_ = true;
-    bool events_needed_ = true;
-    std::vector<void*> deferred_free_;  // another stream waits on ev_ready_ / ev_int_ / ev_bnd_
+    bool events_needed_ = true;  // another stream waits on ev_ready_ / ev_int_ / ev_bnd_
+    std::vector<void*> deferred_free_;
     std::map<int, DevPlan> plans_;
     std::map<int, DevCopies> copies_;
     std::map<int, std::vector<HaloItem>> items_;

@@ -57,7 +57,7 @@ class Simulation:
     transport:    a ``_gol.Transport``; defaults to a single-rank transport.  See
                   :mod:`gol_amd.parallel` for torch.distributed / RCCL / thread transports.
     backend:      ``"hip"``, ``"cpu"`` or ``"auto"``.
-    halo_depth:   generations per halo exchange (<= 64; 0 = auto: 8, or 32 for 1-D multi-rank).
+    halo_depth:   generations per halo exchange (<= 64; 0 = auto: 16 on one rank, 32 with neighbours, 64 for 1-D strips of >= 8192 rows).
     kernel_depth: generations per kernel pass (HIP; 0 = auto).  A superstep of halo_depth
                   generations runs as several kernel passes in 1-D (communication-avoiding halos).
     decomp/grid:  ``"1d"`` row strips (reference) or ``"2d"`` blocks, optional ``"PxxPy"`` grid.

@@ -224,6 +224,41 @@ def test_python_threads_device_transport(gol, decomp, grid, P):
     assert np.array_equal(board, numpy_step(initial_board(5, N, 1, True, 9), gens))
 
 
+def test_threads_device_transport_deep_halo_64(gol):
+    """Tall 1-D strips (>= 8192 rows) get the auto halo depth 64: 8 kernel passes per exchange, the
+    first seven also computing ghost rows.  2 thread ranks on one GPU (RCCL-semantics transport),
+    16384^2 board vs the PyTorch conv2d oracle."""
+    import threading
+
+    import torch
+
+    N, P, gens = 16384, 2, 64 * 2 + 13
+    ts = gol.parallel.p2p_thread_transports(P)
+    out, errs = [None] * P, []
+
+    def rank_main(r):
+        try:
+            s = gol.Simulation(N, ts[r], backend="hip", device=0, global_mode=True)
+            s.init(5, seed=5)
+            assert s.stats()["depth"] == 64, s.stats()
+            s.step(gens)
+            out[r] = (s.geometry.row0, s.board())
+        except Exception as e:  # pragma: no cover - reported below
+            errs.append(repr(e))
+
+    th = [threading.Thread(target=rank_main, args=(r,)) for r in range(P)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=300)
+    assert not errs, errs
+    ref = torch_step(random_board(N, N, 5), gens, device="cuda:0").cpu().numpy()
+    for r0, b in out:
+        assert np.array_equal(b, ref[r0 : r0 + b.shape[0]])
+    del ref
+    torch.cuda.empty_cache()
+
+
 @pytest.mark.parametrize("kernel", ["temporal", "tile"])
 def test_known_physics_gpu(gol, kernel):
     """Blinker period 2, block still life, glider back home after 4N generations on an N x N torus,
