@@ -129,6 +129,9 @@ class Engine {
     virtual std::vector<u64> read_row(i64 r) = 0;  // full-pitch row r of the current buffer
     // Largest superstep depth <= want that the backend can run (HIP: instantiated kernel depths).
     virtual int supported_depth(int want) const { return want; }
+    // Generations per full superstep (<= the halo depth R; HIP: a multiple of the tuned pass depth
+    // when the rank has no neighbours, so no superstep ends with a short, slow pass).
+    virtual int superstep_depth() const { return L_.R; }
     void setup_compat();
     void maybe_inject_fault();
     // Watchdog mode: wait until earlier work has completed (bounded lookahead), polling the

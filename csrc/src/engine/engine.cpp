@@ -23,12 +23,13 @@ Engine::Engine(const Geometry& g, const EngineConfig& c, std::shared_ptr<Transpo
     if (t_->size() != g_.dec.P || t_->rank() != g_.rank)
         throw Error(strprintf("transport (rank %d of %d) does not match the geometry (rank %d of %d)", t_->rank(),
                               t_->size(), g_.rank, g_.dec.P));
-    // auto depth: 16 generations per superstep on one rank, 32 with neighbours (64 for 1-D strips
-    // of >= 8192 rows: half the exchanges and cross-stream events per generation for < 0.5% of
-    // ghost-row recompute; measured +1.7% on the eager multi-GPU schedule, docs/PERFORMANCE.md).
+    // auto depth: 32 generations per superstep (the tile-kernel autotune tries passes of up to 32
+    // on one rank), 64 for 1-D strips of >= 8192 rows with neighbours: half the exchanges and
+    // cross-stream events per generation for < 0.5% of ghost-row recompute; measured +1.7% on the
+    // eager multi-GPU schedule, docs/PERFORMANCE.md.
     // The HIP backend runs a superstep as kernel passes of K (auto 8) generations (deep halos).
     const bool tall_strips = g_.dec.Px == 1 && g_.h >= 8192;
-    const int want = cfg_.halo_depth > 0 ? cfg_.halo_depth : (g_.dec.P > 1 ? (tall_strips ? 64 : 32) : 16);
+    const int want = cfg_.halo_depth > 0 ? cfg_.halo_depth : (g_.dec.P > 1 && tall_strips ? 64 : 32);
     int R = clamp_halo_depth(g_.dec, want);
     if (cfg_.compat) {
         if (g_.dec.Px != 1) throw Error("GOL_COMPAT=reference supports 1-D row strips only");

@@ -402,6 +402,7 @@ class HipEngine : public Engine {
             if (cfg_.kernel == "auto") autotune_kernel();
             autotune_schedule();
             tuned_ = true;
+            passes_.clear();  // the pass cuts may depend on the tuned kernel (pass_depths)
         }
         stats_.kernel = split_ ? kern_[1] + "+boundary:" + kern_[2] : kern_[0];
         stats_.schedule = split_ ? "split" : (halo_items(L_.R).empty() ? "local" : "full");
@@ -447,7 +448,8 @@ class HipEngine : public Engine {
         std::vector<int> ps;
         for (int left = k; left > 0;) {
             int d = std::min(left, kdepth_);
-            if (cfg_.kernel != "tile") d = supported_kernel_depth(d);  // every kind may be temporal
+            // every kind may be temporal, unless only the (any-depth) tile kernel runs
+            if (cfg_.kernel != "tile" && !(tuned_ && !split_ && tile_kernel(0))) d = supported_kernel_depth(d);
             ps.push_back(d);
             left -= d;
         }
@@ -711,11 +713,19 @@ class HipEngine : public Engine {
         std::vector<int> nws = {nw0};
         if (cfg_.tune_tile_waves && nw0 != 8) nws.push_back(8);
         std::vector<Cand> cands = {{"temporal", k0, nw0}};
-        const int k2 = supported_kernel_depth(std::min({2 * k0, L_.R, 32}));
-        for (int nw : nws) {
-            cands.push_back({"tile", k0, nw});
-            if (!cfg_.compat && cfg_.kernel_depth == 0 && k2 > k0) cands.push_back({"tile", k2, nw});
+        // Deeper tile passes: 2 k0 always; 3 k0 and 4 k0 (any depth) when the full-tile plan is the
+        // only kind a superstep runs (no split), so the passes need not suit the register kernel.
+        // 8192^2 on one GPU: tile@16 1.51-1.52, tile@24 1.475, tile@32 1.496 us/gen.
+        std::vector<int> kts = {k0};
+        if (!cfg_.compat && cfg_.kernel_depth == 0) {
+            const int kmax = std::min(L_.R, 32);
+            const int k2 = supported_kernel_depth(std::min(2 * k0, kmax));
+            if (k2 > k0) kts.push_back(k2);
+            if (!split_used())
+                for (int m = 3; m <= 4 && m * k0 <= kmax; ++m) kts.push_back(m * k0);
         }
+        for (int nw : nws)
+            for (int k : kts) cands.push_back({"tile", k, nw});
         for (const auto& c : cands) time_pass(0, c.kern, c.k, true);
         spin_up();
         float best = 1e30f;

@@ -172,6 +172,20 @@ def test_auto_kernel_choice(gol, N):
     assert np.array_equal(s.board(), numpy_step(initial_board(5, N, 1, True, N), gens))
 
 
+@pytest.mark.parametrize("N", [1000, 8192])
+def test_auto_single_rank_depth_32(gol, N):
+    """One rank, auto depth (32): the tuner may pick tile passes of 24 or 32 generations (not a
+    register-kernel depth); remainder supersteps and every pass cut stay exact."""
+    gens = 32 * 5 + 8 + 3
+    s = _sim(gol, N, kernel="auto").init(5, seed=N + 1)
+    st = s.stats()
+    assert st["depth"] == 32 and st["kernel"] in ("temporal", "tile"), st
+    if st["kernel"] == "temporal":
+        assert st["kernel_depth"] <= 16, st
+    s.step(gens)
+    assert np.array_equal(s.board(), numpy_step(initial_board(5, N, 1, True, N + 1), gens))
+
+
 @pytest.mark.parametrize("kernel", ["temporal", "tile"])
 @pytest.mark.parametrize("graph", [True, False])
 @pytest.mark.parametrize("edge_cus", [8, 0])
