@@ -36,7 +36,7 @@ def main() -> int:
     ap.add_argument("--scaling", choices=["weak", "strong"], default="weak")
     ap.add_argument("--decomp", default="1d", help="1d | 2d | auto")
     ap.add_argument("--halo-depth", type=int, default=int(os.environ.get("GOL_HALO_DEPTH", "0")),
-                    help="generations per halo exchange (0 = auto: 16 on one GPU, 32-64 multi-GPU)")
+                    help="generations per halo exchange (0 = auto: 32; 64 for tall multi-GPU strips)")
     ap.add_argument("--kernel-depth", type=int, default=int(os.environ.get("GOL_KERNEL_DEPTH", "0")),
                     help="generations per kernel pass (0 = auto)")
     ap.add_argument("--kernel", default=os.environ.get("GOL_KERNEL", "auto"),
