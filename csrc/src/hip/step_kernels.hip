@@ -66,7 +66,13 @@ __device__ __forceinline__ u32 rule32(u32 a0, u32 a1, u32 b0, u32 b1, u32 c0, u3
 // odd cell j (hi).  Odd cell j: left = even cell j (lo), right = even cell j+1 (lo shifted down one,
 // bit 31 from the next lane's lo).  2 DPP + 2 funnel shifts + 4 bitop3 per 64 cells.
 __device__ __forceinline__ void hsum_split(u32 lo, u32 hi, u32& s0lo, u32& s1lo, u32& s0hi, u32& s1hi) {
+#ifdef GOL_HSUM_BPERM
+    const int lane = (int)__lane_id();
+    const u32 ph = (u32)__builtin_amdgcn_ds_bpermute(((lane - 1) & 63) << 2, (int)hi);
+    const u32 nl = (u32)__builtin_amdgcn_ds_bpermute(((lane + 1) & 63) << 2, (int)lo);
+#else
     const u32 ph = dpp_prev(hi), nl = dpp_next(lo);
+#endif
     const u32 Le = __builtin_amdgcn_alignbit(hi, ph, 31);  // (hi << 1) | (ph >> 31)
     const u32 Ro = __builtin_amdgcn_alignbit(nl, lo, 1);   // (lo >> 1) | (nl << 31)
     s0lo = b3<kLutXor3>(Le, lo, hi);
