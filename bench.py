@@ -166,8 +166,17 @@ def main() -> int:
             out["speedup_vs_yardstick"] = value / (yard["cell_updates_per_s"] * P)
         print(json.dumps(out), flush=True)
     if P > 1:
+        import gc
+
         import torch.distributed as dist
 
+        # Tear the engine and its RCCL communicator down on every rank while all peers are still
+        # alive (not at interpreter exit, where a rank could outlive its neighbours).
+        sim.synchronize()
+        del sim, transport
+        if backend == "hip":
+            del rccl
+        gc.collect()
         dist.barrier(group=cpu_group)  # gloo: also fine when ranks share a GPU (rehearsal runs)
         dist.destroy_process_group()
     return 0
