@@ -1,7 +1,14 @@
+#!/bin/bash
+# Generic A/B of two kbench builds, alternating on one box: tools/kb_ab.sh <a> <b> [rounds]
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
-for v in old new old new; do
-  timeout -k 5 60 build/kbench_$v 32768 8 960 >> gpurun_out/kb.txt 2>&1 || exit 3
-  timeout -k 5 60 build/kbench_$v 8192 16 1920 0 0 8 0 2 >> gpurun_out/kb.txt 2>&1 || exit 3
+out=gpurun_out/kb_ab_$1_$2.txt; : > $out
+for r in $(seq ${3:-3}); do
+  for v in $1 $2; do
+    echo "== $v" >> $out
+    timeout -k 5 60 build/kbench_$v 32768 8 1920 >> $out 2>&1 || exit 3
+    timeout -k 5 60 build/kbench_$v 16384 8 1920 >> $out 2>&1 || exit 3
+    timeout -k 5 60 build/kbench_$v 65536 8 480 >> $out 2>&1 || exit 3
+  done
 done
-cat gpurun_out/kb.txt
+cat $out
