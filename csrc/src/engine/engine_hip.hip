@@ -696,7 +696,8 @@ class HipEngine : public Engine {
             float ms = 0;
             HIP_CHECK(hipEventElapsedTime(&ms, e0, e1));
             const float per_gen = ms / 3 / (float)k;
-            tune_ms_[tile ? strprintf("%d:%s@%dx%dw", kind, kern, k, cfg_.tile_waves) : strprintf("%d:%s@%d", kind, kern, k)] =
+            tune_ms_[tile ? strprintf("%d:%s@%dx%dw", kind, kern, k, cfg_.tile_waves)
+                          : (occ_ ? strprintf("%d:%s@%d/%dw", kind, kern, k, occ_) : strprintf("%d:%s@%d", kind, kern, k))] =
                 per_gen;
             return per_gen;
         };
@@ -707,12 +708,17 @@ class HipEngine : public Engine {
         struct Cand {
             const char* kern;
             int k, nw;
+            int occ = 0;  // temporal: waves per SIMD of the plan (0 = full occupancy)
         };
         const int k0 = cfg_.compat ? 1 : kdepth_;
         const int nw0 = cfg_.tile_waves;
         std::vector<int> nws = {nw0};
         if (cfg_.tune_tile_waves && nw0 != 8) nws.push_back(8);
         std::vector<Cand> cands = {{"temporal", k0, nw0}};
+        // fewer, taller temporal waves (2 per SIMD instead of 3) for small tiles: less vertical halo
+        if (!cfg_.compat && cfg_.rows_per_wave <= 0 && cfg_.waves_target <= 0 &&
+            hipk::step_blocks_per_cu(k0, step_flags()) > 2)
+            cands.push_back({"temporal", k0, nw0, 2});
         // Deeper tile passes: 2 k0 always; 3 k0 and 4 k0 (any depth) when the full-tile plan is the
         // only kind a superstep runs (no split), so the passes need not suit the register kernel.
         // 8192^2 on one GPU: tile@16 1.51-1.52, tile@24 1.475, tile@32 1.496 us/gen.
@@ -726,12 +732,16 @@ class HipEngine : public Engine {
         }
         for (int nw : nws)
             for (int k : kts) cands.push_back({"tile", k, nw});
-        for (const auto& c : cands) time_pass(0, c.kern, c.k, true);
+        for (const auto& c : cands) {
+            occ_ = c.occ;
+            time_pass(0, c.kern, c.k, true);
+        }
         spin_up();
         float best = 1e30f;
         Cand pick = cands[0];
         for (const auto& c : cands) {
             cfg_.tile_waves = c.nw;
+            occ_ = c.occ;
             const float t = time_pass(0, c.kern, c.k);
             if (t < best) {
                 best = t;
@@ -741,6 +751,7 @@ class HipEngine : public Engine {
         kern_[0] = pick.kern;
         kdepth_ = pick.k;
         cfg_.tile_waves = pick.nw;
+        occ_ = pick.occ;
         passes_.clear();
         // interior / boundary plans of split supersteps, at the chosen pass depth
         if (split_used()) {
@@ -800,7 +811,7 @@ class HipEngine : public Engine {
     }
 
     const DevPlan& plan(int kind, int k, i64 e = 0) {
-        const int key = (tile_kernel(kind) ? 1000000 : 0) + kind * 100000 + (int)e * 100 + k;
+        const int key = occ_ * 10000000 + (tile_kernel(kind) ? 1000000 : 0) + kind * 100000 + (int)e * 100 + k;
         auto it = plans_.find(key);
         if (it != plans_.end()) return it->second;
         std::vector<Region> rg = regions(kind, k, e);
@@ -828,7 +839,9 @@ class HipEngine : public Engine {
                 rows = choose_rows_per_chunk(rg, k, cfg_.waves_target, 4 * (i64)k);
             if (rows <= 0) {
                 // one full round of resident waves (occupancy of this kernel instantiation)
-                const i64 resident = (i64)hipk::step_blocks_per_cu(k, step_flags()) * kWavesPerBlock * plan_cus(kind);
+                i64 bpc = hipk::step_blocks_per_cu(k, step_flags());
+                if (occ_ > 0) bpc = std::min<i64>(bpc, occ_);  // 256-thread blocks per CU = waves per SIMD
+                const i64 resident = bpc * kWavesPerBlock * plan_cus(kind);
                 rows = balanced_rows_per_chunk(rg, L_.nw, L_.h, k, resident, 2 * (i64)k, xwrap_by_plan());
             }
         }
@@ -1063,6 +1076,10 @@ class HipEngine : public Engine {
     std::string kernel_;  // resolved kernel: temporal | tile | lds (auto resolves at init)
     std::string kern_[3];  // per plan kind (full / interior / boundary), resolved by autotune
     int kdepth_ = 8;       // kernel pass depth K (<= halo depth R)
+    // temporal-kernel plans: waves per SIMD the one-round plan is sized for (0: the kernel's full
+    // occupancy).  Small tiles pay (K+1)/S of vertical halo with S rows per wave, so fewer, taller
+    // waves can win there; the autotuner tries 2 per SIMD against the full occupancy (3 at K=8).
+    int occ_ = 0;
     bool tile_l2_ = env_int("GOL_TILE_LEVELS", 2) == 2;  // tile kernel: generations per LDS pass
     bool multipass_ = false;
     std::map<int, std::vector<int>> passes_;
