@@ -166,7 +166,7 @@ void Engine::run(u64 generations) {
     Armed armed(wd_.get());
     while (generations > 0) {
         maybe_inject_fault();
-        int k = cfg_.compat ? 1 : supported_depth((int)std::min<u64>((u64)L_.R, generations));
+        int k = cfg_.compat ? 1 : supported_depth((int)std::min<u64>((u64)superstep_depth(), generations));
         {
             trace::Range r("gol.superstep");
             do_superstep(k);

@@ -292,7 +292,7 @@ class HipEngine : public Engine {
     // Graph shape of run(): m supersteps of k generations per replay; false when run() stays eager.
     bool graph_shape(int& k, int& m) {
         if (!cfg_.graph || cfg_.profile) return false;
-        k = cfg_.compat ? 1 : L_.R;
+        k = cfg_.compat ? 1 : superstep_depth();
         m = cfg_.graph_supersteps;
         if (m <= 0) m = k >= 8 ? 16 : 32;
         m += m & 1;  // even: the graph returns to the same buffer parity
@@ -369,7 +369,19 @@ class HipEngine : public Engine {
         Engine::run(generations);
     }
 
-    const DevPlan& full_plan_stats() { return plan(0, pass_depths(L_.R)[0], ext_after(pass_depths(L_.R), 0)); }
+    const DevPlan& full_plan_stats() {
+        const int R = superstep_depth();
+        return plan(0, pass_depths(R)[0], ext_after(pass_depths(R), 0));
+    }
+
+    // A rank without neighbours (nothing to exchange) cuts its supersteps at the largest multiple
+    // of the tuned pass depth within R, so none ends with a short pass (8192^2: tile passes of 24
+    // in 32-generation supersteps ran 24 + 8, and an 8-generation tile pass is 27% slower per
+    // generation).  With neighbours every rank keeps R: the exchanges must match.
+    int superstep_depth() const override {
+        if (!tuned_ || cfg_.compat || kdepth_ <= 0 || kdepth_ >= L_.R || !halo_items(L_.R).empty()) return L_.R;
+        return (L_.R / kdepth_) * kdepth_;
+    }
 
    protected:
     void do_init(const PatternSpec& p) override {
