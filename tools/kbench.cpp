@@ -6,6 +6,7 @@
 //   build/kbench_<variant> [N=32768] [K=8] [gens=960] [pf=0|1]
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -57,7 +58,9 @@ int main(int argc, char** argv) {
             if (r <= rmax) rows = r;
         }
     } else if (rows <= 0) {
-        const i64 resident = (i64)hipk::step_blocks_per_cu(K, flags) * kWavesPerBlock * prop.multiProcessorCount;
+        i64 bpc = hipk::step_blocks_per_cu(K, flags);
+        if (getenv("KB_BPC")) bpc = std::min<i64>(bpc, atoi(getenv("KB_BPC")));  // waves per SIMD of the plan
+        const i64 resident = bpc * kWavesPerBlock * prop.multiProcessorCount;
         rows = balanced_rows_per_chunk(rg, L.nw, N, K, resident, 2 * K, true);
     }
     PlanStats st;
