@@ -1,4 +1,5 @@
 cd $GRAFT_REPO_ROOT
+# Config-2 sweep of bench.py at 8192^2: kernel:halo-depth:kernel-depth specs (auto vs fixed tile depths).
 mkdir -p gpurun_out/cfg2
 for spec in "auto:16:0" "tile:16:16" "tile:32:32" "tile:32:16" "tile:24:24"; do
   IFS=: read kern R K <<< "$spec"
