@@ -1,5 +1,6 @@
-cd $GRAFT_REPO_ROOT
+#!/bin/bash
 # Config-2 sweep of bench.py at 8192^2: kernel:halo-depth:kernel-depth specs (auto vs fixed tile depths).
+cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out/cfg2
 for spec in "auto:16:0" "tile:16:16" "tile:32:32" "tile:32:16" "tile:24:24"; do
   IFS=: read kern R K <<< "$spec"

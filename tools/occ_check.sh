@@ -1,6 +1,7 @@
-cd $GRAFT_REPO_ROOT
+#!/bin/bash
 # bench.py at 8192^2 / 16384^2 / 32768^2 (autotune strings show the 3- vs 2-waves/SIMD temporal plans) and the
 # one-GPU multi-rank rehearsal at strong-scaling tile sizes.
+cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out/occ
 for n in 8192 16384 32768; do
   timeout -k 10 120 python bench.py --size $n --steps 2000 --warmup 200 > gpurun_out/occ/b$n.log 2>&1 || exit 3
