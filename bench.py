@@ -94,6 +94,7 @@ def main() -> int:
         overlap=not args.no_overlap,
         kernel=args.kernel,
         device=local if backend == "hip" else None,
+        run_hint=steps,  # the timed run replays one captured graph (graph boundaries idle the GPU)
     )
     sim.init(pattern=5, seed=args.seed)
     dec = sim.decomposition

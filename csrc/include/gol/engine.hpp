@@ -50,6 +50,8 @@ struct EngineConfig {
     std::string transport = "auto";   // auto | device | host  (host = stage halos through host memory)
     bool profile = false;             // per-phase event timing
     int graph_supersteps = 0;         // supersteps per captured graph (0 = auto, even)
+    u64 run_hint = 0;                 // generations of the runs to come (CLI: iterations); the HIP
+                                      // engine captures one graph covering them (<= 256 supersteps)
     bool graph_rccl = false;          // also capture supersteps whose exchange is an RCCL group
     double watchdog_s = 0;            // abort the job after this long without progress (0 = off)
     int edge_cus = 0;                 // >0: CU-partitioned edge-stream schedule (experimental, opt-in)

@@ -356,6 +356,7 @@ int run_rank(const CliArgs& a, const Options& o, const LaunchInfo& li, std::shar
         std::shared_ptr<Transport> t = make_data_transport(control, backend, o, device);
         EngineConfig ec = engine_config(o, backend, device);
         apply_threads_hint(ec, a.threads, rank == 0);
+        ec.run_hint = o.checkpoint_every > 0 ? (u64)o.checkpoint_every : (u64)a.iterations;
         std::unique_ptr<Engine> eng = Engine::create(g, ec, t);
         if (o.verbose && rank == 0) fprintf(stderr, "[gol] %s\n", eng->describe().c_str());
         eng->init(pat);

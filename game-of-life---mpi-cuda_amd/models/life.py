@@ -91,6 +91,7 @@ class Simulation:
         edge_cus: int = int(os.environ.get("GOL_EDGE_CUS", "0")),
         force_split: bool = os.environ.get("GOL_FORCE_SPLIT", "0") == "1",
         schedule: str = os.environ.get("GOL_SCHEDULE", "auto"),
+        run_hint: int = 0,
     ):
         self.transport = transport if transport is not None else _gol.SelfTransport()
         P, rank = self.transport.size(), self.transport.rank()
@@ -107,6 +108,7 @@ class Simulation:
         cfg.kernel = kernel
         cfg.prefetch = prefetch
         cfg.pipeline = pipeline
+        cfg.run_hint = int(run_hint)  # generations of the runs to come: one replay graph covers them
         cfg.rows_per_wave = rows_per_wave
         cfg.waves_target = waves_target
         cfg.profile = profile

@@ -60,6 +60,21 @@ def test_graph_replay(gol, graph):
     assert np.array_equal(s.board(), numpy_step(initial_board(5, N, 1, True, 11), gens))
 
 
+def test_run_hint_single_graph(gol):
+    """run_hint: one replay graph covers the whole expected run (37 supersteps here), other run
+    lengths still use the 16/4/1 ladder; both parities stay exact."""
+    N, R = 512, 8
+    hint = R * 37 + 5
+    s = _sim(gol, N, halo_depth=R, kernel_depth=R, kernel="temporal", run_hint=hint).init(5, seed=13)
+    g0 = s.stats()["graph_launches"]
+    s.step(hint)
+    assert s.stats()["graph_launches"] - g0 == 1, s.stats()
+    s.step(R * 21 + 3)
+    s.step(hint)
+    total = 2 * hint + R * 21 + 3
+    assert np.array_equal(s.board(), numpy_step(initial_board(5, N, 1, True, 13), total))
+
+
 @pytest.mark.parametrize("R,K", [(16, 8), (8, 8), (24, 8)])
 def test_graph_replay_after_parity_flip(gol, R, K):
     """Replays are keyed by buffer parity and track it: graphs of 16, 4 and 1 supersteps (1 or 3
