@@ -428,6 +428,15 @@ class HipEngine : public Engine {
             autotune_schedule();
             tuned_ = true;
             passes_.clear();  // the pass cuts may depend on the tuned kernel (pass_depths)
+            // keep the collective choice for later init() calls (split_ is recomputed above)
+            if (cfg_.sched == "auto" && split_used()) cfg_.sched = split_ ? "split" : "full";
+            // The comm stream waits on the compute stream's ready event only in the split
+            // schedule (and the edge-stream / forced-split measurement modes).  The full schedule
+            // exchanges on the compute stream itself: recording the event there every superstep
+            // only idles the GPU (~15 us per record, a release fence).  GOL_READY_EVENTS=always
+            // restores the record (measurement knob).
+            events_needed_ = edge_mode_ || cfg_.force_split || (split_ && !halo_items(L_.R).empty()) ||
+                             env_str("GOL_READY_EVENTS", "") == "always";
         }
         stats_.kernel = split_ ? kern_[1] + "+boundary:" + kern_[2] : kern_[0];
         stats_.schedule = split_ ? "split" : (halo_items(L_.R).empty() ? "local" : "full");
