@@ -29,6 +29,10 @@
 
 namespace gol {
 
+// Tile rows from which GOL_SUBTILES=auto uses two sub-tiles (measured: 32768^2 +3-5% per generation,
+// 65536^2 equal, 16384^2 -3%; docs/PERFORMANCE.md).
+constexpr i64 kSubtileMinRows = 24576;
+
 struct EngineConfig {
     std::string backend = "cpu";      // cpu | hip
     int halo_depth = 0;               // R: generations per halo exchange (0 = auto: 8 on one rank,
@@ -50,6 +54,8 @@ struct EngineConfig {
     std::string transport = "auto";   // auto | device | host  (host = stage halos through host memory)
     bool profile = false;             // per-phase event timing
     int graph_supersteps = 0;         // supersteps per captured graph (0 = auto, even)
+    int subtiles = -1;                // HIP, 1-D: two sub-tiles per rank on two streams (GOL_SUBTILES:
+                                      // 2 on, 0 off, -1 auto = on for tiles of >= kSubtileMinRows rows)
     u64 run_hint = 0;                 // generations of the runs to come (CLI: iterations); the HIP
                                       // engine captures one graph covering them (<= 256 supersteps)
     bool graph_rccl = false;          // also capture supersteps whose exchange is an RCCL group

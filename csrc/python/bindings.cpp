@@ -251,6 +251,7 @@ PYBIND11_MODULE(_gol, m) {
         .def_readwrite("profile", &EngineConfig::profile)
         .def_readwrite("graph_supersteps", &EngineConfig::graph_supersteps)
         .def_readwrite("run_hint", &EngineConfig::run_hint)
+        .def_readwrite("subtiles", &EngineConfig::subtiles)
         .def_readwrite("watchdog_s", &EngineConfig::watchdog_s)
         .def_readwrite("tile_waves", &EngineConfig::tile_waves)
         .def_readwrite("tune_tile_waves", &EngineConfig::tune_tile_waves)

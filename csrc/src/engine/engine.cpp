@@ -29,7 +29,10 @@ Engine::Engine(const Geometry& g, const EngineConfig& c, std::shared_ptr<Transpo
     // eager multi-GPU schedule, docs/PERFORMANCE.md.
     // The HIP backend runs a superstep as kernel passes of K (auto 8) generations (deep halos).
     const bool tall_strips = g_.dec.Px == 1 && g_.h >= 8192;
-    const int want = cfg_.halo_depth > 0 ? cfg_.halo_depth : (g_.dec.P > 1 && tall_strips ? 64 : 32);
+    // ... and 64 for the two-sub-tile mode (HIP, GOL_SUBTILES auto or 2, tiles of >= 24576 rows): it
+    // synchronises its two streams once per superstep, so longer supersteps keep more of the overlap
+    const bool sub_tall = cfg_.backend == "hip" && cfg_.subtiles != 0 && g_.dec.Px == 1 && g_.h >= kSubtileMinRows;
+    const int want = cfg_.halo_depth > 0 ? cfg_.halo_depth : ((g_.dec.P > 1 && tall_strips) || sub_tall ? 64 : 32);
     int R = clamp_halo_depth(g_.dec, want);
     if (cfg_.compat) {
         if (g_.dec.Px != 1) throw Error("GOL_COMPAT=reference supports 1-D row strips only");

@@ -201,6 +201,13 @@ class HipEngine : public Engine {
     ~HipEngine() override {
         hipStreamSynchronize(s_comp_);
         hipStreamSynchronize(s_comm_);
+        for (auto& kv : sub_plans_) hipFree(kv.second.d);
+        for (auto& kv : dual_copies_) hipFree(kv.second.d);
+        for (auto& sb : sub_buf_)
+            for (u64* b : sb)
+                if (b) hipFree(b);
+        if (ev_sub_a_) hipEventDestroy(ev_sub_a_);
+        if (ev_sub_b_) hipEventDestroy(ev_sub_b_);
         for (auto& kv : graphs_) hipGraphExecDestroy(kv.second);
         for (auto& kv : plans_) hipFree(kv.second.d);
         for (auto& kv : copies_) {
@@ -378,8 +385,172 @@ class HipEngine : public Engine {
 
     void run(u64 generations) override {
         Armed armed(wd_.get());
+        if (dual_) {
+            run_dual(generations);
+            return;
+        }
         run_graphed(generations);
         Engine::run(generations);
+    }
+
+    // ----- two sub-tiles per rank (GOL_SUBTILES=2, 1-D) -----
+    // The tile's rows are split into two halves with their own double buffers and R ghost rows.
+    // Per superstep the halves exchange R edge rows by device copies (and the rank's north / south
+    // halos go to sub-tile 0 / 1 through the transport, in the same canonical messages as the
+    // one-tile engine), then each half runs the superstep's passes on its own stream, planned for
+    // the whole GPU.  The two kernels of a pass overlap: while one drains, the other's waves fill
+    // the freed SIMD slots (two half-board kernels on two streams: 9.8 vs 11.0 us/gen at 32768^2,
+    // docs/PERFORMANCE.md).  The canonical buffers are copied in at run() entry and back at exit.
+    bool dual_eligible() const {
+        const bool want = cfg_.subtiles == 2 || (cfg_.subtiles < 0 && L_.h >= kSubtileMinRows && L_.R >= 64);
+        if (!want || g_.dec.Px != 1 || cfg_.compat || cfg_.profile || edge_mode_ || split_ || wd_ ||
+            kern_[0] != "temporal" || !L_.aligned() || L_.h < 8 * (i64)L_.R)
+            return false;
+        if (!self_y() && !device_transport_) return false;
+        size_t fr = 0, tot = 0;
+        if (hipMemGetInfo(&fr, &tot) != hipSuccess) return false;
+        return 2 * alloc_bytes_ + ((size_t)1 << 30) < fr;  // sub-tile buffers ~ one more board pair
+    }
+
+    void setup_dual() {
+        const i64 h0 = L_.h / 2;
+        sub_r0_[0] = 0;
+        sub_r0_[1] = h0;
+        for (int s = 0; s < 2; ++s) {
+            const i64 hs = s == 0 ? h0 : L_.h - h0;
+            sub_L_[s] = Layout(hs, L_.w, L_.R);
+            const size_t bytes = (size_t)(sub_L_[s].words() + hipk::kSlackRows * sub_L_[s].pitch) * 8;
+            for (int i = 0; i < 2; ++i) {
+                HIP_CHECK(hipMalloc(&sub_buf_[s][i], bytes));
+                HIP_CHECK(hipMemsetAsync(sub_buf_[s][i], 0, bytes, s_comp_));
+            }
+        }
+        HIP_CHECK(hipEventCreateWithFlags(&ev_sub_a_, hipEventDisableTiming));
+        HIP_CHECK(hipEventCreateWithFlags(&ev_sub_b_, hipEventDisableTiming));
+        HIP_CHECK(hipStreamSynchronize(s_comp_));
+        for (int k = 1; k <= L_.R; ++k)
+            if (supported_depth(k) == k) {
+                const std::vector<int>& ps = pass_depths(k);
+                for (size_t j = 0; j < ps.size(); ++j)
+                    for (int s = 0; s < 2; ++s) sub_plan(s, ps[j], ext_after(ps, j));
+                for (int par = 0; par < 2; ++par) dual_copies(k, par);
+            }
+        dual_ = true;
+    }
+
+    const DevPlan& sub_plan(int s, int k, i64 e) {
+        const int key = (s * 100000 + (int)e * 100 + k);
+        auto it = sub_plans_.find(key);
+        if (it != sub_plans_.end()) return it->second;
+        const Layout& L = sub_L_[s];
+        std::vector<Region> rg = {{-e, L.h + e, 0, L.nw}};
+        i64 bpc = hipk::step_blocks_per_cu(k, sub_flags());
+        if (occ_ > 0) bpc = std::min<i64>(bpc, occ_);
+        const i64 rows = balanced_rows_per_chunk(rg, L.nw, L.h, k, bpc * kWavesPerBlock * cus_, 2 * (i64)k, true);
+        DevPlan p;
+        std::vector<LaneDesc> lanes = build_plan(rg, L.nw, L.h, rows, k, true, &p.st, kWavesPerBlock, cfg_.plan_xcds);
+        const std::string bad = validate_plan(lanes, L.nw, L.h, L.R, k, false);
+        if (!bad.empty()) throw Error(strprintf("refusing to launch an unsafe sub-tile plan: %s", bad.c_str()));
+        p.waves = (i64)lanes.size() / kWaveLanes;
+        p.rows = rows;
+        HIP_CHECK(hipMalloc(&p.d, lanes.size() * sizeof(LaneDesc)));
+        upload(p.d, lanes.data(), lanes.size() * sizeof(LaneDesc));
+        return sub_plans_.emplace(key, p).first->second;
+    }
+
+    u32 sub_flags() const { return step_flags() & ~hipk::STEP_WRAP_Y; }  // sub-tiles always have ghost rows
+
+    // rows [r0, r0 + n) of sub-tile s at parity par (full pitch, contiguous)
+    u64* sub_rows(int s, int par, i64 r0) { return sub_buf_[s][par] + sub_L_[s].index(r0, -1); }
+    size_t rows_bytes(int s, i64 n) const { return (size_t)(n * sub_L_[s].pitch) * 8; }
+
+    void dual_copy(u64* dst, const u64* src, size_t bytes) {
+        HIP_CHECK(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, s_comp_));
+    }
+
+    void run_dual(u64 generations) {
+        // canonical board -> sub-tiles (interior rows)
+        for (int s = 0; s < 2; ++s)
+            dual_copy(sub_rows(s, sub_cur_, 0), buf_[cur_] + L_.index(sub_r0_[s], -1), rows_bytes(s, sub_L_[s].h));
+        while (generations > 0) {
+            maybe_inject_fault();
+            const int k = supported_depth((int)std::min<u64>((u64)L_.R, generations));
+            dual_superstep(k);
+            gen_ += (u64)k;
+            generations -= (u64)k;
+            stats_.generations += (u64)k;
+            stats_.supersteps += 1;
+            progress("superstep");
+        }
+        // both halves done -> back into the canonical buffer
+        HIP_CHECK(hipEventRecord(ev_sub_b_, s_comm_));
+        HIP_CHECK(hipStreamWaitEvent(s_comp_, ev_sub_b_, 0));
+        for (int s = 0; s < 2; ++s)
+            dual_copy(buf_[cur_] + L_.index(sub_r0_[s], -1), sub_rows(s, sub_cur_, 0), rows_bytes(s, sub_L_[s].h));
+        maybe_inject_fault();
+    }
+
+    struct DualCopies {
+        hipk::CopyDesc* d = nullptr;
+        int n = 0;
+        i64 max = 0;
+    };
+    const DualCopies& dual_copies(int k, int p) {
+        const int key = k * 2 + p;
+        auto it = dual_copies_.find(key);
+        if (it != dual_copies_.end()) return it->second;
+        const i64 h0 = sub_L_[0].h, h1 = sub_L_[1].h, P = sub_L_[0].pitch;
+        std::vector<hipk::CopyDesc> v = {{sub_rows(0, p, h0 - k), sub_rows(1, p, -k), P, P, k, (i32)P},
+                                         {sub_rows(1, p, 0), sub_rows(0, p, h0), P, P, k, (i32)P}};
+        if (self_y()) {
+            v.push_back({sub_rows(1, p, h1 - k), sub_rows(0, p, -k), P, P, k, (i32)P});
+            v.push_back({sub_rows(0, p, 0), sub_rows(1, p, h1), P, P, k, (i32)P});
+        }
+        DualCopies dc;
+        dc.n = (int)v.size();
+        dc.max = (i64)k * P;
+        HIP_CHECK(hipMalloc(&dc.d, v.size() * sizeof(hipk::CopyDesc)));
+        upload(dc.d, v.data(), v.size() * sizeof(hipk::CopyDesc));
+        return dual_copies_.emplace(key, dc).first->second;
+    }
+
+    void dual_superstep(int k) {
+        const int p = sub_cur_;
+        const i64 h0 = sub_L_[0].h, h1 = sub_L_[1].h;
+        // sub-tile 1's previous superstep must be done before its edge rows are read / its ghost
+        // rows are overwritten (the halo work runs on the compute stream)
+        HIP_CHECK(hipEventRecord(ev_sub_b_, s_comm_));
+        HIP_CHECK(hipStreamWaitEvent(s_comp_, ev_sub_b_, 0));
+        // internal seam (sub0 bottom edge -> sub1 top ghost, sub1 top edge -> sub0 bottom ghost) and,
+        // when the rank is its own N/S neighbour, the torus wrap: one batched copy kernel
+        const DualCopies& dc = dual_copies(k, p);
+        hipk::launch_copy_regions(dc.d, dc.n, dc.max, s_comp_);
+        if (!self_y()) {
+            // the one-tile engine's canonical messages (Engine::halo_items, 1-D): N then S
+            std::vector<Message> sends, recvs;
+            sends.push_back({g_.nbr[DIR_N], sub_rows(0, p, 0), rows_bytes(0, k)});
+            recvs.push_back({g_.nbr[DIR_S], sub_rows(1, p, h1), rows_bytes(1, k)});
+            sends.push_back({g_.nbr[DIR_S], sub_rows(1, p, h1 - k), rows_bytes(1, k)});
+            recvs.push_back({g_.nbr[DIR_N], sub_rows(0, p, -k), rows_bytes(0, k)});
+            t_->exchange(sends, recvs, (void*)s_comp_);
+            stats_.exchanges += 1;
+            stats_.halo_bytes += (u64)(rows_bytes(0, k) + rows_bytes(1, k));
+        }
+        HIP_CHECK(hipEventRecord(ev_sub_a_, s_comp_));
+        HIP_CHECK(hipStreamWaitEvent(s_comm_, ev_sub_a_, 0));
+        const std::vector<int>& ps = pass_depths(k);
+        int q = p;
+        for (size_t j = 0; j < ps.size(); ++j) {
+            const i64 e = ext_after(ps, j);
+            for (int s = 0; s < 2; ++s) {
+                const DevPlan& pl = sub_plan(s, ps[j], e);
+                hipk::StepParams sp{sub_L_[s].pitch, (i32)sub_L_[s].h, (i32)sub_L_[s].nw, sub_L_[s].R, sub_flags()};
+                hipk::launch_step(ps[j], sub_buf_[s][q], sub_buf_[s][q ^ 1], pl.d, pl.waves, sp, s ? s_comm_ : s_comp_);
+            }
+            q ^= 1;
+        }
+        HIP_CHECK(hipGetLastError());
+        sub_cur_ = q;
     }
 
     const DevPlan& full_plan_stats() {
@@ -451,7 +622,9 @@ class HipEngine : public Engine {
         // neither graph capture nor a timed loop ever builds or uploads a plan.
         for (int k = 1; k <= (cfg_.compat ? 1 : L_.R); ++k)
             if (supported_depth(k) == k) prepare(k);
-        prewarm_graph();
+        if (!dual_ && dual_eligible()) setup_dual();
+        if (dual_) stats_.schedule += "+subtiles2";
+        if (!dual_) prewarm_graph();
         spin_up();  // init ends with the GPU at its steady clock (plan building and captures idle it)
         const DevPlan& fp = full_plan_stats();
         stats_.plan_waves = fp.waves;
@@ -1145,6 +1318,15 @@ class HipEngine : public Engine {
     bool events_needed_ = true;  // another stream waits on ev_ready_ / ev_int_ / ev_bnd_
     std::vector<void*> deferred_free_;
     std::map<int, DevPlan> plans_;
+    // GOL_SUBTILES=2 state
+    bool dual_ = false;
+    Layout sub_L_[2];
+    i64 sub_r0_[2] = {0, 0};
+    u64* sub_buf_[2][2] = {{nullptr, nullptr}, {nullptr, nullptr}};
+    int sub_cur_ = 0;
+    std::map<int, DevPlan> sub_plans_;
+    std::map<int, DualCopies> dual_copies_;
+    hipEvent_t ev_sub_a_ = nullptr, ev_sub_b_ = nullptr;
     std::map<int, DevCopies> copies_;
     std::map<int, std::vector<HaloItem>> items_;
     std::map<int, hipGraphExec_t> graphs_;

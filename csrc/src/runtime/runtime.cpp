@@ -173,6 +173,7 @@ EngineConfig engine_config(const Options& o, const std::string& backend, int dev
     c.transport = (o.transport == "rccl" || o.transport == "p2p") ? "device" : o.transport;
     c.profile = o.profile;
     c.graph_supersteps = (int)env_int("GOL_GRAPH_SUPERSTEPS", 0);
+    c.subtiles = env_str("GOL_SUBTILES", "auto") == "auto" ? -1 : (int)env_int("GOL_SUBTILES", 0);
     c.watchdog_s = o.watchdog_s;
     c.edge_cus = (int)env_int("GOL_EDGE_CUS", 0);
     c.force_split = env_int("GOL_FORCE_SPLIT", 0) != 0;

@@ -92,6 +92,7 @@ class Simulation:
         force_split: bool = os.environ.get("GOL_FORCE_SPLIT", "0") == "1",
         schedule: str = os.environ.get("GOL_SCHEDULE", "auto"),
         run_hint: int = 0,
+        subtiles: int = -1 if os.environ.get("GOL_SUBTILES", "auto") == "auto" else int(os.environ["GOL_SUBTILES"]),
     ):
         self.transport = transport if transport is not None else _gol.SelfTransport()
         P, rank = self.transport.size(), self.transport.rank()
@@ -108,6 +109,7 @@ class Simulation:
         cfg.kernel = kernel
         cfg.prefetch = prefetch
         cfg.pipeline = pipeline
+        cfg.subtiles = int(subtiles)  # 2 / 0 / -1 auto: two sub-tiles per rank on two streams (HIP, 1-D)
         cfg.run_hint = int(run_hint)  # generations of the runs to come: one replay graph covers them
         cfg.rows_per_wave = rows_per_wave
         cfg.waves_target = waves_target

@@ -60,6 +60,51 @@ def test_graph_replay(gol, graph):
     assert np.array_equal(s.board(), numpy_step(initial_board(5, N, 1, True, 11), gens))
 
 
+@pytest.mark.parametrize("N,R", [(640, 8), (1024, 16), (4096, 32)])
+def test_subtiles_single_rank(gol, N, R):
+    """GOL_SUBTILES=2: two half-tiles on two streams with seam copies and the torus wrap between
+    them; remainder supersteps and repeated run() calls (copy in / copy back) stay exact."""
+    s = _sim(gol, N, halo_depth=R, kernel="temporal", subtiles=2).init(5, seed=N + R)
+    assert "subtiles2" in s.stats()["schedule"], s.stats()
+    total = 0
+    for gens in (R * 5 + 3, 7, R * 2):
+        s.step(gens)
+        total += gens
+    assert np.array_equal(s.board(), numpy_step(initial_board(5, N, 1, True, N + R), total))
+
+
+@pytest.mark.parametrize("P", [2, 3])
+def test_subtiles_thread_ranks(gol, P):
+    """Sub-tiles with neighbours: each rank's north / south halos go to its two halves through the
+    RCCL-semantics transport (thread ranks sharing one GPU)."""
+    import threading
+
+    N, gens = 512, 16 * 4 + 5
+    ts = gol.parallel.p2p_thread_transports(P)
+    out, errs = [None] * P, []
+
+    def rank_main(r):
+        try:
+            s = gol.Simulation(N, ts[r], backend="hip", device=0, global_mode=True, halo_depth=16,
+                               kernel="temporal", subtiles=2)
+            s.init(5, seed=17)
+            assert "subtiles2" in s.stats()["schedule"], s.stats()
+            s.step(gens)
+            out[r] = (s.geometry.row0, s.board())
+        except Exception as e:  # pragma: no cover - reported below
+            errs.append(repr(e))
+
+    th = [threading.Thread(target=rank_main, args=(r,)) for r in range(P)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=300)
+    assert not errs, errs
+    ref = numpy_step(initial_board(5, N, 1, True, 17), gens)
+    for r0, b in out:
+        assert np.array_equal(b, ref[r0 : r0 + b.shape[0]])
+
+
 def test_run_hint_single_graph(gol):
     """run_hint: one replay graph covers the whole expected run (37 supersteps here), other run
     lengths still use the 16/4/1 ladder; both parities stay exact."""
