@@ -401,6 +401,15 @@ class HipEngine : public Engine {
     // the whole GPU.  The two kernels of a pass overlap: while one drains, the other's waves fill
     // the freed SIMD slots (two half-board kernels on two streams: 9.8 vs 11.0 us/gen at 32768^2,
     // docs/PERFORMANCE.md).  The canonical buffers are copied in at run() entry and back at exit.
+    // Inputs identical on every rank (the decision gates a collective): mode requested, 1-D, the
+    // average strip height, the halo depth and the transport kind.
+    bool dual_preferred() const {
+        const bool want = cfg_.subtiles == 2 ||
+                          (cfg_.subtiles < 0 && g_.dec.H / std::max(1, g_.dec.Py) >= kSubtileMinRows && L_.R >= 64);
+        return want && g_.dec.Px == 1 && !cfg_.compat && !cfg_.profile && !edge_mode_ && !wd_ && L_.aligned() &&
+               (self_y() || device_transport_);
+    }
+
     bool dual_eligible() const {
         const bool want = cfg_.subtiles == 2 || (cfg_.subtiles < 0 && L_.h >= kSubtileMinRows && L_.R >= 64);
         if (!want || g_.dec.Px != 1 || cfg_.compat || cfg_.profile || edge_mode_ || split_ || wd_ ||
@@ -596,7 +605,13 @@ class HipEngine : public Engine {
         split_ = split_used() && (cfg_.sched == "auto" || cfg_.sched == "split");
         if (!tuned_) {
             if (cfg_.kernel == "auto") autotune_kernel();
-            autotune_schedule();
+            // The two-sub-tile mode runs the full schedule (its halves own the exchange); when it
+            // is wanted, every rank skips the (collective) schedule autotune: the split schedule
+            // hides an exchange of ~2-3% of a 64-generation superstep, the sub-tiles gain ~5%.
+            if (cfg_.sched == "auto" && dual_preferred())
+                split_ = false;
+            else
+                autotune_schedule();
             tuned_ = true;
             passes_.clear();  // the pass cuts may depend on the tuned kernel (pass_depths)
             // keep the collective choice for later init() calls (split_ is recomputed above)
