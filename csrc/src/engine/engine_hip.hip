@@ -255,6 +255,7 @@ class HipEngine : public Engine {
     }
 
     std::vector<u64> tile_words() override {
+        sync_canonical();
         synchronize();
         std::vector<u64> d((size_t)(L_.h * L_.nw));
         // stream-ordered (never the legacy null stream: in thread mode another rank's engine may be
@@ -272,6 +273,8 @@ class HipEngine : public Engine {
     }
 
     void set_tile_words(const std::vector<u64>& dense) override {
+        sub_current_ = false;  // the canonical board is rewritten: sub-tiles reload at the next run()
+        canon_stale_ = false;
         if ((i64)dense.size() != L_.h * L_.nw) throw Error("set_tile_words: wrong size");
         synchronize();
         std::vector<u64> m = dense;
@@ -289,6 +292,7 @@ class HipEngine : public Engine {
     }
 
     std::pair<u64, u64> local_reduce() override {
+        sync_canonical();
         HIP_CHECK(hipMemsetAsync(d_red_, 0, 2 * sizeof(u64), s_comp_));
         hipk::launch_reduce_board(buf_[cur_], L_, g_.row0, g_.word0(), g_.global_words(), d_red_, s_comp_);
         HIP_CHECK(hipGetLastError());
@@ -478,9 +482,12 @@ class HipEngine : public Engine {
     }
 
     void run_dual(u64 generations) {
-        // canonical board -> sub-tiles (interior rows)
-        for (int s = 0; s < 2; ++s)
-            dual_copy(sub_rows(s, sub_cur_, 0), buf_[cur_] + L_.index(sub_r0_[s], -1), rows_bytes(s, sub_L_[s].h));
+        // canonical board -> sub-tiles (interior rows), unless the sub-tiles already hold the board
+        // (consecutive run() calls keep the board in the halves; readers sync it back lazily)
+        if (!sub_current_)
+            for (int s = 0; s < 2; ++s)
+                dual_copy(sub_rows(s, sub_cur_, 0), buf_[cur_] + L_.index(sub_r0_[s], -1), rows_bytes(s, sub_L_[s].h));
+        sub_current_ = true;
         while (generations > 0) {
             maybe_inject_fault();
             const int k = supported_depth((int)std::min<u64>((u64)L_.R, generations));
@@ -491,12 +498,18 @@ class HipEngine : public Engine {
             stats_.supersteps += 1;
             progress("superstep");
         }
-        // both halves done -> back into the canonical buffer
+        canon_stale_ = true;  // copied back by the next reader (sync_canonical)
+        maybe_inject_fault();
+    }
+
+    // Both halves done -> the canonical buffer (before anything reads it).
+    void sync_canonical() {
+        if (!canon_stale_) return;
         HIP_CHECK(hipEventRecord(ev_sub_b_, s_comm_));
         HIP_CHECK(hipStreamWaitEvent(s_comp_, ev_sub_b_, 0));
         for (int s = 0; s < 2; ++s)
             dual_copy(buf_[cur_] + L_.index(sub_r0_[s], -1), sub_rows(s, sub_cur_, 0), rows_bytes(s, sub_L_[s].h));
-        maybe_inject_fault();
+        canon_stale_ = false;
     }
 
     struct DualCopies {
@@ -578,6 +591,8 @@ class HipEngine : public Engine {
 
    protected:
     void do_init(const PatternSpec& p) override {
+        sub_current_ = false;
+        canon_stale_ = false;
         synchronize();
         for (int i = 0; i < 2; ++i) HIP_CHECK(hipMemsetAsync(buf_[i], 0, alloc_bytes_, s_comp_));
         hipk::InitParams ip{g_.row0, g_.word0(), g_.global_words(), p.seed,
@@ -840,6 +855,7 @@ class HipEngine : public Engine {
     }
 
     std::vector<u64> read_row(i64 r) override {
+        sync_canonical();
         synchronize();
         std::vector<u64> row((size_t)L_.pitch);
         HIP_CHECK(hipMemcpyAsync(row.data(), buf_[cur_] + L_.index(r, -1), (size_t)L_.pitch * 8, hipMemcpyDeviceToHost,
@@ -1339,6 +1355,8 @@ class HipEngine : public Engine {
     i64 sub_r0_[2] = {0, 0};
     u64* sub_buf_[2][2] = {{nullptr, nullptr}, {nullptr, nullptr}};
     int sub_cur_ = 0;
+    bool sub_current_ = false;  // the halves hold the current board
+    bool canon_stale_ = false;  // buf_[cur_] lags the halves (sync_canonical before reading it)
     std::map<int, DevPlan> sub_plans_;
     std::map<int, DualCopies> dual_copies_;
     hipEvent_t ev_sub_a_ = nullptr, ev_sub_b_ = nullptr;

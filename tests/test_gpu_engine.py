@@ -70,7 +70,13 @@ def test_subtiles_single_rank(gol, N, R):
     for gens in (R * 5 + 3, 7, R * 2):
         s.step(gens)
         total += gens
+        if gens == 7:  # a reader between runs syncs the canonical board; the halves stay current
+            assert s.population() == int(numpy_step(initial_board(5, N, 1, True, N + R), total).sum())
     assert np.array_equal(s.board(), numpy_step(initial_board(5, N, 1, True, N + R), total))
+    cells = (np.random.default_rng(N).random((N, N)) < 0.3).astype(np.uint8)
+    s.set_board(cells)  # a writer invalidates the halves: the next run() reloads them
+    s.step(R + 1)
+    assert np.array_equal(s.board(), numpy_step(cells, R + 1))
 
 
 @pytest.mark.parametrize("P", [2, 3])
