@@ -84,7 +84,7 @@ Options options_from_env() {
     o.restart = env_str("GOL_RESTART", "");
     o.watchdog_s = (double)env_int("GOL_WATCHDOG", 0);
     o.verbose = env_flag("GOL_VERBOSE", false);
-    if (o.halo_depth < 0 || o.halo_depth > 64) throw Error("GOL_HALO_DEPTH must be in 1..64 (0 = auto)");
+    if (o.halo_depth < 0 || o.halo_depth > 128) throw Error("GOL_HALO_DEPTH must be in 1..128 (0 = auto)");
     if (o.kernel_depth < 0 || o.kernel_depth > 64) throw Error("GOL_KERNEL_DEPTH must be in 1..64 (0 = auto)");
     return o;
 }

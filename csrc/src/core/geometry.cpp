@@ -135,8 +135,9 @@ int clamp_halo_depth(const Decomposition& dec, int requested) {
     i64 min_h = dec.H;
     for (int i = 0; i < dec.Py; ++i) min_h = std::min(min_h, dec.row_starts[i + 1] - dec.row_starts[i]);
     i64 r = std::max(1, requested);
-    // the column halo is one 64-cell word: in 2-D a superstep may not exceed 63 generations
-    r = std::min<i64>(r, dec.Px > 1 ? 63 : 64);
+    // the column halo is one 64-cell word: in 2-D a superstep may not exceed 63 generations; 1-D
+    // strips have no column halo (128: deep supersteps for the two-sub-tile mode)
+    r = std::min<i64>(r, dec.Px > 1 ? 63 : 128);
     r = std::min<i64>(r, min_h);
     return (int)std::max<i64>(1, r);
 }

@@ -63,7 +63,7 @@ std::vector<std::vector<Item>> pack_waves(const std::vector<Region>& regions, i6
         if (rows <= 0 || words <= 0) continue;
         // rows may extend into the ghost rows and columns into the ghost words (multi-pass
         // supersteps: at most the 64-row halo and the one-word column halo)
-        if (rg.r0 < -64 || rg.r1 > h + 64 || rg.c0 < -1 || rg.c1 > nw + 1) throw Error("plan region outside the tile");
+        if (rg.r0 < -128 || rg.r1 > h + 128 || rg.c0 < -1 || rg.c1 > nw + 1) throw Error("plan region outside the tile");
         i64 nch = ceil_div(rows, rows_per_chunk);
         i64 base = rows / nch, extra = rows % nch;
         i64 r = rg.r0;

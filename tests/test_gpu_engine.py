@@ -60,7 +60,7 @@ def test_graph_replay(gol, graph):
     assert np.array_equal(s.board(), numpy_step(initial_board(5, N, 1, True, 11), gens))
 
 
-@pytest.mark.parametrize("N,R", [(640, 8), (1024, 16), (4096, 32)])
+@pytest.mark.parametrize("N,R", [(640, 8), (1024, 16), (4096, 32), (2048, 128)])
 def test_subtiles_single_rank(gol, N, R):
     """GOL_SUBTILES=2: two half-tiles on two streams with seam copies and the torus wrap between
     them; remainder supersteps and repeated run() calls (copy in / copy back) stay exact."""
