@@ -458,7 +458,14 @@ class HipEngine : public Engine {
         const Layout& L = sub_L_[s];
         std::vector<Region> rg = {{-e, L.h + e, 0, L.nw}};
         i64 bpc = hipk::step_blocks_per_cu(k, sub_flags());
-        if (occ_ > 0) bpc = std::min<i64>(bpc, occ_);
+        // waves/SIMD each half's plan is sized for: two concurrent halves fill the SIMDs between
+        // them, so 2-wave plans (taller segments, less halo) measured best (kbench: 9.85 vs 10.11
+        // us/gen at 32768^2); GOL_SUB_OCC overrides (0 = the single-tile tuned occupancy)
+        const int so = (int)env_int("GOL_SUB_OCC", 2);
+        if (so > 0)
+            bpc = std::min<i64>(bpc, so);
+        else if (occ_ > 0)
+            bpc = std::min<i64>(bpc, occ_);
         const i64 rows = balanced_rows_per_chunk(rg, L.nw, L.h, k, bpc * kWavesPerBlock * cus_, 2 * (i64)k, true);
         DevPlan p;
         std::vector<LaneDesc> lanes = build_plan(rg, L.nw, L.h, rows, k, true, &p.st, kWavesPerBlock, cfg_.plan_xcds);
