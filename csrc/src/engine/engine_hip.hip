@@ -410,13 +410,14 @@ class HipEngine : public Engine {
     bool dual_preferred() const {
         const bool want = cfg_.subtiles == 2 ||
                           (cfg_.subtiles < 0 && g_.dec.H / std::max(1, g_.dec.Py) >= kSubtileMinRows && L_.R >= 64);
-        return want && g_.dec.Px == 1 && !cfg_.compat && !cfg_.profile && !edge_mode_ && !wd_ && L_.aligned() &&
+        return want && g_.dec.Px == 1 && !cfg_.compat && !cfg_.profile && !edge_mode_ && !cfg_.force_split && !wd_ &&
+               L_.aligned() &&
                (self_y() || device_transport_);
     }
 
     bool dual_eligible() const {
         const bool want = cfg_.subtiles == 2 || (cfg_.subtiles < 0 && L_.h >= kSubtileMinRows && L_.R >= 64);
-        if (!want || g_.dec.Px != 1 || cfg_.compat || cfg_.profile || edge_mode_ || split_ || wd_ ||
+        if (!want || g_.dec.Px != 1 || cfg_.compat || cfg_.profile || edge_mode_ || cfg_.force_split || split_ || wd_ ||
             kern_[0] != "temporal" || !L_.aligned() || L_.h < 8 * (i64)L_.R)
             return false;
         if (!self_y() && !device_transport_) return false;

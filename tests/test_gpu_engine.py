@@ -116,7 +116,7 @@ def test_run_hint_single_graph(gol):
     lengths still use the 16/4/1 ladder; both parities stay exact."""
     N, R = 512, 8
     hint = R * 37 + 5
-    s = _sim(gol, N, halo_depth=R, kernel_depth=R, kernel="temporal", run_hint=hint).init(5, seed=13)
+    s = _sim(gol, N, halo_depth=R, kernel_depth=R, kernel="temporal", run_hint=hint, subtiles=0).init(5, seed=13)
     g0 = s.stats()["graph_launches"]
     s.step(hint)
     assert s.stats()["graph_launches"] - g0 == 1, s.stats()
@@ -131,7 +131,7 @@ def test_graph_replay_after_parity_flip(gol, R, K):
     """Replays are keyed by buffer parity and track it: graphs of 16, 4 and 1 supersteps (1 or 3
     passes per superstep flip the parity per superstep) interleaved with eager remainders."""
     N = 512
-    s = _sim(gol, N, halo_depth=R, kernel_depth=K, kernel="temporal").init(5, seed=12)
+    s = _sim(gol, N, halo_depth=R, kernel_depth=K, kernel="temporal", subtiles=0).init(5, seed=12)  # graphs
     total = 0
     for gens in (R * 16, 8, R * 21 + 3, 5, R * 16 + R * 4 + R + 7, 2 * R + 1):
         s.step(gens)
