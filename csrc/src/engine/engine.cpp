@@ -28,10 +28,13 @@ Engine::Engine(const Geometry& g, const EngineConfig& c, std::shared_ptr<Transpo
     // cross-stream events per generation for < 0.5% of ghost-row recompute; measured +1.7% on the
     // eager multi-GPU schedule, docs/PERFORMANCE.md.
     // The HIP backend runs a superstep as kernel passes of K (auto 8) generations (deep halos).
-    const bool tall_strips = g_.dec.Px == 1 && g_.h >= 8192;
+    // (from the average strip height, identical on every rank: all ranks must cut the same
+    // supersteps, and uneven strips differ by a row)
+    const i64 strip_rows = g_.dec.H / std::max(1, g_.dec.Py);
+    const bool tall_strips = g_.dec.Px == 1 && strip_rows >= 8192;
     // ... and 64 for the two-sub-tile mode (HIP, GOL_SUBTILES auto or 2, tiles of >= 24576 rows): it
     // synchronises its two streams once per superstep, so longer supersteps keep more of the overlap
-    const bool sub_tall = cfg_.backend == "hip" && cfg_.subtiles != 0 && g_.dec.Px == 1 && g_.h >= kSubtileMinRows;
+    const bool sub_tall = cfg_.backend == "hip" && cfg_.subtiles != 0 && g_.dec.Px == 1 && strip_rows >= kSubtileMinRows;
     const int want = cfg_.halo_depth > 0 ? cfg_.halo_depth : ((g_.dec.P > 1 && tall_strips) || sub_tall ? 64 : 32);
     int R = clamp_halo_depth(g_.dec, want);
     if (cfg_.compat) {
