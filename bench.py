@@ -44,6 +44,11 @@ def main() -> int:
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--no-overlap", action="store_true")
     ap.add_argument("--yardstick", action="store_true", help="also time the naive byte-per-cell kernel (rank 0)")
+    ap.add_argument("--self-exchange", action="store_true",
+                    help="route the halos of directions whose neighbour is the rank itself through the transport "
+                         "(one GPU: a 1-rank RCCL communicator, ncclSend/ncclRecv to itself)")
+    ap.add_argument("--allow-host-staging", action="store_true",
+                    help="if RCCL cannot initialise, stage halos through host memory instead of failing")
     ap.add_argument("--seed", type=int, default=0x5EED)
     args = ap.parse_args()
 
@@ -61,6 +66,7 @@ def main() -> int:
         size, steps, warmup = 256, min(steps, 100), min(warmup, 10)
 
     rank, P, local, cpu_group = init_distributed()
+    rccl = None
     if P > 1:
         control = torch_transport(cpu_group)
         transport = control
@@ -68,17 +74,26 @@ def main() -> int:
             import torch
             import torch.distributed as dist
 
-            rccl = None
             try:
                 rccl = rccl_transport(control, group=cpu_group)
-            except Exception as e:  # keep the run alive: halos staged through host memory instead
+            except Exception as e:
                 print(f"[bench] rank {rank}: RCCL transport unavailable ({e})", file=sys.stderr, flush=True)
             ok = torch.tensor([1 if rccl is not None else 0], dtype=torch.int32)
             dist.all_reduce(ok, op=dist.ReduceOp.MIN, group=cpu_group)  # every rank must agree
             if int(ok.item()) == 1:
                 transport = rccl
+            elif not args.allow_host_staging:
+                # a multi-GPU number measured over host-staged halos is not the RCCL/xGMI design
+                if rank == 0:
+                    print("[bench] RCCL unavailable on some rank: refusing to measure host-staged halos "
+                          "(pass --allow-host-staging to do so)", file=sys.stderr, flush=True)
+                return 3
             elif rank == 0:
                 print("[bench] using host-staged halos on every rank", file=sys.stderr, flush=True)
+    elif args.self_exchange and backend == "hip":
+        native.hip_set_device(0)
+        rccl = native.make_rccl_transport(native.SelfTransport())
+        transport = rccl
     else:
         transport = native.SelfTransport()
 
@@ -95,6 +110,7 @@ def main() -> int:
         kernel=args.kernel,
         device=local if backend == "hip" else None,
         run_hint=steps,  # the timed run replays one captured graph (graph boundaries idle the GPU)
+        self_exchange=args.self_exchange,
     )
     sim.init(pattern=5, seed=args.seed)
     dec = sim.decomposition
@@ -117,6 +133,8 @@ def main() -> int:
     transport.barrier()
     elapsed = transport.allreduce_max(t1 - t0)
     pop = sim.population()
+    st = sim.stats()
+    halo_bytes = transport.allreduce_sum(int(st["halo_bytes"]))  # all ranks, init + warmup + timed
 
     yard = None
     if args.yardstick and rank == 0 and have_gpu:
@@ -127,7 +145,6 @@ def main() -> int:
 
     if rank == 0:
         value = cells * steps / elapsed
-        st = sim.stats()
         out = {
             "metric": METRIC,
             "value": value,
@@ -159,6 +176,11 @@ def main() -> int:
                 "plan_waves": st["plan_waves"],
                 "lane_efficiency": round(st["lane_efficiency"], 4),
                 "population": pop,
+                "transport": transport.name(),
+                "rccl_nranks": transport.data_plane_ranks() if rccl is not None else None,
+                "self_exchange": bool(args.self_exchange),
+                "halo_exchanges_rank0": st["exchanges"],
+                "halo_bytes_all_ranks": halo_bytes,
             },
             "baseline_note": "reference publishes no numbers (BASELINE.md); vs_baseline is null",
         }
@@ -166,18 +188,19 @@ def main() -> int:
             out["yardstick_naive_byte_kernel"] = yard
             out["speedup_vs_yardstick"] = value / (yard["cell_updates_per_s"] * P)
         print(json.dumps(out), flush=True)
-    if P > 1:
+    if P > 1 or rccl is not None:
         import gc
 
+        # Tear the engine (its graphs first) and then the RCCL communicator down on every rank while
+        # all peers are still alive, not at interpreter exit where a rank could outlive its
+        # neighbours.  (ncclCommDestroy while a graph that captured the communicator still exists
+        # blocks: profiles/rccl_self_probe.txt.)
+        sim.synchronize()
+        del sim, transport, rccl
+        gc.collect()
+    if P > 1:
         import torch.distributed as dist
 
-        # Tear the engine and its RCCL communicator down on every rank while all peers are still
-        # alive (not at interpreter exit, where a rank could outlive its neighbours).
-        sim.synchronize()
-        del sim, transport
-        if backend == "hip":
-            del rccl
-        gc.collect()
         dist.barrier(group=cpu_group)  # gloo: also fine when ranks share a GPU (rehearsal runs)
         dist.destroy_process_group()
     return 0

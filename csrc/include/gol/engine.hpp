@@ -16,6 +16,7 @@
 // replayed; there is no host synchronisation inside run().
 #pragma once
 
+#include <algorithm>
 #include <memory>
 #include <string>
 #include <utility>
@@ -49,8 +50,6 @@ struct EngineConfig {
                                       // tile (LDS-resident) | lds (1 gen, reference-class LDS tile)
     int tile_waves = 8;               // tile kernel: waves per workgroup (4, 8, 16)
     bool tune_tile_waves = true;      // GOL_KERNEL=auto may also try 8 waves (false: GOL_TILE_WAVES set)
-    std::string prefetch = "reg";     // temporal kernel row prefetch: reg (pinned triple) | lds (DMA ring)
-    std::string pipeline = "chain";   // temporal kernel level pipeline: chain | skew (ILP variant)
     std::string transport = "auto";   // auto | device | host  (host = stage halos through host memory)
     bool profile = false;             // per-phase event timing
     int graph_supersteps = 0;         // supersteps per captured graph (0 = auto, even)
@@ -59,8 +58,13 @@ struct EngineConfig {
     u64 run_hint = 0;                 // generations of the runs to come (CLI: iterations); the HIP
                                       // engine captures one graph covering them (<= 256 supersteps)
     bool graph_rccl = false;          // also capture supersteps whose exchange is an RCCL group
+    int sub_occ = 2;                  // sub-tile plans: waves per SIMD each half is sized for (GOL_SUB_OCC;
+                                      // 0 = the single-tile tuned occupancy)
+    bool self_exchange = false;       // GOL_SELF_EXCHANGE: directions whose neighbour is this rank go
+                                      // through the transport (peer == rank) instead of wrapping by
+                                      // addressing: runs every halo path of the multi-GPU engine on
+                                      // one rank (e.g. a 1-rank RCCL communicator)
     double watchdog_s = 0;            // abort the job after this long without progress (0 = off)
-    int edge_cus = 0;                 // >0: CU-partitioned edge-stream schedule (experimental, opt-in)
     bool force_split = false;         // run the interior/boundary edge schedule even without neighbours
     std::string sched = "auto";       // with neighbours: auto (timed at init) | split (overlap) | full
 };
@@ -124,9 +128,21 @@ class Engine {
     };
     // Canonical-order halo messages of a k-deep superstep (self directions omitted).
     std::vector<HaloItem> halo_items(int k) const;
-    bool self_x() const { return g_.nbr[DIR_W] == g_.rank && g_.nbr[DIR_E] == g_.rank; }
-    bool self_y() const { return g_.nbr[DIR_N] == g_.rank && g_.nbr[DIR_S] == g_.rank; }
+    // Halo layout: 2-D blocks (column halos, 8 directions) or 1-D row strips.
+    bool two_d() const { return g_.dec.Px > 1 || (xchg_self_ && g_.dec.want_2d); }
+    // Directions whose neighbour is this rank wrap by addressing (no messages), unless the
+    // self-exchange mode routes them through the transport (x only has halos in the 2-D layout).
+    bool self_x() const {
+        return g_.nbr[DIR_W] == g_.rank && g_.nbr[DIR_E] == g_.rank && !(xchg_self_ && two_d());
+    }
+    bool self_y() const { return g_.nbr[DIR_N] == g_.rank && g_.nbr[DIR_S] == g_.rank && !xchg_self_; }
     bool xwrap_by_plan() const { return self_x() && L_.aligned(); }
+    // Rows of the smallest tile of the job (identical on every rank).
+    i64 min_tile_rows() const {
+        i64 m = g_.dec.H;
+        for (int i = 0; i < g_.dec.Py; ++i) m = std::min(m, g_.dec.row_starts[i + 1] - g_.dec.row_starts[i]);
+        return m;
+    }
 
    protected:
     Engine(const Geometry& g, const EngineConfig& c, std::shared_ptr<Transport> t);
@@ -166,6 +182,7 @@ class Engine {
     i64 fault_gen_ = -1;
     std::string fault_mode_ = "abort";  // GOL_FAULT=rank:gen[:abort|hang|exit]
     std::unique_ptr<Watchdog> wd_;
+    bool xchg_self_ = false;  // cfg_.self_exchange (not in compat mode)
 };
 
 std::unique_ptr<Engine> make_cpu_engine(const Geometry& g, const EngineConfig& c, std::shared_ptr<Transport> t);

@@ -50,6 +50,8 @@ struct Decomposition {
     // strip s covers global rows [strip_starts[s], strip_starts[s+1]).  Always P strips.
     std::vector<i64> strip_starts;
 
+    bool want_2d = false;   // GOL_DECOMP=2d was requested (a 1 x Py grid can still run the 2-D halo
+                            // layout through the transport: Engine self-exchange mode)
     bool two_d() const { return Px > 1; }
     int rank_of(int cx, int cy) const { return (int)(pmod(cy, Py) * Px + pmod(cx, Px)); }
     std::string describe() const;

@@ -28,16 +28,12 @@ enum : u32 {
     STEP_WRAP_X = 1u << 0,  // LDS kernel: tile is its own E/W neighbour (w % 64 == 0); the temporal
                             // kernel gets x-wrap from its plan (build_plan(..., xwrap = true))
     STEP_WRAP_Y = 1u << 1,  // tile is its own N/S neighbour: rows are read modulo h, no ghost rows
-    STEP_PF_LDS = 1u << 2,  // temporal kernel: prefetch rows through a per-wave LDS ring (DMA)
-    STEP_SKEW = 1u << 3,    // temporal kernel: skewed level pipeline (K independent chains per row)
     STEP_TILE_L2 = 1u << 4, // tile kernel: two generations per LDS pass (half the barriers)
 };
 
-// Rows the HIP engine allocates past the bottom halo: prefetch / flush overrun (skewed pipeline:
-// K-1 rows, LDS ring: kRingRows-1 rows) + the trash row the temporal kernel's halo lanes store into.
+// Rows the HIP engine allocates past the bottom halo: the temporal kernel's 3-row prefetch overrun
+// + the trash row its halo lanes store into (and the tile kernel's over-read slack).
 constexpr int kSlackRows = 32;
-// Per-wave LDS prefetch ring depth (rows) of the temporal kernel.
-constexpr int kRingRows = 10;
 
 struct StepParams {
     i64 pitch;

@@ -19,6 +19,7 @@
 // (torch.distributed / gloo) in the bindings.
 #pragma once
 
+#include <deque>
 #include <memory>
 #include <string>
 #include <vector>
@@ -66,6 +67,9 @@ class Transport {
     [[noreturn]] virtual void abort(int code);
     // Asynchronous failure of the data plane (e.g. ncclCommGetAsyncError); empty when healthy.
     virtual std::string async_error() { return ""; }
+    // Ranks of the device data plane's communicator as the library reports them (RCCL:
+    // ncclCommCount); -1 for host transports.
+    virtual int data_plane_ranks() { return -1; }
 };
 
 // P = 1.
@@ -74,8 +78,11 @@ class SelfTransport : public Transport {
     int rank() const override { return 0; }
     int size() const override { return 1; }
     std::string name() const override { return "self"; }
-    void send_bytes(int, const void*, size_t) override;
-    void recv_bytes(int, void*, size_t) override;
+    void send_bytes(int peer, const void* buf, size_t n) override;
+    void recv_bytes(int peer, void* buf, size_t n) override;
+
+   private:
+    std::deque<std::vector<u8>> box_;  // loopback FIFO
 };
 
 // P ranks as threads of one process; host-memory mailboxes.

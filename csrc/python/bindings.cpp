@@ -199,6 +199,7 @@ PYBIND11_MODULE(_gol, m) {
         .def("size", &Transport::size)
         .def("name", &Transport::name)
         .def("device_buffers", &Transport::device_buffers)
+        .def("data_plane_ranks", &Transport::data_plane_ranks)
         .def("barrier", &Transport::barrier, py::call_guard<py::gil_scoped_release>())
         .def("allreduce_max", &Transport::allreduce_max, py::call_guard<py::gil_scoped_release>())
         .def("allreduce_sum", &Transport::allreduce_sum, py::call_guard<py::gil_scoped_release>());
@@ -245,8 +246,6 @@ PYBIND11_MODULE(_gol, m) {
         .def_readwrite("rows_per_wave", &EngineConfig::rows_per_wave)
         .def_readwrite("waves_target", &EngineConfig::waves_target)
         .def_readwrite("kernel", &EngineConfig::kernel)
-        .def_readwrite("prefetch", &EngineConfig::prefetch)
-        .def_readwrite("pipeline", &EngineConfig::pipeline)
         .def_readwrite("transport", &EngineConfig::transport)
         .def_readwrite("profile", &EngineConfig::profile)
         .def_readwrite("graph_supersteps", &EngineConfig::graph_supersteps)
@@ -255,7 +254,8 @@ PYBIND11_MODULE(_gol, m) {
         .def_readwrite("watchdog_s", &EngineConfig::watchdog_s)
         .def_readwrite("tile_waves", &EngineConfig::tile_waves)
         .def_readwrite("tune_tile_waves", &EngineConfig::tune_tile_waves)
-        .def_readwrite("edge_cus", &EngineConfig::edge_cus)
+        .def_readwrite("sub_occ", &EngineConfig::sub_occ)
+        .def_readwrite("self_exchange", &EngineConfig::self_exchange)
         .def_readwrite("force_split", &EngineConfig::force_split)
         .def_readwrite("sched", &EngineConfig::sched)
         .def_readwrite("kernel_depth", &EngineConfig::kernel_depth)

@@ -66,6 +66,11 @@ class RcclTransport : public Transport {
     void gatherv(const void* send, size_t n, std::vector<std::vector<u8>>* out, int root) override {
         ctl_->gatherv(send, n, out, root);
     }
+    int data_plane_ranks() override {
+        int n = -1;
+        if (comm_ && ncclCommCount(comm_, &n) != ncclSuccess) return -1;
+        return n;
+    }
     std::string async_error() override {
         if (!comm_) return "";
         ncclResult_t st = ncclSuccess;

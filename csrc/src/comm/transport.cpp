@@ -99,8 +99,20 @@ void Transport::abort(int code) {
 // SelfTransport
 // ---------------------------------------------------------------------------------------------
 
-void SelfTransport::send_bytes(int, const void*, size_t) { throw Error("SelfTransport has no peers"); }
-void SelfTransport::recv_bytes(int, void*, size_t) { throw Error("SelfTransport has no peers"); }
+// Loopback: messages to rank 0 (itself) queue in FIFO order (the engine's self-exchange mode sends
+// every halo to itself before receiving it).
+void SelfTransport::send_bytes(int peer, const void* buf, size_t n) {
+    if (peer != 0) throw Error(strprintf("SelfTransport: no rank %d", peer));
+    box_.emplace_back((const u8*)buf, (const u8*)buf + n);
+}
+void SelfTransport::recv_bytes(int peer, void* buf, size_t n) {
+    if (peer != 0) throw Error(strprintf("SelfTransport: no rank %d", peer));
+    if (box_.empty()) throw Error("SelfTransport: receive without a matching send (would block forever)");
+    if (box_.front().size() != n)
+        throw Error(strprintf("SelfTransport: message size mismatch (%zu vs %zu bytes)", box_.front().size(), n));
+    if (n) memcpy(buf, box_.front().data(), n);
+    box_.pop_front();
+}
 
 // ---------------------------------------------------------------------------------------------
 // ThreadTransport: mailboxes[dst][src] of byte messages; sends never block.

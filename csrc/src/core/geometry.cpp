@@ -97,6 +97,7 @@ Decomposition make_decomposition(i64 N, int P, bool global_mode, const std::stri
     if (Py > d.H) throw Error("grid has more row ranks than board rows");
     d.Px = Px;
     d.Py = Py;
+    d.want_2d = Px > 1 || (dm == "2d" && (d.W % 64) == 0);
     d.row_starts = even_split(d.H, Py, 1);
     d.col_starts = (Px > 1) ? even_split(d.W, Px, 64) : std::vector<i64>{0, d.W};
     if (d.per_rank) {

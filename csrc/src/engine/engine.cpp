@@ -20,6 +20,7 @@ namespace gol {
 Engine::Engine(const Geometry& g, const EngineConfig& c, std::shared_ptr<Transport> t)
     : g_(g), cfg_(c), t_(std::move(t)) {
     if (!t_) throw Error("engine needs a transport");
+    xchg_self_ = cfg_.self_exchange && !cfg_.compat;
     if (t_->size() != g_.dec.P || t_->rank() != g_.rank)
         throw Error(strprintf("transport (rank %d of %d) does not match the geometry (rank %d of %d)", t_->rank(),
                               t_->size(), g_.rank, g_.dec.P));
@@ -31,14 +32,20 @@ Engine::Engine(const Geometry& g, const EngineConfig& c, std::shared_ptr<Transpo
     // (from the average strip height, identical on every rank: all ranks must cut the same
     // supersteps, and uneven strips differ by a row)
     const i64 strip_rows = g_.dec.H / std::max(1, g_.dec.Py);
-    const bool tall_strips = g_.dec.Px == 1 && strip_rows >= 8192;
-    // ... and 64 for the two-sub-tile mode (HIP, GOL_SUBTILES auto or 2, tiles of >= 24576 rows): it
-    // synchronises its two streams once per superstep, so longer supersteps keep more of the overlap
-    const bool sub_tall = cfg_.backend == "hip" && cfg_.subtiles != 0 && g_.dec.Px == 1 && strip_rows >= kSubtileMinRows;
+    const bool tall_strips = !two_d() && strip_rows >= 8192;
+    // ... and 64 when the two-sub-tile mode can run (HIP, GOL_SUBTILES auto or 2, 1-D tiles of >=
+    // 24576 rows, aligned width, no measurement / watchdog / compat mode, and a transport whose
+    // exchange it can drive): it synchronises its two streams once per superstep, so longer
+    // supersteps keep more of the overlap.  Rank-invariant inputs only.
+    const bool sub_transport = cfg_.transport != "host" && (g_.dec.P == 1 || t_->device_buffers());
+    const bool sub_tall = cfg_.backend == "hip" && cfg_.subtiles != 0 && !two_d() && strip_rows >= kSubtileMinRows &&
+                          g_.dec.W % 64 == 0 && !cfg_.force_split && !cfg_.profile && cfg_.watchdog_s <= 0 &&
+                          !cfg_.compat && cfg_.kernel != "lds" && sub_transport;
     const int want = cfg_.halo_depth > 0 ? cfg_.halo_depth : ((g_.dec.P > 1 && tall_strips) || sub_tall ? 64 : 32);
     int R = clamp_halo_depth(g_.dec, want);
+    if (two_d()) R = std::min(R, 63);  // the column halo is one 64-cell word
     if (cfg_.compat) {
-        if (g_.dec.Px != 1) throw Error("GOL_COMPAT=reference supports 1-D row strips only");
+        if (two_d()) throw Error("GOL_COMPAT=reference supports 1-D row strips only");
         R = 1;
     }
     L_ = Layout(g_.h, g_.w, R);
@@ -95,10 +102,10 @@ std::vector<Engine::HaloItem> Engine::halo_items(int k) const {
     const i64 h = L_.h, nw = L_.nw, P = L_.pitch;
     auto add = [&](Dir d, Rect s, Rect r, bool contig) {
         const int sp = g_.nbr[d], rp = g_.nbr[opposite(d)];
-        if (sp == g_.rank && rp == g_.rank) return;  // self direction: wrap by addressing
+        if (sp == g_.rank && rp == g_.rank && !xchg_self_) return;  // self direction: wrap by addressing
         items.push_back({d, sp, rp, s, r, contig});
     };
-    if (g_.dec.Px == 1) {
+    if (!two_d()) {
         if (!self_y()) {
             add(DIR_N, {0, k, -1, P}, {h, k, -1, P}, true);
             add(DIR_S, {h - k, k, -1, P}, {-k, k, -1, P}, true);

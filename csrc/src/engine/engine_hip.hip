@@ -8,7 +8,6 @@
 //   split:  s_comm:  wait(ev_ready) -> pack (2-D) -> RCCL group send/recv (or host staging) -> unpack -> ev_halo
 //           s_comp:  interior kernel -> wait(ev_halo) -> boundary kernel -> later passes -> ev_ready
 //   full:   s_comp:  exchange -> full-region kernel -> later passes
-//   (opt-in edge mode: boundary bands on a CU-partitioned s_comm, concurrently with the interior)
 // With graphs on, G/(m*R) captures of m supersteps (even pass count => parity preserved) are replayed.
 #include <hip/hip_runtime.h>
 
@@ -90,6 +89,7 @@ class HipEngine : public Engine {
         }
         if (!multipass_) R = std::min(R, K);
         kdepth_ = K;
+        tdepth_ = supported_kernel_depth(std::min(K, hipk::max_step_depth()));
         if (R != L_.R) L_ = Layout(L_.h, L_.w, R);
         stats_.depth = R;
         // slack rows: the temporal kernel prefetches 3 rows past a segment's last input row
@@ -99,17 +99,10 @@ class HipEngine : public Engine {
         device_transport_ = t_->device_buffers() && cfg_.transport != "host";
         if (cfg_.transport == "device" && !t_->device_buffers())
             throw Error("GOL_TRANSPORT=device needs a device transport (RCCL)");
-        // Edge-stream schedule (multi-GPU with a device transport): halo exchange + boundary bands
-        // run on their own stream, concurrently with the interior of the same superstep.
-        // Opt-in (GOL_EDGE_CUS > 0): measured on MI355X, a CU-masked compute stream runs the
-        // interior ~20% slower, which costs more than the partition saves (docs/PERFORMANCE.md).
         for (auto& kk : kern_) kk = kernel_;
-        edge_mode_ = cfg_.edge_cus > 0 && L_.R == kdepth_ && cfg_.overlap && !cfg_.compat && !cfg_.profile &&
-                     kernel_ != "lds" &&
-                     can_overlap() && !(self_x() && !L_.aligned()) &&
-                     ((device_transport_ && !halo_items(L_.R).empty()) || cfg_.force_split);
-        create_streams();
-        events_needed_ = edge_mode_ || cfg_.force_split || !halo_items(L_.R).empty();
+        HIP_CHECK(hipStreamCreateWithFlags(&s_comp_, hipStreamNonBlocking));
+        HIP_CHECK(hipStreamCreateWithFlags(&s_comm_, hipStreamNonBlocking));
+        events_needed_ = cfg_.force_split || !halo_items(L_.R).empty();
         // All device memory work is ordered on the engine's own streams.  (They are non-blocking:
         // null-stream calls such as hipMemset, or a pageable hipMemcpy whose DMA may still be in
         // flight when it returns, would NOT be ordered before their kernels.)
@@ -121,8 +114,6 @@ class HipEngine : public Engine {
                              (env_str("GOL_EVENT_SCOPE", "system") == "device" ? hipEventReleaseToDevice : 0u);
         HIP_CHECK(hipEventCreateWithFlags(&ev_ready_, evf));
         HIP_CHECK(hipEventCreateWithFlags(&ev_halo_, evf));
-        HIP_CHECK(hipEventCreateWithFlags(&ev_int_, evf));
-        HIP_CHECK(hipEventCreateWithFlags(&ev_bnd_, evf));
         if (cfg_.profile) {
             for (auto* e : {&ev_t0_, &ev_t1_, &ev_t2_, &ev_t3_}) HIP_CHECK(hipEventCreate(e));
         }
@@ -130,59 +121,10 @@ class HipEngine : public Engine {
         HIP_CHECK(hipHostMalloc(&h_red_, 2 * sizeof(u64), hipHostMallocDefault));
     }
 
-    // The compute stream and the comm/edge stream.  In edge mode the edge stream gets a private
-    // partition of `edge_cus` CUs (hipExtStreamCreateWithCUMask) and the compute stream the rest:
-    // a one-round interior plan fills every VGPR slot of its CUs, so without a partition the RCCL
-    // kernels and the boundary bands could not become resident until the interior retires, and
-    // the exchange would serialise behind it.
-    void create_streams() {
-        comp_cus_ = cus_;
-        edge_cus_ = 0;
-        const int want = cfg_.edge_cus;
-        if (edge_mode_ && want > 0 && want <= cus_ / 4) {
-            // Workgroups are dispatched round-robin over the XCDs, so both partitions must span
-            // every XCD (a partition missing from one XCD makes that XCD the straggler).  Pick
-            // c = x*per + (per-1 - 8r - x) for XCD x and round r: one CU per XCD per round whether
-            // the mask numbers CUs XCD-major (c / per) or XCD-interleaved (c % 8).
-            const int xcds = 8, per = cus_ / xcds;
-            const int words = (cus_ + 31) / 32;
-            std::vector<uint32_t> mc(words, 0), me(words, 0);
-            std::vector<char> edge(cus_, 0);
-            int picked = 0;
-            for (int r = 0; picked < want && r < per / xcds; ++r)
-                for (int x = 0; x < xcds && picked < want; ++x, ++picked) edge[x * per + (per - 1 - 8 * r - x)] = 1;
-            if (cus_ % xcds) picked = 0;  // unexpected topology: fall back to the plain layout
-            for (int c = 0; c < cus_; ++c) (edge[c] ? me : mc)[c / 32] |= 1u << (c % 32);
-            if (picked != want) {
-                std::fill(me.begin(), me.end(), 0);
-                std::fill(mc.begin(), mc.end(), 0);
-                for (int c = 0; c < cus_; ++c) (c >= cus_ - want ? me : mc)[c / 32] |= 1u << (c % 32);
-            }
-            if (hipExtStreamCreateWithCUMask(&s_comp_, (uint32_t)words, mc.data()) == hipSuccess &&
-                hipExtStreamCreateWithCUMask(&s_comm_, (uint32_t)words, me.data()) == hipSuccess) {
-                comp_cus_ = cus_ - want;
-                edge_cus_ = want;
-                return;
-            }
-            hipGetLastError();
-            if (s_comp_) hipStreamDestroy(s_comp_);
-            s_comp_ = nullptr;
-            fprintf(stderr, "[gol] CU-masked streams unavailable; edge stream shares all CUs\n");
-        }
-        HIP_CHECK(hipStreamCreateWithFlags(&s_comp_, hipStreamNonBlocking));
-        HIP_CHECK(hipStreamCreateWithFlags(&s_comm_, hipStreamNonBlocking));
-    }
-
     // Host -> device copy ordered on the compute stream; returns when the data is in HBM.
     void upload(void* dst, const void* src, size_t n) {
         HIP_CHECK(hipMemcpyAsync(dst, src, n, hipMemcpyHostToDevice, s_comp_));
         HIP_CHECK(hipStreamSynchronize(s_comp_));
-    }
-
-    // CUs a plan of this kind runs on (resident-wave budget of its one-round balance).
-    int plan_cus(int kind) const {
-        if (kind == 2 && edge_mode_) return edge_cus_ > 0 ? edge_cus_ : cus_;
-        return comp_cus_;
     }
 
     // Every buffer-writing operation on the compute stream ends with this: the next superstep's
@@ -193,9 +135,6 @@ class HipEngine : public Engine {
         // GPU (a release fence), measured between eager supersteps on one MI355X.
         if (!events_needed_) return;
         HIP_CHECK(hipEventRecord(ev_ready_, s_comp_));
-        if (!edge_mode_) return;  // ev_int_ / ev_bnd_ order the edge-stream schedule only
-        HIP_CHECK(hipEventRecord(ev_int_, s_comp_));
-        HIP_CHECK(hipEventRecord(ev_bnd_, s_comp_));
     }
 
     ~HipEngine() override {
@@ -224,8 +163,6 @@ class HipEngine : public Engine {
         hipHostFree(h_red_);
         hipEventDestroy(ev_ready_);
         hipEventDestroy(ev_halo_);
-        hipEventDestroy(ev_int_);
-        hipEventDestroy(ev_bnd_);
         for (auto e : fence_ev_)
             if (e) hipEventDestroy(e);
         for (auto e : {ev_sync_comm_, ev_sync_comp_})
@@ -316,19 +253,31 @@ class HipEngine : public Engine {
         return true;
     }
 
-    // Replay sizes, largest first: the run-length hint (one graph for the whole expected run, at
-    // most 256 supersteps), then M, 4 and 1 supersteps for any other length.  Every graph boundary
-    // costs ~8.5 us of GPU idle (8192^2 x 1000 through the CLI: 5 boundaries, 3% of the run).
-    std::vector<int> graph_ladder(int k, int M) const {
-        std::vector<int> ms;
-        const u64 h = cfg_.run_hint / (u64)std::max(1, k);
-        if (h > 1 && h != (u64)M && h != 4) ms.push_back((int)std::min<u64>(h, 256));
+    // Replay shapes {m supersteps of k, then one superstep of rem < k generations}, largest first:
+    // the run-length hint as ONE graph (its whole superstep count, at most 256, plus its remainder:
+    // the driver's 20-generation bench is a single replay), then M, 4 and 1 supersteps, then the
+    // hint's remainder alone.  Every graph boundary costs ~8.5 us of GPU idle (8192^2 x 1000 through
+    // the CLI: 5 boundaries, 3% of the run).
+    struct Shape {
+        int m, rem;
+    };
+    std::vector<Shape> graph_ladder(int k, int M) const {
+        std::vector<Shape> v;
+        const u64 hm = std::min<u64>(cfg_.run_hint / (u64)std::max(1, k), 256);
+        const int hr = cfg_.compat || cfg_.run_hint / (u64)std::max(1, k) > 256 ? 0 : (int)(cfg_.run_hint % (u64)k);
+        if (hm > 0 && hm + (hr > 0) > 1) v.push_back({(int)hm, hr});
         for (int m : {M, 4, 1})
-            if (m <= M) ms.push_back(m);
-        std::sort(ms.begin(), ms.end(), std::greater<int>());
-        ms.erase(std::unique(ms.begin(), ms.end()), ms.end());
-        return ms;
+            if (m <= M && !(m == (int)hm && hr == 0)) v.push_back({m, 0});
+        if (hr > 0) v.push_back({0, hr});
+        std::sort(v.begin(), v.end(), [&](const Shape& a, const Shape& b) {
+            return (u64)a.m * k + a.rem > (u64)b.m * k + b.rem;
+        });
+        return v;
     }
+
+    // Buffer parity of the active mode (one tile: cur_; two sub-tiles: sub_cur_).
+    int par() const { return dual_ ? sub_cur_ : cur_; }
+    void set_par(int p) { (dual_ ? sub_cur_ : cur_) = p; }
 
     // Capture and instantiate the replay graphs at init, so no timed run() ever pays for
     // stream capture or graph instantiation (a 16-superstep capture costs milliseconds: more than
@@ -336,97 +285,103 @@ class HipEngine : public Engine {
     void prewarm_graph() {
         int k = 0, M = 0;
         if (!graph_shape(k, M)) return;
-        for (int m : graph_ladder(k, M)) {
+        for (const Shape& sh : graph_ladder(k, M)) {
             // both parities: a remainder graph of odd pass count leaves the other one current
-            for (int par = 0; par < 2; ++par) {
-                const int cur0 = cur_;
-                cur_ = par;
-                graph_for(k, m);
-                cur_ = cur0;
+            for (int p = 0; p < 2; ++p) {
+                const int p0 = par();
+                set_par(p);
+                graph_for(k, sh.m, sh.rem);
+                set_par(p0);
             }
         }
         mark_ready();
         synchronize();
     }
 
-    // Replays: graphs of m supersteps, then of 4 and 1 for the remainder (eager launches of a
-    // superstep cost ~15 us of GPU idle each; graph replays none), every size captured at init.
+    // Replays, largest shape first (eager launches of a superstep cost ~15 us of GPU idle each;
+    // graph replays none), every shape captured at init; what no shape covers runs eagerly.
     void run_graphed(u64& generations) {
         int k = 0, M = 0;
         if (!graph_shape(k, M)) return;
-        for (int m : graph_ladder(k, M)) {
-            const u64 per = (u64)m * (u64)k;
+        for (const Shape& sh : graph_ladder(k, M)) {
+            const u64 per = (u64)sh.m * (u64)k + (u64)sh.rem;
             while (generations >= per && graph_ok_) {
-                hipGraphExec_t exec = graph_for(k, m);
+                hipGraphExec_t exec = graph_for(k, sh.m, sh.rem);
                 if (!exec) return;
-                replay(exec, k, m);
+                replay(exec, k, sh.m, sh.rem);
                 generations -= per;
             }
         }
     }
 
-    void replay(hipGraphExec_t exec, int k, int m) {
-        const u64 per = (u64)m * (u64)k;
+    void replay(hipGraphExec_t exec, int k, int m, int rem) {
+        const u64 per = (u64)m * (u64)k + (u64)rem;
+        maybe_inject_fault();
         {
-            maybe_inject_fault();
-            {
-                trace::Range r("gol.graph_launch");
-                HIP_CHECK(hipGraphLaunch(exec, s_comp_));
-            }
-            cur_ ^= graph_flip(k, m);
-            // Events recorded during capture are not re-recorded by replays: re-mark them after
-            // the graph so later eager supersteps (and the comm stream) wait for its work.
-            mark_ready();
-            gen_ += per;
-            stats_.generations += per;
-            stats_.supersteps += (u64)m;
-            stats_.graph_launches += 1;
-            progress("graph");
+            trace::Range r("gol.graph_launch");
+            HIP_CHECK(hipGraphLaunch(exec, s_comp_));
         }
+        set_par(par() ^ graph_flip(k, m, rem));
+        // Events recorded during capture are not re-recorded by replays: re-mark them after
+        // the graph so later eager supersteps (and the comm stream) wait for its work.
+        mark_ready();
+        gen_ += per;
+        stats_.generations += per;
+        stats_.supersteps += (u64)m + (rem > 0);
+        stats_.graph_launches += 1;
+        progress("graph");
     }
-    // Buffer-parity flip of m supersteps of k generations (one flip per kernel pass).
-    int graph_flip(int k, int m) { return (int)((pass_depths(k).size() * (size_t)m) & 1); }
+    // Buffer-parity flip of a shape (one flip per kernel pass).
+    int graph_flip(int k, int m, int rem) {
+        size_t n = pass_depths(k).size() * (size_t)m;
+        if (rem) n += pass_depths(rem).size();
+        return (int)(n & 1);
+    }
 
     void run(u64 generations) override {
         Armed armed(wd_.get());
-        if (dual_) {
-            run_dual(generations);
-            return;
+        if (dual_ && !sub_current_) {
+            // canonical board -> sub-tiles (interior rows), unless the sub-tiles already hold the
+            // board (consecutive run() calls keep it in the halves; readers sync it back lazily)
+            for (int s = 0; s < 2; ++s)
+                dual_copy(sub_rows(s, sub_cur_, 0), buf_[cur_] + L_.index(sub_r0_[s], -1), rows_bytes(s, sub_L_[s].h));
+            sub_current_ = true;
         }
         run_graphed(generations);
         Engine::run(generations);
+        if (dual_) canon_stale_ = true;  // copied back by the next reader (sync_canonical)
     }
 
-    // ----- two sub-tiles per rank (GOL_SUBTILES=2, 1-D) -----
+    // ----- two sub-tiles per rank (1-D) -----
     // The tile's rows are split into two halves with their own double buffers and R ghost rows.
     // Per superstep the halves exchange R edge rows by device copies (and the rank's north / south
     // halos go to sub-tile 0 / 1 through the transport, in the same canonical messages as the
     // one-tile engine), then each half runs the superstep's passes on its own stream, planned for
     // the whole GPU.  The two kernels of a pass overlap: while one drains, the other's waves fill
     // the freed SIMD slots (two half-board kernels on two streams: 9.8 vs 11.0 us/gen at 32768^2,
-    // docs/PERFORMANCE.md).  The canonical buffers are copied in at run() entry and back at exit.
-    // Inputs identical on every rank (the decision gates a collective): mode requested, 1-D, the
-    // average strip height, the halo depth and the transport kind.
-    bool dual_preferred() const {
+    // docs/PERFORMANCE.md).  Whether a rank runs one tile or two sub-tiles is decided by
+    // measurement at init (choose_schedule).
+    // Requested (GOL_SUBTILES=2) or auto-wanted: inputs identical on every rank (the mode is a
+    // candidate of the collective schedule timing): mode, layout, average strip height, halo depth,
+    // transport kind.
+    bool dual_wanted() const {
         const bool want = cfg_.subtiles == 2 ||
                           (cfg_.subtiles < 0 && g_.dec.H / std::max(1, g_.dec.Py) >= kSubtileMinRows && L_.R >= 64);
-        return want && g_.dec.Px == 1 && !cfg_.compat && !cfg_.profile && !edge_mode_ && !cfg_.force_split && !wd_ &&
-               L_.aligned() &&
-               (self_y() || device_transport_);
+        return want && !two_d() && !cfg_.compat && !cfg_.profile && !cfg_.force_split && !wd_ && L_.aligned() &&
+               (halo_items(L_.R).empty() || device_transport_) && cfg_.kernel != "lds" && cfg_.kernel != "tile";
     }
-
-    bool dual_eligible() const {
-        const bool want = cfg_.subtiles == 2 || (cfg_.subtiles < 0 && L_.h >= kSubtileMinRows && L_.R >= 64);
-        if (!want || g_.dec.Px != 1 || cfg_.compat || cfg_.profile || edge_mode_ || cfg_.force_split || split_ || wd_ ||
-            kern_[0] != "temporal" || !L_.aligned() || L_.h < 8 * (i64)L_.R)
-            return false;
-        if (!self_y() && !device_transport_) return false;
+    // Rank-local conditions (agreed over the ranks by the caller): a tile tall enough for two
+    // halves, and memory for one more board pair.  (The halves always run the temporal kernel, at
+    // its own pass depth, whatever the one-tile kernel autotune picked.)
+    bool dual_local_ok() const {
+        if (L_.h < 8 * (i64)L_.R) return false;
         size_t fr = 0, tot = 0;
         if (hipMemGetInfo(&fr, &tot) != hipSuccess) return false;
-        return 2 * alloc_bytes_ + ((size_t)1 << 30) < fr;  // sub-tile buffers ~ one more board pair
+        return 2 * alloc_bytes_ + ((size_t)1 << 30) < fr;
     }
 
     void setup_dual() {
+        if (sub_buf_[0][0]) return;
         const i64 h0 = L_.h / 2;
         sub_r0_[0] = 0;
         sub_r0_[1] = h0;
@@ -439,17 +394,33 @@ class HipEngine : public Engine {
                 HIP_CHECK(hipMemsetAsync(sub_buf_[s][i], 0, bytes, s_comp_));
             }
         }
-        HIP_CHECK(hipEventCreateWithFlags(&ev_sub_a_, hipEventDisableTiming));
-        HIP_CHECK(hipEventCreateWithFlags(&ev_sub_b_, hipEventDisableTiming));
+        if (!ev_sub_a_) {
+            HIP_CHECK(hipEventCreateWithFlags(&ev_sub_a_, hipEventDisableTiming));
+            HIP_CHECK(hipEventCreateWithFlags(&ev_sub_b_, hipEventDisableTiming));
+        }
         HIP_CHECK(hipStreamSynchronize(s_comp_));
-        for (int k = 1; k <= L_.R; ++k)
-            if (supported_depth(k) == k) {
-                const std::vector<int>& ps = pass_depths(k);
-                for (size_t j = 0; j < ps.size(); ++j)
-                    for (int s = 0; s < 2; ++s) sub_plan(s, ps[j], ext_after(ps, j));
-                for (int par = 0; par < 2; ++par) dual_copies(k, par);
+    }
+    // Free the sub-tile buffers, plans and copy lists (the measurement chose one tile).
+    void teardown_dual() {
+        synchronize();
+        for (auto& kv : sub_plans_) hipFree(kv.second.d);
+        sub_plans_.clear();
+        for (auto& kv : dual_copies_) hipFree(kv.second.d);
+        dual_copies_.clear();
+        for (auto& sb : sub_buf_)
+            for (u64*& b : sb) {
+                if (b) hipFree(b);
+                b = nullptr;
             }
-        dual_ = true;
+        dual_ = false;
+        sub_current_ = canon_stale_ = false;
+    }
+    // Plans and copy lists of a k-generation sub-tile superstep (built before any capture).
+    void prepare_dual(int k) {
+        const std::vector<int>& ps = pass_depths(k);
+        for (size_t j = 0; j < ps.size(); ++j)
+            for (int s = 0; s < 2; ++s) sub_plan(s, ps[j], ext_after(ps, j));
+        for (int p = 0; p < 2; ++p) dual_copies(k, p);
     }
 
     const DevPlan& sub_plan(int s, int k, i64 e) {
@@ -462,9 +433,8 @@ class HipEngine : public Engine {
         // waves/SIMD each half's plan is sized for: two concurrent halves fill the SIMDs between
         // them, so 2-wave plans (taller segments, less halo) measured best (kbench: 9.85 vs 10.11
         // us/gen at 32768^2); GOL_SUB_OCC overrides (0 = the single-tile tuned occupancy)
-        const int so = (int)env_int("GOL_SUB_OCC", 2);
-        if (so > 0)
-            bpc = std::min<i64>(bpc, so);
+        if (cfg_.sub_occ > 0)
+            bpc = std::min<i64>(bpc, cfg_.sub_occ);
         else if (occ_ > 0)
             bpc = std::min<i64>(bpc, occ_);
         const i64 rows = balanced_rows_per_chunk(rg, L.nw, L.h, k, bpc * kWavesPerBlock * cus_, 2 * (i64)k, true);
@@ -489,32 +459,9 @@ class HipEngine : public Engine {
         HIP_CHECK(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, s_comp_));
     }
 
-    void run_dual(u64 generations) {
-        // canonical board -> sub-tiles (interior rows), unless the sub-tiles already hold the board
-        // (consecutive run() calls keep the board in the halves; readers sync it back lazily)
-        if (!sub_current_)
-            for (int s = 0; s < 2; ++s)
-                dual_copy(sub_rows(s, sub_cur_, 0), buf_[cur_] + L_.index(sub_r0_[s], -1), rows_bytes(s, sub_L_[s].h));
-        sub_current_ = true;
-        while (generations > 0) {
-            maybe_inject_fault();
-            const int k = supported_depth((int)std::min<u64>((u64)L_.R, generations));
-            dual_superstep(k);
-            gen_ += (u64)k;
-            generations -= (u64)k;
-            stats_.generations += (u64)k;
-            stats_.supersteps += 1;
-            progress("superstep");
-        }
-        canon_stale_ = true;  // copied back by the next reader (sync_canonical)
-        maybe_inject_fault();
-    }
-
     // Both halves done -> the canonical buffer (before anything reads it).
     void sync_canonical() {
         if (!canon_stale_) return;
-        HIP_CHECK(hipEventRecord(ev_sub_b_, s_comm_));
-        HIP_CHECK(hipStreamWaitEvent(s_comp_, ev_sub_b_, 0));
         for (int s = 0; s < 2; ++s)
             dual_copy(buf_[cur_] + L_.index(sub_r0_[s], -1), sub_rows(s, sub_cur_, 0), rows_bytes(s, sub_L_[s].h));
         canon_stale_ = false;
@@ -544,13 +491,13 @@ class HipEngine : public Engine {
         return dual_copies_.emplace(key, dc).first->second;
     }
 
+    // One sub-tile superstep.  s_comp holds the joined state of the previous superstep on entry and
+    // on exit (fork after the halo work, join after the last pass), so the body is also a valid
+    // stream capture: the comm stream joins the capture through the fork event.
     void dual_superstep(int k) {
+        prepare_dual(k);
         const int p = sub_cur_;
-        const i64 h0 = sub_L_[0].h, h1 = sub_L_[1].h;
-        // sub-tile 1's previous superstep must be done before its edge rows are read / its ghost
-        // rows are overwritten (the halo work runs on the compute stream)
-        HIP_CHECK(hipEventRecord(ev_sub_b_, s_comm_));
-        HIP_CHECK(hipStreamWaitEvent(s_comp_, ev_sub_b_, 0));
+        const i64 h1 = sub_L_[1].h;
         // internal seam (sub0 bottom edge -> sub1 top ghost, sub1 top edge -> sub0 bottom ghost) and,
         // when the rank is its own N/S neighbour, the torus wrap: one batched copy kernel
         const DualCopies& dc = dual_copies(k, p);
@@ -580,6 +527,8 @@ class HipEngine : public Engine {
             q ^= 1;
         }
         HIP_CHECK(hipGetLastError());
+        HIP_CHECK(hipEventRecord(ev_sub_b_, s_comm_));
+        HIP_CHECK(hipStreamWaitEvent(s_comp_, ev_sub_b_, 0));
         sub_cur_ = q;
     }
 
@@ -588,12 +537,13 @@ class HipEngine : public Engine {
         return plan(0, pass_depths(R)[0], ext_after(pass_depths(R), 0));
     }
 
-    // A rank without neighbours (nothing to exchange) cuts its supersteps at the largest multiple
-    // of the tuned pass depth within R, so none ends with a short pass (8192^2: tile passes of 24
-    // in 32-generation supersteps ran 24 + 8, and an 8-generation tile pass is 27% slower per
+    // A one-tile rank without neighbours (nothing to exchange) cuts its supersteps at the largest
+    // multiple of the tuned pass depth within R, so none ends with a short pass (8192^2: tile passes
+    // of 24 in 32-generation supersteps ran 24 + 8, and an 8-generation tile pass is 27% slower per
     // generation).  With neighbours every rank keeps R: the exchanges must match.
     int superstep_depth() const override {
-        if (!tuned_ || cfg_.compat || kdepth_ <= 0 || kdepth_ >= L_.R || !halo_items(L_.R).empty()) return L_.R;
+        if (dual_ || !tuned_ || cfg_.compat || kdepth_ <= 0 || kdepth_ >= L_.R || !halo_items(L_.R).empty())
+            return L_.R;
         return (L_.R / kdepth_) * kdepth_;
     }
 
@@ -625,44 +575,39 @@ class HipEngine : public Engine {
         mark_ready();
         synchronize();
         if (dcells) deferred_free_.push_back(dcells);  // hipFree may synchronise the whole device
-        split_ = split_used() && (cfg_.sched == "auto" || cfg_.sched == "split");
         if (!tuned_) {
             if (cfg_.kernel == "auto") autotune_kernel();
-            // The two-sub-tile mode runs the full schedule (its halves own the exchange); when it
-            // is wanted, every rank skips the (collective) schedule autotune: the split schedule
-            // hides an exchange of ~2-3% of a 64-generation superstep, the sub-tiles gain ~5%.
-            if (cfg_.sched == "auto" && dual_preferred())
-                split_ = false;
-            else
-                autotune_schedule();
+            choose_schedule();  // collective when ranks have neighbours
             tuned_ = true;
             passes_.clear();  // the pass cuts may depend on the tuned kernel (pass_depths)
-            // keep the collective choice for later init() calls (split_ is recomputed above)
-            if (cfg_.sched == "auto" && split_used()) cfg_.sched = split_ ? "split" : "full";
             // The comm stream waits on the compute stream's ready event only in the split
-            // schedule (and the edge-stream / forced-split measurement modes).  The full schedule
+            // schedule (and the forced-split measurement mode).  The full schedule
             // exchanges on the compute stream itself: recording the event there every superstep
             // only idles the GPU (~15 us per record, a release fence).  GOL_READY_EVENTS=always
             // restores the record (measurement knob).
-            events_needed_ = edge_mode_ || cfg_.force_split || (split_ && !halo_items(L_.R).empty()) ||
+            events_needed_ = cfg_.force_split || (split_ && !halo_items(L_.R).empty()) ||
                              env_str("GOL_READY_EVENTS", "") == "always";
         }
         stats_.kernel = split_ ? kern_[1] + "+boundary:" + kern_[2] : kern_[0];
         stats_.schedule = split_ ? "split" : (halo_items(L_.R).empty() ? "local" : "full");
+        if (dual_) stats_.schedule += "+subtiles2";
         stats_.kernel_depth = kdepth_;
         stats_.tile_waves = cfg_.tile_waves;
         std::string tn;
         for (const auto& kv : tune_ms_) tn += strprintf("%s%s=%.3fus/gen", tn.empty() ? "" : " ", kv.first.c_str(), kv.second * 1e3);
-        if (sched_ms_[0] > 0)
-            tn += strprintf("%ssplit=%.3fms full=%.3fms", tn.empty() ? "" : " ", sched_ms_[0], sched_ms_[1]);
+        for (const auto& kv : sched_us_)
+            tn += strprintf("%ssched:%s=%.3fus/gen", tn.empty() ? "" : " ", kv.first.c_str(), kv.second);
         stats_.tuning = tn;
-        // Build the plans for every depth a run can use (remainder supersteps included) now, so
-        // neither graph capture nor a timed loop ever builds or uploads a plan.
-        for (int k = 1; k <= (cfg_.compat ? 1 : L_.R); ++k)
-            if (supported_depth(k) == k) prepare(k);
-        if (!dual_ && dual_eligible()) setup_dual();
-        if (dual_) stats_.schedule += "+subtiles2";
-        if (!dual_) prewarm_graph();
+        // Build the plans of the supersteps the runs will use now (the full superstep and the
+        // remainder of the hinted run length), so neither graph capture nor a hinted timed loop
+        // builds or uploads a plan.  Other remainders are built on first use.
+        for (int k : init_depths()) {
+            if (dual_)
+                prepare_dual(k);
+            else
+                prepare(k);
+        }
+        prewarm_graph();
         spin_up();  // init ends with the GPU at its steady clock (plan building and captures idle it)
         const DevPlan& fp = full_plan_stats();
         stats_.plan_waves = fp.waves;
@@ -670,7 +615,26 @@ class HipEngine : public Engine {
             fp.st.lane_rows ? (double)fp.st.out_words / (double)fp.st.lane_rows : 0.0;
     }
 
+    // Superstep depths prepared at init: the full superstep, and the hinted run's remainder.
+    std::vector<int> init_depths() const {
+        if (cfg_.compat) return {1};
+        const int R = superstep_depth();
+        std::vector<int> ks = {R};
+        for (u64 n : {cfg_.run_hint}) {
+            const int r = (int)(n % (u64)R);
+            if (r > 0 && std::find(ks.begin(), ks.end(), r) == ks.end()) ks.push_back(r);
+        }
+        return ks;
+    }
+
     void do_superstep(int k) override {
+        if (dual_)
+            dual_superstep(k);
+        else
+            tile_superstep(k);
+    }
+
+    void tile_superstep(int k) {
         const std::vector<int>& ps = pass_depths(k);
         first_pass(k, ps[0], ext_after(ps, 0), split_);
         cur_ ^= 1;
@@ -685,20 +649,36 @@ class HipEngine : public Engine {
         if (ps.size() > 1) mark_ready();  // the next exchange reads what the last pass wrote
     }
 
-    // Kernel passes of a superstep of k generations (each <= the kernel depth), and the rows beyond
-    // the tile each pass must still produce for the passes after it (0 when y wraps locally).
+    // Kernel passes of a superstep of k generations: the fewest passes of at most the kernel depth
+    // K, with depths as equal as possible (20 = 7 + 7 + 6, not 8 + 8 + 4: a shallow pass streams the
+    // board through HBM for few generations and is memory bound, docs/PERFORMANCE.md §6).
     const std::vector<int>& pass_depths(int k) {
-        auto it = passes_.find(k);
+        const int key = k + (dual_ ? (1 << 20) : 0);
+        auto it = passes_.find(key);
         if (it != passes_.end()) return it->second;
+        // every kind may be temporal, unless only the (any-depth) tile kernel runs; sub-tiles always
+        // run the temporal kernel at its own depth
+        const bool any_depth = !dual_ && (cfg_.kernel == "tile" || (tuned_ && !split_ && tile_kernel(0)));
+        auto ok = [&](int d) { return any_depth || hipk::step_depth_supported(d); };
+        const int K = std::max(1, dual_ ? tdepth_ : kdepth_);
         std::vector<int> ps;
-        for (int left = k; left > 0;) {
-            int d = std::min(left, kdepth_);
-            // every kind may be temporal, unless only the (any-depth) tile kernel runs
-            if (cfg_.kernel != "tile" && !(tuned_ && !split_ && tile_kernel(0))) d = supported_kernel_depth(d);
+        const int n = (k + K - 1) / K;
+        bool balanced = true;
+        for (int j = 0; j < n; ++j) {
+            const int d = k / n + (j < k % n ? 1 : 0);
+            if (!ok(d)) balanced = false;
             ps.push_back(d);
-            left -= d;
         }
-        return passes_.emplace(k, ps).first->second;
+        if (!balanced) {  // greedy over the instantiated depths
+            ps.clear();
+            for (int left = k; left > 0;) {
+                int d = std::min(left, K);
+                if (!any_depth) d = supported_kernel_depth(d);
+                ps.push_back(d);
+                left -= d;
+            }
+        }
+        return passes_.emplace(key, ps).first->second;
     }
     // Generations still to run after pass j of a superstep (the "extension" of pass j's output:
     // that many ghost rows when y has neighbours, plus the ghost words when x has neighbours).
@@ -721,22 +701,6 @@ class HipEngine : public Engine {
         u64* dst = buf_[cur_ ^ 1];
         const std::vector<HaloItem>& items = items_for(kx);
         const bool prof = cfg_.profile;
-        if (edge_mode_ && split) {
-            // I(s) interior on the compute stream, H(s) exchange + B(s) boundary on the edge
-            // stream, concurrently.  I(s) needs B(s-1) (its input rows and its output buffer);
-            // B(s) needs H(s) and I(s-1).  The waits are issued before this superstep re-records
-            // the events, so they refer to superstep s-1.  (Single-pass supersteps only.)
-            HIP_CHECK(hipStreamWaitEvent(s_comp_, ev_bnd_, 0));
-            launch(1, kp, 0, src, dst, s_comp_);
-            if (!items.empty()) exchange_device(kx, items, cur_, s_comm_);
-            HIP_CHECK(hipStreamWaitEvent(s_comm_, ev_int_, 0));
-            launch(2, kp, e, src, dst, s_comm_);
-            HIP_CHECK(hipEventRecord(ev_bnd_, s_comm_));
-            HIP_CHECK(hipEventRecord(ev_int_, s_comp_));
-            HIP_CHECK(hipStreamWaitEvent(s_comp_, ev_bnd_, 0));  // join: s_comp holds the whole board
-            HIP_CHECK(hipEventRecord(ev_ready_, s_comp_));
-            return;
-        }
         if (cfg_.compat || (items.empty() && !cfg_.force_split)) {
             if (prof) HIP_CHECK(hipEventRecord(ev_t2_, s_comp_));
             launch(0, kp, e, src, dst, s_comp_);
@@ -816,36 +780,97 @@ class HipEngine : public Engine {
         kern_[0] = saved;
     }
 
-    // With neighbours, pick the superstep schedule by measurement: every rank times a few
-    // supersteps of each schedule on the scratch buffer (the exchange writes the same halo rows a
-    // real superstep would, the kernels write the scratch buffer; parity is not flipped), and the
-    // schedule with the smaller max-over-ranks time wins.  Split overlaps the exchange with the
-    // interior but pays a serial boundary kernel and cross-stream waits; full pays the exchange
-    // latency.  Which is cheaper depends on the tile size and the link latency.
-    static constexpr int kSchedReps = 8;
-    void autotune_schedule() {
-        if (!split_ || halo_items(L_.R).empty() || cfg_.sched != "auto") return;
-        const int k = L_.R;
-        const std::vector<int>& ps = pass_depths(k);
-        const i64 e0 = ext_after(ps, 0);
-        double t[2] = {0, 0};
-        for (int m = 0; m < 2; ++m) {
-            // only the exchange + first pass differ between the schedules; later passes are equal
-            const bool sp = m == 0;
-            first_pass(k, ps[0], e0, sp);  // warm-up: RCCL connections, plans, code objects
-            synchronize();
-            t_->barrier();
-            const auto t0 = std::chrono::steady_clock::now();
-            for (int i = 0; i < kSchedReps; ++i) first_pass(k, ps[0], e0, sp);
-            synchronize();
-            const double dt = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
-            t[m] = t_->allreduce_max(dt);
+    // Pick the superstep schedule by measurement.  Candidates (every rank builds the same list from
+    // rank-invariant inputs, and agrees on the sub-tile mode's rank-local conditions by a reduction,
+    // because the timing is collective):
+    //   local / full  one tile; with neighbours the exchange runs on the compute stream, then one
+    //                 full-region kernel pass (plus the later passes)
+    //   split         one tile; the exchange on the comm stream overlaps the interior kernel, then the
+    //                 boundary bands (needs an interior on every rank)
+    //   subtiles      two half-tiles on two streams (1-D; dual_superstep)
+    // Each candidate runs whole R-generation supersteps on scratch state (one tile: every pass reads
+    // the board and writes the scratch buffer, the exchange writes the ghost rows a real superstep
+    // writes; sub-tiles: their own buffers, loaded from the board at the next run), timed in three
+    // interleaved rounds, best round per candidate, max over ranks.  The smallest time per
+    // generation wins.
+    static constexpr int kSchedReps = 4;
+    void choose_schedule() {
+        const bool nbrs = !halo_items(L_.R).empty();  // identical on every rank (uniform grid)
+        std::vector<std::string> cands;
+        if (cfg_.force_split || (cfg_.sched == "split" && split_used())) {
+            cands = {"split"};
+        } else {
+            cands.push_back(nbrs ? "full" : "local");
+            if (cfg_.sched == "auto" && split_used()) cands.push_back("split");
         }
-        split_ = t[0] <= t[1];
-        sched_ms_[0] = t[0] * 1e3 / kSchedReps;  // ms per (exchange + first pass)
-        sched_ms_[1] = t[1] * 1e3 / kSchedReps;
-        stats_.exchanges = 0;  // the timing exchanges are not part of the run
-        stats_.halo_bytes = 0;
+        bool dual_ok = cfg_.subtiles != 0 && cands[0] != "split" && dual_wanted();
+        if (dual_ok) {
+            double ok = dual_local_ok() ? 1.0 : 0.0;
+            if (t_->size() > 1) ok = t_->allreduce_min(ok);
+            dual_ok = ok > 0;
+        }
+        if (dual_ok) {
+            if (cfg_.subtiles == 2)
+                cands = {"subtiles"};
+            else
+                cands.push_back("subtiles");
+        }
+        std::string pick = cands[0];
+        if (cands.size() > 1) {
+            const int k = L_.R;
+            std::vector<double> best(cands.size(), 1e30);
+            spin_up();
+            for (int round = 0; round < 3; ++round)
+                for (size_t c = 0; c < cands.size(); ++c) {
+                    if (round == 0) time_schedule(cands[c], k, 1);  // warm-up: connections, plans
+                    synchronize();
+                    t_->barrier();
+                    const auto t0 = std::chrono::steady_clock::now();
+                    time_schedule(cands[c], k, kSchedReps);
+                    synchronize();
+                    const double dt = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+                    best[c] = std::min(best[c], t_->allreduce_max(dt) * 1e6 / (kSchedReps * k));
+                }
+            size_t bi = 0;
+            for (size_t c = 0; c < cands.size(); ++c) {
+                sched_us_[cands[c]] = best[c];
+                if (best[c] < best[bi]) bi = c;
+            }
+            pick = cands[bi];
+            stats_.exchanges = 0;  // the timing exchanges are not part of the run
+            stats_.halo_bytes = 0;
+        }
+        split_ = pick == "split";
+        dual_ = pick == "subtiles";
+        if (dual_) {
+            setup_dual();
+            sub_current_ = false;  // the halves hold timing scratch: load the board at the next run
+        } else if (sub_buf_[0][0]) {
+            teardown_dual();
+        }
+        passes_.clear();
+    }
+
+    // `reps` supersteps of k generations of schedule `c` on scratch state (see choose_schedule).
+    void time_schedule(const std::string& c, int k, int reps) {
+        if (c == "subtiles") {
+            setup_dual();
+            dual_ = true;
+            for (int i = 0; i < reps; ++i) dual_superstep(k);
+            dual_ = false;
+            return;
+        }
+        split_ = c == "split";
+        const std::vector<int>& ps = pass_depths(k);
+        for (int i = 0; i < reps; ++i) {
+            first_pass(k, ps[0], ext_after(ps, 0), split_);
+            for (size_t j = 1; j < ps.size(); ++j) {
+                const i64 e = ext_after(ps, j);
+                launch(0, ps[j], e, buf_[cur_], buf_[cur_ ^ 1], s_comp_);
+                post(buf_[cur_ ^ 1], s_comp_, e);
+            }
+        }
+        split_ = false;
     }
 
     void do_set_compat_halos(const std::vector<u64>& above, const std::vector<u64>& below) override {
@@ -886,8 +911,6 @@ class HipEngine : public Engine {
         u32 f = 0;
         if (self_y() && !cfg_.compat) f |= hipk::STEP_WRAP_Y;
         if (xwrap_by_plan()) f |= hipk::STEP_WRAP_X;
-        if (cfg_.prefetch == "lds") f |= hipk::STEP_PF_LDS;
-        if (cfg_.pipeline == "skew") f |= hipk::STEP_SKEW;
         if (tile_l2_) f |= hipk::STEP_TILE_L2;  // tile kernel: 2 generations per LDS pass
         return f;
     }
@@ -902,7 +925,7 @@ class HipEngine : public Engine {
         i64 tiles = 0;
         for (const Region& r : regions(kind, k, e))
             tiles += ceil_div(r.r1 - r.r0, rmax) * ceil_div(r.c1 - r.c0, (i64)kSegWords);
-        return ceil_div(tiles, (i64)plan_cus(kind));
+        return ceil_div(tiles, (i64)cus_);
     }
 
     // Whether supersteps use the interior (kind 1) / boundary (kind 2) split.
@@ -933,7 +956,7 @@ class HipEngine : public Engine {
                 return 0.f;
             }
             const bool tile = kern_[kind] == "tile";
-            hipStream_t s = (kind == 2 && edge_mode_) ? s_comm_ : s_comp_;
+            hipStream_t s = s_comp_;
             launch(kind, k, 0, buf_[cur_], buf_[cur_ ^ 1], s);  // warm-up (and plan build)
             HIP_CHECK(hipEventRecord(e0, s));
             for (int i = 0; i < 3; ++i) launch(kind, k, 0, buf_[cur_], buf_[cur_ ^ 1], s);
@@ -1030,9 +1053,11 @@ class HipEngine : public Engine {
     }
 
     bool can_overlap() const {
-        // interior must exist, and the LDS kernel reads ghost words for every row (2-D needs them)
-        if (L_.h <= 2 * (i64)L_.R) return false;
-        if (kernel_ == "lds" && g_.dec.Px > 1) return false;
+        // an interior must exist on EVERY rank (the schedule timing is collective, so the decision
+        // uses the smallest strip, not this rank's), and the LDS kernel reads ghost words for every
+        // row (2-D needs them)
+        if (min_tile_rows() <= 2 * (i64)L_.R) return false;
+        if (kernel_ == "lds" && two_d()) return false;
         return true;
     }
 
@@ -1040,7 +1065,7 @@ class HipEngine : public Engine {
     // the ghost rows, 1-D multi-pass supersteps): kind 0 full, 1 interior, 2 boundary bands.
     std::vector<Region> regions(int kind, int k, i64 rem = 0) const {
         const i64 h = L_.h, nw = L_.nw;
-        const bool two_d = g_.dec.Px > 1;
+        const bool two_d = this->two_d();
         // multi-pass: earlier passes also produce the ghost rows (y neighbours) and the ghost
         // words, columns -1 and nw (x neighbours), that later passes read
         const i64 e = self_y() ? 0 : rem;
@@ -1081,10 +1106,10 @@ class HipEngine : public Engine {
                                       "kernel for boards this large",
                                       (long long)tile_rounds(kind, k, e)));
             if (rows <= 0) {
-                const i64 r1 = balanced_rows_per_chunk(rg, L_.nw, L_.h, k, plan_cus(kind), 1, xwrap_by_plan());
+                const i64 r1 = balanced_rows_per_chunk(rg, L_.nw, L_.h, k, cus_, 1, xwrap_by_plan());
                 const i64 rounds = ceil_div(r1, rmax);
                 rows = rounds <= 1 ? r1
-                                   : std::min(rmax, balanced_rows_per_chunk(rg, L_.nw, L_.h, k, rounds * plan_cus(kind), 1,
+                                   : std::min(rmax, balanced_rows_per_chunk(rg, L_.nw, L_.h, k, rounds * cus_, 1,
                                                                             xwrap_by_plan()));
             }
         } else {
@@ -1094,7 +1119,7 @@ class HipEngine : public Engine {
                 // one full round of resident waves (occupancy of this kernel instantiation)
                 i64 bpc = hipk::step_blocks_per_cu(k, step_flags());
                 if (occ_ > 0) bpc = std::min<i64>(bpc, occ_);  // 256-thread blocks per CU = waves per SIMD
-                const i64 resident = bpc * kWavesPerBlock * plan_cus(kind);
+                const i64 resident = bpc * kWavesPerBlock * cus_;
                 rows = balanced_rows_per_chunk(rg, L_.nw, L_.h, k, resident, 2 * (i64)k, xwrap_by_plan());
             }
         }
@@ -1263,20 +1288,28 @@ class HipEngine : public Engine {
     }
 
     // ----- graphs -----
-    hipGraphExec_t graph_for(int k, int m) {
-        // the captured kernels bake in the buffer pointers, so a replay must start at the parity
-        // it was captured at (an odd-pass remainder superstep flips it between run() calls)
-        const int key = (k * 1000 + m) * 2 + cur_;
+    // The captured kernels bake in the buffer pointers, so a replay must start at the parity it was
+    // captured at (an odd-pass remainder superstep flips it between run() calls).
+    i64 graph_key(int k, int m, int rem) const { return (((i64)k * 1000 + m) * 1000 + rem) * 2 + par(); }
+    hipGraphExec_t graph_for(int k, int m, int rem) {
+        const i64 key = graph_key(k, m, rem);
         auto it = graphs_.find(key);
         if (it != graphs_.end()) return it->second;
-        prepare(k);
+        for (int kk : {k, rem}) {
+            if (kk <= 0) continue;
+            if (dual_)
+                prepare_dual(kk);
+            else
+                prepare(kk);
+        }
         hipGraph_t graph = nullptr;
         hipGraphExec_t exec = nullptr;
-        const int cur0 = cur_;
+        const int p0 = par();
         try {
             HIP_CHECK(hipStreamBeginCapture(s_comp_, hipStreamCaptureModeRelaxed));
             mark_ready();  // fork points for the comm stream, recorded inside the capture
             for (int i = 0; i < m; ++i) do_superstep(k);
+            if (rem) do_superstep(rem);
             HIP_CHECK(hipStreamEndCapture(s_comp_, &graph));
             HIP_CHECK(hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0));
             HIP_CHECK(hipGraphDestroy(graph));
@@ -1285,13 +1318,13 @@ class HipEngine : public Engine {
             hipStreamEndCapture(s_comp_, &g2);
             if (g2) hipGraphDestroy(g2);
             hipGetLastError();
-            cur_ = cur0;
+            set_par(p0);
             graph_ok_ = false;
             fprintf(stderr, "[gol] hipGraph capture disabled: %s\n", e.what());
             mark_ready();
             return nullptr;
         }
-        cur_ = cur0;  // capture does not execute: the replay flips the parity (graph_flip)
+        set_par(p0);  // capture does not execute: the replay flips the parity (graph_flip)
         graphs_[key] = exec;
         return exec;
     }
@@ -1322,13 +1355,10 @@ class HipEngine : public Engine {
     }
 
     int dev_ = 0, cus_ = 256;
-    bool edge_mode_ = false;       // exchange + boundary on the (CU-partitioned) edge stream
-    int comp_cus_ = 256, edge_cus_ = 0;
-    hipEvent_t ev_int_ = nullptr;  // interior of the last superstep done (compute stream)
-    hipEvent_t ev_bnd_ = nullptr;  // boundary of the last superstep done (edge stream)
     std::string kernel_;  // resolved kernel: temporal | tile | lds (auto resolves at init)
     std::string kern_[3];  // per plan kind (full / interior / boundary), resolved by autotune
     int kdepth_ = 8;       // kernel pass depth K (<= halo depth R)
+    int tdepth_ = 8;       // temporal-kernel pass depth (the sub-tile mode's, whatever kernel one tile uses)
     // temporal-kernel plans: waves per SIMD the one-round plan is sized for (0: the kernel's full
     // occupancy).  Small tiles pay (K+1)/S of vertical halo with S rows per wave, so fewer, taller
     // waves can win there; the autotuner tries 2 per SIMD against the full occupancy (3 at K=8).
@@ -1337,7 +1367,7 @@ class HipEngine : public Engine {
     bool multipass_ = false;
     std::map<int, std::vector<int>> passes_;
     bool split_ = false;   // superstep schedule: interior/boundary split with overlapped exchange
-    double sched_ms_[2] = {0, 0};
+    std::map<std::string, double> sched_us_;  // choose_schedule: us per generation per candidate
     bool tuned_ = false;
     std::map<std::string, float> tune_ms_;
     hipEvent_t fence_ev_[kFenceDepth] = {};
@@ -1354,7 +1384,7 @@ class HipEngine : public Engine {
     u64* h_red_ = nullptr;
     bool device_transport_ = false;
     bool graph_ok_ = true;
-    bool events_needed_ = true;  // another stream waits on ev_ready_ / ev_int_ / ev_bnd_
+    bool events_needed_ = true;  // another stream waits on ev_ready_
     std::vector<void*> deferred_free_;
     std::map<int, DevPlan> plans_;
     // GOL_SUBTILES=2 state
@@ -1370,7 +1400,7 @@ class HipEngine : public Engine {
     hipEvent_t ev_sub_a_ = nullptr, ev_sub_b_ = nullptr;
     std::map<int, DevCopies> copies_;
     std::map<int, std::vector<HaloItem>> items_;
-    std::map<int, hipGraphExec_t> graphs_;
+    std::map<i64, hipGraphExec_t> graphs_;
     std::vector<u64*> dstage_s_, dstage_r_, hstage_s_, hstage_r_;
 };
 

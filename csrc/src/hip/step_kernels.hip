@@ -66,13 +66,7 @@ __device__ __forceinline__ u32 rule32(u32 a0, u32 a1, u32 b0, u32 b1, u32 c0, u3
 // odd cell j (hi).  Odd cell j: left = even cell j (lo), right = even cell j+1 (lo shifted down one,
 // bit 31 from the next lane's lo).  2 DPP + 2 funnel shifts + 4 bitop3 per 64 cells.
 __device__ __forceinline__ void hsum_split(u32 lo, u32 hi, u32& s0lo, u32& s1lo, u32& s0hi, u32& s1hi) {
-#ifdef GOL_HSUM_BPERM
-    const int lane = (int)__lane_id();
-    const u32 ph = (u32)__builtin_amdgcn_ds_bpermute(((lane - 1) & 63) << 2, (int)hi);
-    const u32 nl = (u32)__builtin_amdgcn_ds_bpermute(((lane + 1) & 63) << 2, (int)lo);
-#else
     const u32 ph = dpp_prev(hi), nl = dpp_next(lo);
-#endif
     const u32 Le = __builtin_amdgcn_alignbit(hi, ph, 31);  // (hi << 1) | (ph >> 31)
     const u32 Ro = __builtin_amdgcn_alignbit(nl, lo, 1);   // (lo >> 1) | (nl << 31)
     s0lo = b3<kLutXor3>(Le, lo, hi);
@@ -111,75 +105,21 @@ __device__ __forceinline__ bool advance(Pipe<K>& P, u32& lo, u32& hi, int i) {
     return true;
 }
 
-// Skewed pipeline: level l consumes the row level l-1 produced in the PREVIOUS iteration (held in
-// dl/dh), so the K levels of one iteration are independent dependency chains the scheduler can
-// interleave (K-way ILP instead of one K-deep chain of DPP -> alignbit -> bitop3 steps).  Level l
-// receives input index i-2l at iteration i and emits index i-2l-1; the last level emits index
-// i-2K+1, i.e. the pipeline is K-1 rows longer than the unskewed one.  Garbage entering a level
-// before its first valid row only reaches output indices outside the valid range, so no guards
-// are needed — the caller just does not store the first 3K-1 outputs.
-template <int K>
-struct SkewPipe : Pipe<K> {
-    u32 dl[K], dh[K];  // dl[l], dh[l]: input of level l (l >= 1) for the current iteration
-};
-
-template <int K, int PH>
-__device__ __forceinline__ void advance_skew(SkewPipe<K>& P, u32& lo, u32& hi) {
-    constexpr int s = PH, sp = (PH + 2) % 3, spp = (PH + 1) % 3;
-    u32 out_lo = 0, out_hi = 0;
-#pragma unroll
-    for (int l = K - 1; l >= 0; --l) {
-        const u32 a = l ? P.dl[l] : lo, b = l ? P.dh[l] : hi;
-        hsum_split(a, b, P.s0[l][s][0], P.s1[l][s][0], P.s0[l][s][1], P.s1[l][s][1]);
-        P.x[l][s][0] = a;
-        P.x[l][s][1] = b;
-        const u32 o_lo = rule32(P.s0[l][spp][0], P.s1[l][spp][0], P.s0[l][sp][0], P.s1[l][sp][0], P.s0[l][s][0],
-                                P.s1[l][s][0], P.x[l][sp][0]);
-        const u32 o_hi = rule32(P.s0[l][spp][1], P.s1[l][spp][1], P.s0[l][sp][1], P.s1[l][sp][1], P.s0[l][s][1],
-                                P.s1[l][s][1], P.x[l][sp][1]);
-        if (l == K - 1) {
-            out_lo = o_lo;
-            out_hi = o_hi;
-        } else {
-            P.dl[l + 1] = o_lo;
-            P.dh[l + 1] = o_hi;
-        }
-    }
-    lo = out_lo;
-    hi = out_hi;
-}
-
-typedef __attribute__((address_space(3))) void lds_void_t;
-typedef __attribute__((address_space(1))) void glb_void_t;
-
-// Row prefetch.  PF_LDS: each wave owns a ring of kRingRows rows in LDS, filled by
-// global_load_lds_dword DMA (2 per row: lo / hi halves) kRingRows-1 rows ahead of use — deep
-// prefetch that costs no VGPRs.  The ring row for iteration i was issued at iteration i-kRingRows+1;
-// at least 2*kRingRows-4 vector-memory ops (DMAs, stores) were issued after it, so a counted
-// `s_waitcnt vmcnt(2*kRingRows-4)` retires it while the newer rows stay in flight.
-// PF_REG: a register triple prefetched one row-triple ahead, pinned above the compute with a
-// sched_barrier (otherwise the scheduler sinks the loads to the end of the loop body).
-enum { PF_REG = 0, PF_LDS = 1 };
-constexpr int kRingWait = 2 * kRingRows - 4;
-
-template <int K, bool WRAPY, int MODE>
+// Row prefetch: a register triple loaded one row-triple ahead, pinned above the compute with a
+// sched_barrier (otherwise the scheduler sinks the loads to the end of the loop body).  (An LDS
+// DMA ring and a skewed level pipeline were built and measured slower; docs/PERFORMANCE.md §2.)
+template <int K, bool WRAPY>
 struct WaveRunner {
-    static constexpr int PF = MODE & 1;                // PF_REG | PF_LDS
-    static constexpr bool SKEW = (MODE & 2) != 0;     // skewed (ILP) level pipeline
     const StepParams& p;
     const LaneDesc& d;
-    const int n;   // row iterations: nrows + 2K (+ K-1 flush rows when skewed)
+    const int n;   // row iterations: nrows + 2K
     const i64 hp;  // h * pitch
     const uint2* ld;
     uint2* st;
     i64 st_stride;  // pitch for output lanes, 0 for halo/idle lanes (they write a trash slot)
     int lrow;       // tile row of the next load (WRAPY only)
-    uint2 pf[3];    // PF_REG
-    u32* ring;      // PF_LDS: kRingRows x {lo, hi} x 64 lanes
-    int slot;       // PF_LDS: ring slot of the next row to consume
-    int fill;       // PF_LDS: ring slot the next DMA writes
-    int lane;
-    std::conditional_t<SKEW, SkewPipe<K>, Pipe<K>> P;
+    uint2 pf[3];
+    Pipe<K> P;
 
     __device__ __forceinline__ void next_row() {
         ld += p.pitch;
@@ -191,19 +131,8 @@ struct WaveRunner {
         }
     }
 
-    __device__ __forceinline__ void issue_dma() {
-        const u32* g = reinterpret_cast<const u32*>(ld);
-        u32* dst = ring + fill * 128;
-        __builtin_amdgcn_global_load_lds((glb_void_t*)g, (lds_void_t*)dst, 4, 0, 0);
-        __builtin_amdgcn_global_load_lds((glb_void_t*)(g + 1), (lds_void_t*)(dst + 64), 4, 0, 0);
-        fill = fill + 1 == kRingRows ? 0 : fill + 1;
-        next_row();
-    }
-
-    __device__ __forceinline__ WaveRunner(const u64* src, u64* dst, const LaneDesc& d_, int nrows,
-                                          const StepParams& p_, u32* ring_)
-        : p(p_), d(d_), n(nrows + (SKEW ? 3 * K - 1 : 2 * K)), hp((i64)p_.h * p_.pitch), ring(ring_), slot(0), fill(0) {
-        lane = threadIdx.x & 63;
+    __device__ __forceinline__ WaveRunner(const u64* src, u64* dst, const LaneDesc& d_, int nrows, const StepParams& p_)
+        : p(p_), d(d_), n(nrows + 2 * K), hp((i64)p_.h * p_.pitch) {
         lrow = d.row0 - K;
         if (WRAPY && lrow < 0) lrow += p.h;
         ld = reinterpret_cast<const uint2*>(src + (i64)(lrow + p.R) * p.pitch + (d.col + 1));
@@ -214,45 +143,27 @@ struct WaveRunner {
         const i64 srow = out ? (i64)(d.row0 + p.R) : (i64)(p.h + 2 * p.R + kSlackRows - 1);
         st = reinterpret_cast<uint2*>(dst + srow * p.pitch + (d.col + 1));
         st_stride = out ? p.pitch : 0;
-        if (PF == PF_LDS) {
-            for (int j = 0; j < kRingRows - 1; ++j) issue_dma();
-        } else {
-            pf[0] = *ld;
-            next_row();
-            pf[1] = *ld;
-            next_row();
-            pf[2] = *ld;
-            next_row();
-        }
+        pf[0] = *ld;
+        next_row();
+        pf[1] = *ld;
+        next_row();
+        pf[2] = *ld;
+        next_row();
     }
 
     // Next input row (lo, hi) in order.
     template <int PH>
     __device__ __forceinline__ void fetch(u32& lo, u32& hi) {
-        if (PF == PF_LDS) {
-            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kRingWait) : "memory");
-            const u32* r = ring + slot * 128;
-            lo = r[lane];
-            hi = r[64 + lane];
-            slot = slot + 1 == kRingRows ? 0 : slot + 1;
-            issue_dma();  // refills the slot consumed by the previous row
-        } else {
-            const uint2 x = pf[PH];
-            pf[PH] = *ld;  // prefetch 3 rows ahead (the allocation has slack rows past the halo)
-            next_row();
-            lo = x.x;
-            hi = x.y;
-        }
+        const uint2 x = pf[PH];
+        pf[PH] = *ld;  // prefetch 3 rows ahead (the allocation has slack rows past the halo)
+        next_row();
+        lo = x.x;
+        hi = x.y;
     }
 
     template <int PH, bool GUARD>
     __device__ __forceinline__ void compute_store(u32 lo, u32 hi, int i) {
-        if constexpr (SKEW) {
-            advance_skew<K, PH>(P, lo, hi);
-            if (GUARD && i < 3 * K - 1) return;  // outputs before the first valid row
-        } else {
-            if (!advance<K, PH, GUARD>(P, lo, hi, i)) return;
-        }
+        if (!advance<K, PH, GUARD>(P, lo, hi, i)) return;
         *st = make_uint2(lo, hi);
         st += st_stride;
     }
@@ -266,8 +177,7 @@ struct WaveRunner {
     }
 
     __device__ __forceinline__ void run() {
-        // first multiple of 3 at which the pipeline is full (2K rows; 3K-1 when skewed)
-        constexpr int i0 = SKEW ? 3 * K : ((2 * K + 2) / 3) * 3;
+        constexpr int i0 = ((2 * K + 2) / 3) * 3;  // first multiple of 3 at which the pipeline is full
         int i = 0;
         for (; i < i0; i += 3) {
             body<0, true>(i);
@@ -275,32 +185,24 @@ struct WaveRunner {
             body<2, true>(i + 2);
         }
         for (; i + 3 <= n; i += 3) {
-            if (PF == PF_REG) {
-                // hoist the whole next triple's loads above this triple's compute
-                const uint2 x0 = pf[0], x1 = pf[1], x2 = pf[2];
-                pf[0] = *ld;
-                next_row();
-                pf[1] = *ld;
-                next_row();
-                pf[2] = *ld;
-                next_row();
-                __builtin_amdgcn_sched_barrier(0);
-                compute_store<0, false>(x0.x, x0.y, i);
-                compute_store<1, false>(x1.x, x1.y, i + 1);
-                compute_store<2, false>(x2.x, x2.y, i + 2);
-            } else {
-                body<0, false>(i);
-                body<1, false>(i + 1);
-                body<2, false>(i + 2);
-            }
+            // hoist the whole next triple's loads above this triple's compute
+            const uint2 x0 = pf[0], x1 = pf[1], x2 = pf[2];
+            pf[0] = *ld;
+            next_row();
+            pf[1] = *ld;
+            next_row();
+            pf[2] = *ld;
+            next_row();
+            __builtin_amdgcn_sched_barrier(0);
+            compute_store<0, false>(x0.x, x0.y, i);
+            compute_store<1, false>(x1.x, x1.y, i + 1);
+            compute_store<2, false>(x2.x, x2.y, i + 2);
         }
         if (i < n) body<0, false>(i);
         if (i + 1 < n) body<1, false>(i + 1);
-        if (PF == PF_LDS) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // drain DMAs before exit
     }
 };
 
-// MODE bit 0: PF_LDS prefetch ring; bit 1: skewed level pipeline.
 // GOL_TEMPORAL_WAVES_PER_EU (build-time experiment knob): minimum waves per SIMD the register
 // allocator must fit (e.g. 4 caps K=8 at 128 VGPRs instead of its natural 163).
 #ifdef GOL_TEMPORAL_WAVES_PER_EU
@@ -308,44 +210,26 @@ struct WaveRunner {
 #else
 #define GOL_TEMPORAL_OCC
 #endif
-template <int K, bool WRAPY, int MODE>
+template <int K, bool WRAPY>
 __global__ __launch_bounds__(256) GOL_TEMPORAL_OCC void step_temporal(const u64* __restrict__ src, u64* __restrict__ dst,
-                                                     const LaneDesc* __restrict__ plan, StepParams p) {
+                                                                      const LaneDesc* __restrict__ plan, StepParams p) {
     const int wv = threadIdx.x >> 6;
     const i64 wave = (i64)blockIdx.x * kWavesPerBlock + wv;
     const int lane = threadIdx.x & 63;
     const LaneDesc d = plan[wave * kWaveLanes + lane];
     const int nrows = __builtin_amdgcn_readfirstlane(d.nrows);
     if (nrows <= 0) return;  // padding wave (uniform)
-    if constexpr ((MODE & 1) == PF_LDS) {
-        __shared__ __attribute__((aligned(16))) u32 ring[kWavesPerBlock * kRingRows * 128];
-        WaveRunner<K, WRAPY, MODE> w(src, dst, d, nrows, p, ring + wv * kRingRows * 128);
-        w.run();
-    } else {
-        WaveRunner<K, WRAPY, MODE> w(src, dst, d, nrows, p, nullptr);
-        w.run();
-    }
-}
-
-template <int K, bool WRAPY>
-const void* kernel_ptr(int mode) {
-    switch (mode & 3) {
-        case 0:
-            return (const void*)step_temporal<K, WRAPY, 0>;
-        case 1:
-            return (const void*)step_temporal<K, WRAPY, 1>;
-        case 2:
-            return (const void*)step_temporal<K, WRAPY, 2>;
-        default:
-            return (const void*)step_temporal<K, WRAPY, 3>;
-    }
+    WaveRunner<K, WRAPY> w(src, dst, d, nrows, p);
+    w.run();
 }
 
 template <int K>
 const void* kernel_for(u32 flags) {
-    const int mode = ((flags & STEP_PF_LDS) ? 1 : 0) | ((flags & STEP_SKEW) ? 2 : 0);
-    return (flags & STEP_WRAP_Y) ? kernel_ptr<K, true>(mode) : kernel_ptr<K, false>(mode);
+    return (flags & STEP_WRAP_Y) ? (const void*)step_temporal<K, true> : (const void*)step_temporal<K, false>;
 }
+
+typedef __attribute__((address_space(3))) void lds_void_t;
+typedef __attribute__((address_space(1))) void glb_void_t;
 
 // ------------------------------------------------------------------------------------------
 // step_tile: LDS-resident temporal blocking.  One workgroup of NW waves per plan wave: the plan
@@ -554,7 +438,7 @@ __global__ __launch_bounds__(256) void step_lds(const u64* __restrict__ src, u64
 
 // Instantiated depths.  Larger K amortises HBM traffic over more generations at the cost of
 // registers (10 VGPRs per level per lane) and 2K halo rows per segment.
-#define GOL_FOR_EACH_DEPTH(X) X(1) X(2) X(3) X(4) X(6) X(8) X(12) X(16)
+#define GOL_FOR_EACH_DEPTH(X) X(1) X(2) X(3) X(4) X(5) X(6) X(7) X(8) X(12) X(16)
 
 bool step_depth_supported(int k) {
     switch (k) {

@@ -168,14 +168,13 @@ EngineConfig engine_config(const Options& o, const std::string& backend, int dev
     c.kernel = env_str("GOL_KERNEL", "auto");
     c.tile_waves = (int)env_int("GOL_TILE_WAVES", 8);
     c.tune_tile_waves = getenv("GOL_TILE_WAVES") == nullptr;
-    c.prefetch = env_str("GOL_PREFETCH", "reg");
-    c.pipeline = env_str("GOL_PIPELINE", "chain");
     c.transport = (o.transport == "rccl" || o.transport == "p2p") ? "device" : o.transport;
     c.profile = o.profile;
     c.graph_supersteps = (int)env_int("GOL_GRAPH_SUPERSTEPS", 0);
     c.subtiles = env_str("GOL_SUBTILES", "auto") == "auto" ? -1 : (int)env_int("GOL_SUBTILES", 0);
     c.watchdog_s = o.watchdog_s;
-    c.edge_cus = (int)env_int("GOL_EDGE_CUS", 0);
+    c.sub_occ = (int)env_int("GOL_SUB_OCC", 2);
+    c.self_exchange = env_int("GOL_SELF_EXCHANGE", 0) != 0;
     c.force_split = env_int("GOL_FORCE_SPLIT", 0) != 0;
     c.graph_rccl = env_int("GOL_GRAPH_RCCL", 0) != 0;
     c.plan_xcds = (int)env_int("GOL_PLAN_XCDS", 8);

@@ -81,17 +81,16 @@ class Simulation:
         compat: bool = False,
         device: Optional[int] = None,
         kernel: str = os.environ.get("GOL_KERNEL", "auto"),
-        prefetch: str = os.environ.get("GOL_PREFETCH", "reg"),
-        pipeline: str = os.environ.get("GOL_PIPELINE", "chain"),
         rows_per_wave: int = 0,
         waves_target: int = 0,
         profile: bool = False,
         watchdog: float = float(os.environ.get("GOL_WATCHDOG", "0")),
         tile_waves: int = int(os.environ.get("GOL_TILE_WAVES", "8")),
-        edge_cus: int = int(os.environ.get("GOL_EDGE_CUS", "0")),
         force_split: bool = os.environ.get("GOL_FORCE_SPLIT", "0") == "1",
         schedule: str = os.environ.get("GOL_SCHEDULE", "auto"),
         run_hint: int = 0,
+        sub_occ: int = int(os.environ.get("GOL_SUB_OCC", "2")),
+        self_exchange: bool = os.environ.get("GOL_SELF_EXCHANGE", "0") == "1",
         subtiles: int = -1 if os.environ.get("GOL_SUBTILES", "auto") == "auto" else int(os.environ["GOL_SUBTILES"]),
     ):
         self.transport = transport if transport is not None else _gol.SelfTransport()
@@ -107,8 +106,6 @@ class Simulation:
         cfg.graph = graph
         cfg.compat = compat
         cfg.kernel = kernel
-        cfg.prefetch = prefetch
-        cfg.pipeline = pipeline
         cfg.subtiles = int(subtiles)  # 2 / 0 / -1 auto: two sub-tiles per rank on two streams (HIP, 1-D)
         cfg.run_hint = int(run_hint)  # generations of the runs to come: one replay graph covers them
         cfg.rows_per_wave = rows_per_wave
@@ -117,7 +114,8 @@ class Simulation:
         cfg.watchdog_s = float(watchdog)
         cfg.tile_waves = int(tile_waves)
         cfg.tune_tile_waves = "GOL_TILE_WAVES" not in os.environ
-        cfg.edge_cus = int(edge_cus)
+        cfg.sub_occ = int(sub_occ)
+        cfg.self_exchange = bool(self_exchange)
         cfg.force_split = bool(force_split)
         cfg.sched = schedule
         cfg.graph_rccl = os.environ.get("GOL_GRAPH_RCCL", "0") == "1"

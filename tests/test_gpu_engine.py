@@ -26,7 +26,7 @@ def test_random_board_vs_numpy(gol, N):
     assert np.array_equal(s.board(), ref)
 
 
-@pytest.mark.parametrize("depth", [1, 2, 3, 4, 6, 8, 12, 16])
+@pytest.mark.parametrize("depth", [1, 2, 3, 4, 5, 6, 7, 8, 12, 16])
 def test_every_depth(gol, depth):
     N, gens = 192, 37
     s = _sim(gol, N, halo_depth=depth, kernel_depth=depth, kernel="temporal").init(5, seed=3)
@@ -126,6 +126,21 @@ def test_run_hint_single_graph(gol):
     assert np.array_equal(s.board(), numpy_step(initial_board(5, N, 1, True, 13), total))
 
 
+@pytest.mark.parametrize("subtiles", [0, 2])
+def test_run_hint_short_run(gol, subtiles):
+    """A hinted run shorter than one superstep (the driver's bench: 20 generations, R = 64) is ONE
+    graph replay of its balanced passes (7 + 7 + 6), in the one-tile and the sub-tile mode."""
+    N, hint = 1024, 20
+    s = _sim(gol, N, halo_depth=64, kernel="temporal", run_hint=hint, subtiles=subtiles).init(5, seed=23)
+    assert s.stats()["schedule"].endswith("+subtiles2") == (subtiles == 2), s.stats()
+    s.step(5)  # unhinted: eager
+    g0 = s.stats()["graph_launches"]
+    s.step(hint)
+    assert s.stats()["graph_launches"] - g0 == 1, s.stats()
+    s.step(hint)
+    assert np.array_equal(s.board(), numpy_step(initial_board(5, N, 1, True, 23), 5 + 2 * hint))
+
+
 @pytest.mark.parametrize("R,K", [(16, 8), (8, 8), (24, 8)])
 def test_graph_replay_after_parity_flip(gol, R, K):
     """Replays are keyed by buffer parity and track it: graphs of 16, 4 and 1 supersteps (1 or 3
@@ -182,13 +197,12 @@ def test_naive_yardstick(gol):
     assert pop == int(numpy_step(random_board(256, 256, 0x5EED), 10).sum())
 
 
-@pytest.mark.parametrize("pipeline", ["skew", "chain"])
-@pytest.mark.parametrize("prefetch", ["lds", "reg"])
-@pytest.mark.parametrize("depth", [1, 3, 8, 16])
-def test_kernel_variants(gol, pipeline, prefetch, depth):
-    N, gens = 700, 3 * depth + 5
-    s = _sim(gol, N, halo_depth=depth, kernel_depth=depth, kernel="temporal", pipeline=pipeline,
-             prefetch=prefetch).init(5, seed=depth)
+@pytest.mark.parametrize("depth", [1, 3, 5, 7, 8, 16])
+def test_kernel_depth_passes(gol, depth):
+    """Every instantiated temporal depth as the pass depth, with multi-pass supersteps of 2*depth+1
+    generations (balanced pass cuts) and an odd remainder."""
+    N, gens = 700, 7 * depth + 5
+    s = _sim(gol, N, halo_depth=min(64, 2 * depth + 1), kernel_depth=depth, kernel="temporal").init(5, seed=depth)
     s.step(gens)
     assert np.array_equal(s.board(), numpy_step(initial_board(5, N, 1, True, depth), gens))
 
@@ -254,12 +268,11 @@ def test_auto_single_rank_depth_32(gol, N):
 
 @pytest.mark.parametrize("kernel", ["temporal", "tile"])
 @pytest.mark.parametrize("graph", [True, False])
-@pytest.mark.parametrize("edge_cus", [8, 0])
-def test_edge_stream_schedule(gol, kernel, graph, edge_cus):
-    """Interior on the compute stream + boundary bands on the CU-partitioned edge stream
-    (the multi-GPU schedule, forced on one rank) is exact."""
+def test_forced_split_schedule(gol, kernel, graph):
+    """Interior on the compute stream + boundary bands after the (empty) comm-stream exchange
+    (the multi-GPU split schedule, forced on one rank) is exact."""
     N, gens = 1024, 8 * 36 + 5
-    s = _sim(gol, N, halo_depth=8, kernel=kernel, graph=graph, edge_cus=edge_cus, force_split=True)
+    s = _sim(gol, N, halo_depth=8, kernel=kernel, graph=graph, force_split=True)
     s.init(5, seed=31)
     s.step(gens)
     assert np.array_equal(s.board(), numpy_step(initial_board(5, N, 1, True, 31), gens))

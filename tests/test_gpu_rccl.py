@@ -1,0 +1,87 @@
+"""Real RCCL data plane on one GPU: a 1-rank communicator with the engine's self-exchange mode.
+
+Every direction whose neighbour is the rank itself is sent with ncclSend to rank 0 and received
+with ncclRecv from rank 0 inside one ncclGroupStart/End per superstep, on the engine's streams —
+the exact calls a multi-GPU job makes (rccl_transport.cpp), replacing the reference's per-generation
+MPI_Irecv/Isend/Wait of one byte row (gol-main.c:97-111).  Each schedule (one tile full / split,
+two sub-tiles, 2-D packed halos with corners, RCCL captured in hipGraphs) is checked bit for bit
+against the numpy torus oracle.
+"""
+import numpy as np
+import pytest
+
+from gol_amd.ops import initial_board, numpy_step
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def rccl(gol):
+    """One 1-rank RCCL communicator shared by the module (communicator init costs seconds)."""
+    gol.native.hip_set_device(0)
+    t = gol.native.make_rccl_transport(gol.native.SelfTransport())
+    assert t.size() == 1 and t.device_buffers() and t.name().startswith("rccl")
+    yield t
+
+
+def _run(gol, rccl, N, gens, seed, **kw):
+    kw.setdefault("backend", "hip")
+    kw.setdefault("device", 0)
+    s = gol.Simulation(N, rccl, self_exchange=True, **kw).init(5, seed=seed)
+    s.step(gens)
+    st = s.stats()
+    got = s.board()
+    s.synchronize()
+    return got, st
+
+
+@pytest.mark.parametrize("schedule", ["full", "split"])
+@pytest.mark.parametrize("R", [8, 32])
+def test_rccl_self_1d(gol, rccl, schedule, R):
+    N, gens = 1024, 3 * R + 5
+    got, st = _run(gol, rccl, N, gens, R, halo_depth=R, schedule=schedule, subtiles=0)
+    assert st["schedule"] == schedule and st["exchanges"] >= 3, st
+    assert st["halo_bytes"] > 0
+    assert np.array_equal(got, numpy_step(initial_board(5, N, 1, True, R), gens))
+
+
+def test_rccl_self_auto_schedule(gol, rccl):
+    """The collective schedule timing (barrier + max over ranks) also runs on a 1-rank communicator."""
+    N, gens = 2048, 70
+    got, st = _run(gol, rccl, N, gens, 5, halo_depth=32, subtiles=0)
+    assert st["schedule"] in ("full", "split"), st
+    assert "sched:" in st["tuning"], st
+    assert np.array_equal(got, numpy_step(initial_board(5, N, 1, True, 5), gens))
+
+
+@pytest.mark.parametrize("graph_rccl", [False, True])
+def test_rccl_self_subtiles(gol, rccl, graph_rccl, monkeypatch):
+    """Two sub-tiles per rank: the rank's north / south halos go through RCCL straight into the halves."""
+    monkeypatch.setenv("GOL_GRAPH_RCCL", "1" if graph_rccl else "0")
+    N, gens = 1024, 2 * 32 + 20
+    got, st = _run(gol, rccl, N, gens, 9, halo_depth=32, subtiles=2, run_hint=gens)
+    assert st["schedule"].endswith("+subtiles2"), st
+    if graph_rccl:
+        assert st["graph_launches"] >= 1, st
+    assert np.array_equal(got, numpy_step(initial_board(5, N, 1, True, 9), gens))
+
+
+@pytest.mark.parametrize("kernel", ["temporal", "tile"])
+@pytest.mark.parametrize("R", [5, 16])
+def test_rccl_self_2d(gol, rccl, kernel, R):
+    """2-D halo layout on one rank: 8 packed messages (N, S, W, E + corners) per superstep,
+    pack/unpack kernels around the RCCL group."""
+    N, gens = 640, 3 * R + 2
+    got, st = _run(gol, rccl, N, gens, R, halo_depth=R, decomp="2d", kernel=kernel)
+    assert st["exchanges"] >= 3, st
+    assert np.array_equal(got, numpy_step(initial_board(5, N, 1, True, R), gens))
+
+
+@pytest.mark.parametrize("decomp", ["1d", "2d"])
+def test_rccl_self_graph_capture(gol, rccl, decomp, monkeypatch):
+    """RCCL groups captured into hipGraphs (GOL_GRAPH_RCCL=1) and replayed."""
+    monkeypatch.setenv("GOL_GRAPH_RCCL", "1")
+    N, gens = 512, 16 * 8 + 8 * 3 + 5
+    got, st = _run(gol, rccl, N, gens, 17, halo_depth=8, decomp=decomp, subtiles=0)
+    assert st["graph_launches"] >= 1, st
+    assert np.array_equal(got, numpy_step(initial_board(5, N, 1, True, 17), gens))

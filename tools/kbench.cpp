@@ -46,7 +46,9 @@ int main(int argc, char** argv) {
     hipDeviceProp_t prop;
     CK(hipGetDeviceProperties(&prop, 0));
     const int tile_lv = argc > 8 ? atoi(argv[8]) : 1;  // tile kernel: generations per LDS pass
-    const u32 flags = hipk::STEP_WRAP_Y | (pf ? hipk::STEP_PF_LDS : 0u) | (skew ? hipk::STEP_SKEW : 0u) |
+    (void)pf;
+    (void)skew;  // the LDS-ring prefetch and skewed pipeline variants were removed (measured slower)
+    const u32 flags = hipk::STEP_WRAP_Y |
                       (tile_lv == 2 ? hipk::STEP_TILE_L2 : 0u);
     std::vector<Region> rg = {{0, N, 0, L.nw}};
     i64 rows = rows_arg;

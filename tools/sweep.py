@@ -28,19 +28,18 @@ def main():
     ap.add_argument("--waves", type=ints, default=[0])
     ap.add_argument("--rows", type=ints, default=[0])
     ap.add_argument("--kernel", default="temporal")
-    ap.add_argument("--prefetch", default="lds", help="comma list of lds,reg")
     ap.add_argument("--rounds", type=int, default=2)
     args = ap.parse_args()
 
     import gol_amd
 
-    variants = list(itertools.product(args.depth, args.waves, args.rows, args.prefetch.split(",")))
+    variants = list(itertools.product(args.depth, args.waves, args.rows))
     results = {v: [] for v in variants}
     for rnd in range(args.rounds):
         for v in variants:
-            depth, waves, rows, pf = v
+            depth, waves, rows = v
             sim = gol_amd.Simulation(args.size, backend="hip", device=0, halo_depth=depth, waves_target=waves,
-                                     rows_per_wave=rows, kernel=args.kernel, prefetch=pf).init(5, seed=7)
+                                     rows_per_wave=rows, kernel=args.kernel).init(5, seed=7)
             sim.step(max(depth * 40, 64))
             sim.synchronize()
             t0 = time.perf_counter()
@@ -50,12 +49,12 @@ def main():
             st = sim.stats()
             rate = args.size * args.size * args.gens / dt
             results[v].append(rate)
-            print(json.dumps({"round": rnd, "depth": depth, "waves_target": waves, "rows": rows, "pf": pf,
+            print(json.dumps({"round": rnd, "depth": depth, "waves_target": waves, "rows": rows,
                               "plan_waves": st["plan_waves"], "lane_eff": round(st["lane_efficiency"], 4),
                               "us_per_gen": dt / args.gens * 1e6, "cells_per_s": rate}), flush=True)
             del sim
     for v, rs in results.items():
-        print(json.dumps({"summary": True, "depth": v[0], "waves_target": v[1], "rows": v[2], "pf": v[3],
+        print(json.dumps({"summary": True, "depth": v[0], "waves_target": v[1], "rows": v[2],
                           "median_cells_per_s": statistics.median(rs), "max": max(rs)}), flush=True)
 
 
