@@ -100,8 +100,18 @@ class HipEngine : public Engine {
         if (cfg_.transport == "device" && !t_->device_buffers())
             throw Error("GOL_TRANSPORT=device needs a device transport (RCCL)");
         for (auto& kk : kern_) kk = kernel_;
-        HIP_CHECK(hipStreamCreateWithFlags(&s_comp_, hipStreamNonBlocking));
-        HIP_CHECK(hipStreamCreateWithFlags(&s_comm_, hipStreamNonBlocking));
+        // The two streams must sit on different hardware queues, or their kernels serialise.  HIP
+        // multiplexes streams onto GPU_MAX_HW_QUEUES (4) queues, and once an RCCL communicator exists
+        // (it creates streams of its own) two plain streams created afterwards were measured to land
+        // on ONE queue (tools/queue_probe.cpp, profiles/queue_probe.txt: 1.68 vs 0.86 ms for two
+        // concurrent kernels), which serialised the sub-tile halves and the split schedule's
+        // exchange.  Streams of different priority get different queues in every case measured, so
+        // the comm / second-half stream is created with the greatest priority.
+        int prio_least = 0, prio_greatest = 0;
+        HIP_CHECK(hipDeviceGetStreamPriorityRange(&prio_least, &prio_greatest));
+        HIP_CHECK(hipStreamCreateWithPriority(&s_comp_, hipStreamNonBlocking, 0));
+        HIP_CHECK(hipStreamCreateWithPriority(&s_comm_, hipStreamNonBlocking,
+                                              env_int("GOL_COMM_PRIORITY", 1) ? prio_greatest : 0));
         events_needed_ = cfg_.force_split || !halo_items(L_.R).empty();
         // All device memory work is ordered on the engine's own streams.  (They are non-blocking:
         // null-stream calls such as hipMemset, or a pageable hipMemcpy whose DMA may still be in
@@ -241,6 +251,11 @@ class HipEngine : public Engine {
     // Graph shape of run(): m supersteps of k generations per replay; false when run() stays eager.
     bool graph_shape(int& k, int& m) {
         if (!cfg_.graph || cfg_.profile) return false;
+        // Sub-tile supersteps stay eager: captured (fork/join across two streams) they replayed
+        // slower than eager launches on MI355X / ROCm 7.2 (32768^2: 14.2 vs 12.8 us/gen over 20
+        // generations, 13.0 vs 10.4 over 256; profiles/short_run_probe.txt).  GOL_GRAPH_SUBTILES=1
+        // captures them anyway (measurement knob).
+        if (dual_ && env_int("GOL_GRAPH_SUBTILES", 0) == 0) return false;
         k = cfg_.compat ? 1 : superstep_depth();
         m = cfg_.graph_supersteps;
         if (m <= 0) m = k >= 8 ? 16 : 32;
@@ -290,7 +305,8 @@ class HipEngine : public Engine {
             for (int p = 0; p < 2; ++p) {
                 const int p0 = par();
                 set_par(p);
-                graph_for(k, sh.m, sh.rem);
+                // upload now: the first launch of an exec otherwise pays for it (in a timed region)
+                if (hipGraphExec_t ex = graph_for(k, sh.m, sh.rem)) HIP_CHECK(hipGraphUpload(ex, s_comp_));
                 set_par(p0);
             }
         }
@@ -433,10 +449,14 @@ class HipEngine : public Engine {
         // waves/SIMD each half's plan is sized for: two concurrent halves fill the SIMDs between
         // them, so 2-wave plans (taller segments, less halo) measured best (kbench: 9.85 vs 10.11
         // us/gen at 32768^2); GOL_SUB_OCC overrides (0 = the single-tile tuned occupancy)
-        if (cfg_.sub_occ > 0)
-            bpc = std::min<i64>(bpc, cfg_.sub_occ);
-        else if (occ_ > 0)
-            bpc = std::min<i64>(bpc, occ_);
+        // (at the temporal pass depth; shallower passes are memory bound and want every resident
+        // wave: profiles/kb_depth_sweep.txt)
+        if (k >= tdepth_) {
+            if (cfg_.sub_occ > 0)
+                bpc = std::min<i64>(bpc, cfg_.sub_occ);
+            else if (occ_ > 0)
+                bpc = std::min<i64>(bpc, occ_);
+        }
         const i64 rows = balanced_rows_per_chunk(rg, L.nw, L.h, k, bpc * kWavesPerBlock * cus_, 2 * (i64)k, true);
         DevPlan p;
         std::vector<LaneDesc> lanes = build_plan(rg, L.nw, L.h, rows, k, true, &p.st, kWavesPerBlock, cfg_.plan_xcds);
@@ -578,6 +598,7 @@ class HipEngine : public Engine {
         if (!tuned_) {
             if (cfg_.kernel == "auto") autotune_kernel();
             choose_schedule();  // collective when ranks have neighbours
+            measure_pass_costs();
             tuned_ = true;
             passes_.clear();  // the pass cuts may depend on the tuned kernel (pass_depths)
             // The comm stream waits on the compute stream's ready event only in the split
@@ -597,6 +618,7 @@ class HipEngine : public Engine {
         for (const auto& kv : tune_ms_) tn += strprintf("%s%s=%.3fus/gen", tn.empty() ? "" : " ", kv.first.c_str(), kv.second * 1e3);
         for (const auto& kv : sched_us_)
             tn += strprintf("%ssched:%s=%.3fus/gen", tn.empty() ? "" : " ", kv.first.c_str(), kv.second);
+        for (const auto& kv : pass_us_) tn += strprintf("%spass%d=%.1fus", tn.empty() ? "" : " ", kv.first, kv.second);
         stats_.tuning = tn;
         // Build the plans of the supersteps the runs will use now (the full superstep and the
         // remainder of the hinted run length), so neither graph capture nor a hinted timed loop
@@ -649,9 +671,12 @@ class HipEngine : public Engine {
         if (ps.size() > 1) mark_ready();  // the next exchange reads what the last pass wrote
     }
 
-    // Kernel passes of a superstep of k generations: the fewest passes of at most the kernel depth
-    // K, with depths as equal as possible (20 = 7 + 7 + 6, not 8 + 8 + 4: a shallow pass streams the
-    // board through HBM for few generations and is memory bound, docs/PERFORMANCE.md §6).
+    // Kernel passes of a superstep of k generations.  Once the pass costs are measured
+    // (measure_pass_costs), the cheapest cut over the instantiated depths <= K; before that (and with
+    // an explicit GOL_KERNEL_DEPTH) the fewest passes of at most K with depths as equal as possible
+    // (20 = 7 + 7 + 6, not 8 + 8 + 4).  A pass streams the board through HBM once whatever its
+    // depth, so shallow passes cost nearly as much as deep ones (32768^2: ~70-80 us for any depth
+    // <= 6, ~90 us at 8; profiles/kb_depth_sweep.txt).
     const std::vector<int>& pass_depths(int k) {
         const int key = k + (dual_ ? (1 << 20) : 0);
         auto it = passes_.find(key);
@@ -662,6 +687,21 @@ class HipEngine : public Engine {
         auto ok = [&](int d) { return any_depth || hipk::step_depth_supported(d); };
         const int K = std::max(1, dual_ ? tdepth_ : kdepth_);
         std::vector<int> ps;
+        if (tuned_ && !pass_us_.empty() && !any_depth) {
+            // cheapest cut by the measured per-depth pass times (dynamic programming over k)
+            std::vector<double> best((size_t)k + 1, 1e300);
+            std::vector<int> pick((size_t)k + 1, 0);
+            best[0] = 0;
+            for (int x = 1; x <= k; ++x)
+                for (const auto& dc : pass_us_)
+                    if (dc.first <= x && best[(size_t)(x - dc.first)] + dc.second < best[(size_t)x]) {
+                        best[(size_t)x] = best[(size_t)(x - dc.first)] + dc.second;
+                        pick[(size_t)x] = dc.first;
+                    }
+            for (int x = k; x > 0; x -= pick[(size_t)x]) ps.push_back(pick[(size_t)x]);
+            std::sort(ps.begin(), ps.end(), std::greater<int>());
+            return passes_.emplace(key, ps).first->second;
+        }
         const int n = (k + K - 1) / K;
         bool balanced = true;
         for (int j = 0; j < n; ++j) {
@@ -778,6 +818,66 @@ class HipEngine : public Engine {
             if (ms >= budget_ms) break;
         }
         kern_[0] = saved;
+    }
+
+    // Per-depth pass times of the chosen mode (temporal kernel: one tile, or the two halves on two
+    // streams without joins between passes, as inside a superstep), for the pass cuts of supersteps
+    // (pass_depths).  Measured rather than modelled: the cost is an HBM streaming floor plus the
+    // VALU work of the depth, and code generation differs per depth (32768^2 one tile: depth 7 is
+    // slower per pass than depth 8; profiles/kb_depth_sweep.txt).  Rank-local: the cut only changes
+    // kernel passes, never the exchanges.
+    void measure_pass_costs() {
+        pass_us_.clear();
+        if (cfg_.compat || cfg_.kernel_depth > 0 || kernel_ == "lds" || (!dual_ && tile_kernel(0))) return;
+        const int K = dual_ ? tdepth_ : kdepth_;
+        std::vector<int> ds;
+        for (int d = 1; d <= K; ++d)
+            if (hipk::step_depth_supported(d)) ds.push_back(d);
+        if (ds.size() < 2) return;
+        for (int d : ds) {  // every plan first: plan building idles the GPU and drops its clock
+            if (dual_) {
+                sub_plan(0, d, 0);
+                sub_plan(1, d, 0);
+            } else {
+                plan(0, d, 0);
+            }
+        }
+        hipEvent_t e0, e1;
+        HIP_CHECK(hipEventCreate(&e0));
+        HIP_CHECK(hipEventCreate(&e1));
+        spin_up();
+        const int reps = 4;
+        std::map<int, double> best;
+        for (int round = 0; round < 3; ++round)
+            for (int d : ds) {
+                HIP_CHECK(hipEventRecord(e0, s_comp_));
+                if (dual_) {
+                    HIP_CHECK(hipStreamWaitEvent(s_comm_, e0, 0));
+                    for (int i = 0; i < reps; ++i)
+                        for (int sub = 0; sub < 2; ++sub) {
+                            const DevPlan& pl = sub_plan(sub, d, 0);
+                            const Layout& Ls = sub_L_[sub];
+                            hipk::StepParams sp{Ls.pitch, (i32)Ls.h, (i32)Ls.nw, Ls.R, sub_flags()};
+                            hipk::launch_step(d, sub_buf_[sub][sub_cur_], sub_buf_[sub][sub_cur_ ^ 1], pl.d, pl.waves, sp,
+                                              sub ? s_comm_ : s_comp_);
+                        }
+                    HIP_CHECK(hipEventRecord(ev_sub_b_, s_comm_));
+                    HIP_CHECK(hipStreamWaitEvent(s_comp_, ev_sub_b_, 0));
+                } else {
+                    for (int i = 0; i < reps; ++i) launch(0, d, 0, buf_[cur_], buf_[cur_ ^ 1], s_comp_);
+                }
+                HIP_CHECK(hipEventRecord(e1, s_comp_));
+                HIP_CHECK(hipEventSynchronize(e1));
+                float ms = 0;
+                HIP_CHECK(hipEventElapsedTime(&ms, e0, e1));
+                const double us = ms * 1e3 / reps;
+                best[d] = round == 0 ? us : std::min(best[d], us);
+            }
+        HIP_CHECK(hipEventDestroy(e0));
+        HIP_CHECK(hipEventDestroy(e1));
+        HIP_CHECK(hipGetLastError());
+        pass_us_ = best;
+        passes_.clear();
     }
 
     // Pick the superstep schedule by measurement.  Candidates (every rank builds the same list from
@@ -1089,7 +1189,10 @@ class HipEngine : public Engine {
     }
 
     const DevPlan& plan(int kind, int k, i64 e = 0) {
-        const int key = occ_ * 10000000 + (tile_kernel(kind) ? 1000000 : 0) + kind * 100000 + (int)e * 100 + k;
+        // plans depend on e only through regions(): rows beyond the tile when y has neighbours,
+        // ghost words when x has neighbours (so one plan serves every e of a local rank)
+        const i64 ek = self_y() ? (self_x() ? 0 : (e > 0 ? 1 : 0)) : e;
+        const int key = occ_ * 10000000 + (tile_kernel(kind) ? 1000000 : 0) + kind * 100000 + (int)ek * 100 + k;
         auto it = plans_.find(key);
         if (it != plans_.end()) return it->second;
         std::vector<Region> rg = regions(kind, k, e);
@@ -1118,7 +1221,9 @@ class HipEngine : public Engine {
             if (rows <= 0) {
                 // one full round of resident waves (occupancy of this kernel instantiation)
                 i64 bpc = hipk::step_blocks_per_cu(k, step_flags());
-                if (occ_ > 0) bpc = std::min<i64>(bpc, occ_);  // 256-thread blocks per CU = waves per SIMD
+                // 256-thread blocks per CU = waves per SIMD; the tuned cap applies to the tuned depth
+                // only (shallower passes are memory bound and want every resident wave)
+                if (occ_ > 0 && k == kdepth_) bpc = std::min<i64>(bpc, occ_);
                 const i64 resident = bpc * kWavesPerBlock * cus_;
                 rows = balanced_rows_per_chunk(rg, L_.nw, L_.h, k, resident, 2 * (i64)k, xwrap_by_plan());
             }
@@ -1368,6 +1473,7 @@ class HipEngine : public Engine {
     std::map<int, std::vector<int>> passes_;
     bool split_ = false;   // superstep schedule: interior/boundary split with overlapped exchange
     std::map<std::string, double> sched_us_;  // choose_schedule: us per generation per candidate
+    std::map<int, double> pass_us_;           // measure_pass_costs: us per pass by depth (chosen mode)
     bool tuned_ = false;
     std::map<std::string, float> tune_ms_;
     hipEvent_t fence_ev_[kFenceDepth] = {};

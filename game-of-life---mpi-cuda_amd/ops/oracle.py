@@ -33,7 +33,10 @@ def torch_step(board, generations: int = 1, device=None):
     import torch
     import torch.nn.functional as F
 
-    x = torch.as_tensor(np.asarray(board), dtype=torch.float32, device=device)[None, None]
+    if isinstance(board, torch.Tensor):  # e.g. a previous torch_step result, already on the device
+        x = board.to(device=device if device is not None else board.device, dtype=torch.float32)[None, None]
+    else:
+        x = torch.as_tensor(np.asarray(board), dtype=torch.float32, device=device)[None, None]
     k = torch.ones(1, 1, 3, 3, dtype=torch.float32, device=x.device)
     k[0, 0, 1, 1] = 0
     for _ in range(generations):

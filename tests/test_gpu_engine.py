@@ -127,9 +127,10 @@ def test_run_hint_single_graph(gol):
 
 
 @pytest.mark.parametrize("subtiles", [0, 2])
-def test_run_hint_short_run(gol, subtiles):
+def test_run_hint_short_run(gol, subtiles, monkeypatch):
     """A hinted run shorter than one superstep (the driver's bench: 20 generations, R = 64) is ONE
-    graph replay of its balanced passes (7 + 7 + 6), in the one-tile and the sub-tile mode."""
+    graph replay of its passes, in the one-tile and (GOL_GRAPH_SUBTILES=1) the sub-tile mode."""
+    monkeypatch.setenv("GOL_GRAPH_SUBTILES", "1")
     N, hint = 1024, 20
     s = _sim(gol, N, halo_depth=64, kernel="temporal", run_hint=hint, subtiles=subtiles).init(5, seed=23)
     assert s.stats()["schedule"].endswith("+subtiles2") == (subtiles == 2), s.stats()

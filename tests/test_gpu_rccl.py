@@ -58,6 +58,7 @@ def test_rccl_self_auto_schedule(gol, rccl):
 def test_rccl_self_subtiles(gol, rccl, graph_rccl, monkeypatch):
     """Two sub-tiles per rank: the rank's north / south halos go through RCCL straight into the halves."""
     monkeypatch.setenv("GOL_GRAPH_RCCL", "1" if graph_rccl else "0")
+    monkeypatch.setenv("GOL_GRAPH_SUBTILES", "1" if graph_rccl else "0")
     N, gens = 1024, 2 * 32 + 20
     got, st = _run(gol, rccl, N, gens, 9, halo_depth=32, subtiles=2, run_hint=gens)
     assert st["schedule"].endswith("+subtiles2"), st
