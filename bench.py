@@ -118,11 +118,16 @@ def main() -> int:
 
     import torch
 
+    use_torch_sync = backend == "hip" and torch.cuda.is_available()
+
     def device_sync():
         sim.synchronize()  # the engine's own HIP streams
-        if backend == "hip" and torch.cuda.is_available():
+        if use_torch_sync:
             torch.cuda.synchronize()
 
+    # torch's lazy device initialisation (the first torch.cuda.synchronize) takes ~1 ms: do it before
+    # the warmup, so the GPU goes from the warmup straight into the timed region
+    device_sync()
     sim.step(warmup)
     device_sync()
     transport.barrier()

@@ -29,6 +29,8 @@ enum : u32 {
                             // kernel gets x-wrap from its plan (build_plan(..., xwrap = true))
     STEP_WRAP_Y = 1u << 1,  // tile is its own N/S neighbour: rows are read modulo h, no ghost rows
     STEP_TILE_L2 = 1u << 4, // tile kernel: two generations per LDS pass (half the barriers)
+    STEP_SEAM = 1u << 5,    // temporal kernel: rows < 0 are read from StepParams::above, rows >= h
+                            // from StepParams::below (sub-tile first pass: the other half's edges)
 };
 
 // Rows the HIP engine allocates past the bottom halo: the temporal kernel's 3-row prefetch overrun
@@ -41,6 +43,10 @@ struct StepParams {
     i32 nw;
     i32 R;
     u32 flags;
+    // STEP_SEAM: row r < 0 of the source is at above + r * pitch, row r >= h at below + (r - h) * pitch
+    // (word c at + c + 1, like the source buffer's rows)
+    const u64* above = nullptr;
+    const u64* below = nullptr;
 };
 
 // Supported temporal depths (template instantiations).

@@ -151,12 +151,12 @@ class HipEngine : public Engine {
         hipStreamSynchronize(s_comp_);
         hipStreamSynchronize(s_comm_);
         for (auto& kv : sub_plans_) hipFree(kv.second.d);
-        for (auto& kv : dual_copies_) hipFree(kv.second.d);
         for (auto& sb : sub_buf_)
             for (u64* b : sb)
                 if (b) hipFree(b);
         if (ev_sub_a_) hipEventDestroy(ev_sub_a_);
         if (ev_sub_b_) hipEventDestroy(ev_sub_b_);
+        if (ev_sub_x_) hipEventDestroy(ev_sub_x_);
         for (auto& kv : graphs_) hipGraphExecDestroy(kv.second);
         for (auto& kv : plans_) hipFree(kv.second.d);
         for (auto& kv : copies_) {
@@ -253,9 +253,8 @@ class HipEngine : public Engine {
         if (!cfg_.graph || cfg_.profile) return false;
         // Sub-tile supersteps stay eager: captured (fork/join across two streams) they replayed
         // slower than eager launches on MI355X / ROCm 7.2 (32768^2: 14.2 vs 12.8 us/gen over 20
-        // generations, 13.0 vs 10.4 over 256; profiles/short_run_probe.txt).  GOL_GRAPH_SUBTILES=1
-        // captures them anyway (measurement knob).
-        if (dual_ && env_int("GOL_GRAPH_SUBTILES", 0) == 0) return false;
+        // generations, 13.0 vs 10.4 over 256; profiles/short_run_probe.txt).
+        if (dual_) return false;
         k = cfg_.compat ? 1 : superstep_depth();
         m = cfg_.graph_supersteps;
         if (m <= 0) m = k >= 8 ? 16 : 32;
@@ -290,9 +289,9 @@ class HipEngine : public Engine {
         return v;
     }
 
-    // Buffer parity of the active mode (one tile: cur_; two sub-tiles: sub_cur_).
-    int par() const { return dual_ ? sub_cur_ : cur_; }
-    void set_par(int p) { (dual_ ? sub_cur_ : cur_) = p; }
+    // Buffer parity of the captured (one-tile) mode.
+    int par() const { return cur_; }
+    void set_par(int p) { cur_ = p; }
 
     // Capture and instantiate the replay graphs at init, so no timed run() ever pays for
     // stream capture or graph instantiation (a 16-superstep capture costs milliseconds: more than
@@ -361,6 +360,9 @@ class HipEngine : public Engine {
             // board (consecutive run() calls keep it in the halves; readers sync it back lazily)
             for (int s = 0; s < 2; ++s)
                 dual_copy(sub_rows(s, sub_cur_, 0), buf_[cur_] + L_.index(sub_r0_[s], -1), rows_bytes(s, sub_L_[s].h));
+            // both halves' first superstep waits for the copy (each waits on the other's "done" event)
+            HIP_CHECK(hipEventRecord(ev_sub_a_, s_comp_));
+            HIP_CHECK(hipEventRecord(ev_sub_b_, s_comp_));
             sub_current_ = true;
         }
         run_graphed(generations);
@@ -369,14 +371,19 @@ class HipEngine : public Engine {
     }
 
     // ----- two sub-tiles per rank (1-D) -----
-    // The tile's rows are split into two halves with their own double buffers and R ghost rows.
-    // Per superstep the halves exchange R edge rows by device copies (and the rank's north / south
-    // halos go to sub-tile 0 / 1 through the transport, in the same canonical messages as the
-    // one-tile engine), then each half runs the superstep's passes on its own stream, planned for
-    // the whole GPU.  The two kernels of a pass overlap: while one drains, the other's waves fill
-    // the freed SIMD slots (two half-board kernels on two streams: 9.8 vs 11.0 us/gen at 32768^2,
-    // docs/PERFORMANCE.md).  Whether a rank runs one tile or two sub-tiles is decided by
-    // measurement at init (choose_schedule).
+    // The tile's rows are split into two halves, each with THREE buffers of R ghost rows, each
+    // running a superstep's passes on its own stream with a plan sized for the whole GPU.  The two
+    // kernels of a pass overlap: while one drains, the other's waves fill the freed SIMD slots (two
+    // half-board kernels on two streams: 9.8 vs 11.0 us/gen at 32768^2, docs/PERFORMANCE.md).
+    //   * A superstep's first pass reads the other half's edge rows (and the torus wrap) in place
+    //     (STEP_SEAM): no seam copy, no event between the copy and the first kernel.
+    //   * So that the other half can read them at any time during the superstep, a superstep never
+    //     writes the buffer it started from: its passes alternate between the other two buffers.
+    //   * Each stream waits only for the other half's end of the previous superstep (and, with
+    //     neighbours, the compute stream runs the rank's canonical RCCL messages first and the
+    //     second stream waits for them).
+    // Whether a rank runs one tile or two sub-tiles is decided by measurement at init
+    // (choose_schedule).
     // Requested (GOL_SUBTILES=2) or auto-wanted: inputs identical on every rank (the mode is a
     // candidate of the collective schedule timing): mode, layout, average strip height, halo depth,
     // transport kind.
@@ -393,7 +400,7 @@ class HipEngine : public Engine {
         if (L_.h < 8 * (i64)L_.R) return false;
         size_t fr = 0, tot = 0;
         if (hipMemGetInfo(&fr, &tot) != hipSuccess) return false;
-        return 2 * alloc_bytes_ + ((size_t)1 << 30) < fr;
+        return 3 * alloc_bytes_ + ((size_t)1 << 30) < fr;  // 3 buffers of half a tile per half
     }
 
     void setup_dual() {
@@ -405,7 +412,7 @@ class HipEngine : public Engine {
             const i64 hs = s == 0 ? h0 : L_.h - h0;
             sub_L_[s] = Layout(hs, L_.w, L_.R);
             const size_t bytes = (size_t)(sub_L_[s].words() + hipk::kSlackRows * sub_L_[s].pitch) * 8;
-            for (int i = 0; i < 2; ++i) {
+            for (int i = 0; i < 3; ++i) {
                 HIP_CHECK(hipMalloc(&sub_buf_[s][i], bytes));
                 HIP_CHECK(hipMemsetAsync(sub_buf_[s][i], 0, bytes, s_comp_));
             }
@@ -413,6 +420,7 @@ class HipEngine : public Engine {
         if (!ev_sub_a_) {
             HIP_CHECK(hipEventCreateWithFlags(&ev_sub_a_, hipEventDisableTiming));
             HIP_CHECK(hipEventCreateWithFlags(&ev_sub_b_, hipEventDisableTiming));
+            HIP_CHECK(hipEventCreateWithFlags(&ev_sub_x_, hipEventDisableTiming));
         }
         HIP_CHECK(hipStreamSynchronize(s_comp_));
     }
@@ -421,8 +429,6 @@ class HipEngine : public Engine {
         synchronize();
         for (auto& kv : sub_plans_) hipFree(kv.second.d);
         sub_plans_.clear();
-        for (auto& kv : dual_copies_) hipFree(kv.second.d);
-        dual_copies_.clear();
         for (auto& sb : sub_buf_)
             for (u64*& b : sb) {
                 if (b) hipFree(b);
@@ -436,7 +442,6 @@ class HipEngine : public Engine {
         const std::vector<int>& ps = pass_depths(k);
         for (size_t j = 0; j < ps.size(); ++j)
             for (int s = 0; s < 2; ++s) sub_plan(s, ps[j], ext_after(ps, j));
-        for (int p = 0; p < 2; ++p) dual_copies(k, p);
     }
 
     const DevPlan& sub_plan(int s, int k, i64 e) {
@@ -471,7 +476,7 @@ class HipEngine : public Engine {
 
     u32 sub_flags() const { return step_flags() & ~hipk::STEP_WRAP_Y; }  // sub-tiles always have ghost rows
 
-    // rows [r0, r0 + n) of sub-tile s at parity par (full pitch, contiguous)
+    // rows [r0, r0 + n) of sub-tile s in its buffer `par` (0..2; full pitch, contiguous)
     u64* sub_rows(int s, int par, i64 r0) { return sub_buf_[s][par] + sub_L_[s].index(r0, -1); }
     size_t rows_bytes(int s, i64 n) const { return (size_t)(n * sub_L_[s].pitch) * 8; }
 
@@ -482,46 +487,19 @@ class HipEngine : public Engine {
     // Both halves done -> the canonical buffer (before anything reads it).
     void sync_canonical() {
         if (!canon_stale_) return;
+        HIP_CHECK(hipStreamWaitEvent(s_comp_, ev_sub_b_, 0));  // the second half's last superstep
         for (int s = 0; s < 2; ++s)
             dual_copy(buf_[cur_] + L_.index(sub_r0_[s], -1), sub_rows(s, sub_cur_, 0), rows_bytes(s, sub_L_[s].h));
         canon_stale_ = false;
     }
 
-    struct DualCopies {
-        hipk::CopyDesc* d = nullptr;
-        int n = 0;
-        i64 max = 0;
-    };
-    const DualCopies& dual_copies(int k, int p) {
-        const int key = k * 2 + p;
-        auto it = dual_copies_.find(key);
-        if (it != dual_copies_.end()) return it->second;
-        const i64 h0 = sub_L_[0].h, h1 = sub_L_[1].h, P = sub_L_[0].pitch;
-        std::vector<hipk::CopyDesc> v = {{sub_rows(0, p, h0 - k), sub_rows(1, p, -k), P, P, k, (i32)P},
-                                         {sub_rows(1, p, 0), sub_rows(0, p, h0), P, P, k, (i32)P}};
-        if (self_y()) {
-            v.push_back({sub_rows(1, p, h1 - k), sub_rows(0, p, -k), P, P, k, (i32)P});
-            v.push_back({sub_rows(0, p, 0), sub_rows(1, p, h1), P, P, k, (i32)P});
-        }
-        DualCopies dc;
-        dc.n = (int)v.size();
-        dc.max = (i64)k * P;
-        HIP_CHECK(hipMalloc(&dc.d, v.size() * sizeof(hipk::CopyDesc)));
-        upload(dc.d, v.data(), v.size() * sizeof(hipk::CopyDesc));
-        return dual_copies_.emplace(key, dc).first->second;
-    }
-
-    // One sub-tile superstep.  s_comp holds the joined state of the previous superstep on entry and
-    // on exit (fork after the halo work, join after the last pass), so the body is also a valid
-    // stream capture: the comm stream joins the capture through the fork event.
+    // One sub-tile superstep: sub-tile 0 on the compute stream, 1 on the second stream.
     void dual_superstep(int k) {
         prepare_dual(k);
         const int p = sub_cur_;
-        const i64 h1 = sub_L_[1].h;
-        // internal seam (sub0 bottom edge -> sub1 top ghost, sub1 top edge -> sub0 bottom ghost) and,
-        // when the rank is its own N/S neighbour, the torus wrap: one batched copy kernel
-        const DualCopies& dc = dual_copies(k, p);
-        hipk::launch_copy_regions(dc.d, dc.n, dc.max, s_comp_);
+        const int a = (p + 1) % 3, b = (p + 2) % 3;  // the passes alternate a, b, a, ... (never p)
+        const i64 h0 = sub_L_[0].h, h1 = sub_L_[1].h;
+        HIP_CHECK(hipStreamWaitEvent(s_comp_, ev_sub_b_, 0));  // half 1's previous superstep is done
         if (!self_y()) {
             // the one-tile engine's canonical messages (Engine::halo_items, 1-D): N then S
             std::vector<Message> sends, recvs;
@@ -532,24 +510,35 @@ class HipEngine : public Engine {
             t_->exchange(sends, recvs, (void*)s_comp_);
             stats_.exchanges += 1;
             stats_.halo_bytes += (u64)(rows_bytes(0, k) + rows_bytes(1, k));
+            HIP_CHECK(hipEventRecord(ev_sub_x_, s_comp_));  // also implies half 0's previous superstep
+            HIP_CHECK(hipStreamWaitEvent(s_comm_, ev_sub_x_, 0));
+        } else {
+            HIP_CHECK(hipStreamWaitEvent(s_comm_, ev_sub_a_, 0));  // half 0's previous superstep is done
         }
-        HIP_CHECK(hipEventRecord(ev_sub_a_, s_comp_));
-        HIP_CHECK(hipStreamWaitEvent(s_comm_, ev_sub_a_, 0));
         const std::vector<int>& ps = pass_depths(k);
-        int q = p;
-        for (size_t j = 0; j < ps.size(); ++j) {
-            const i64 e = ext_after(ps, j);
-            for (int s = 0; s < 2; ++s) {
-                const DevPlan& pl = sub_plan(s, ps[j], e);
-                hipk::StepParams sp{sub_L_[s].pitch, (i32)sub_L_[s].h, (i32)sub_L_[s].nw, sub_L_[s].R, sub_flags()};
-                hipk::launch_step(ps[j], sub_buf_[s][q], sub_buf_[s][q ^ 1], pl.d, pl.waves, sp, s ? s_comm_ : s_comp_);
+        for (int s = 0; s < 2; ++s) {
+            const Layout& Ls = sub_L_[s];
+            const int o = 1 - s;  // the other half
+            hipk::StepParams sp{Ls.pitch, (i32)Ls.h, (i32)Ls.nw, Ls.R, sub_flags()};
+            hipk::StepParams sp0 = sp;
+            sp0.flags |= hipk::STEP_SEAM;
+            // rows above half 0 / below half 1: the rank's ghost rows (exchanged) or, on a torus
+            // without neighbours, the other half's far edge; between the halves: the other's edge
+            const bool wrap = self_y();
+            sp0.above = s == 0 ? (wrap ? sub_rows(o, p, sub_L_[o].h) : sub_rows(s, p, 0)) : sub_rows(o, p, h0);
+            sp0.below = s == 1 ? (wrap ? sub_rows(o, p, 0) : sub_rows(s, p, h1)) : sub_rows(o, p, 0);
+            int q = p;
+            for (size_t j = 0; j < ps.size(); ++j) {
+                const int dsti = (j % 2 == 0) ? a : b;
+                const DevPlan& pl = sub_plan(s, ps[j], ext_after(ps, j));
+                hipk::launch_step(ps[j], sub_buf_[s][q], sub_buf_[s][dsti], pl.d, pl.waves, j == 0 ? sp0 : sp,
+                                  s ? s_comm_ : s_comp_);
+                q = dsti;
             }
-            q ^= 1;
+            HIP_CHECK(hipEventRecord(s ? ev_sub_b_ : ev_sub_a_, s ? s_comm_ : s_comp_));
         }
         HIP_CHECK(hipGetLastError());
-        HIP_CHECK(hipEventRecord(ev_sub_b_, s_comm_));
-        HIP_CHECK(hipStreamWaitEvent(s_comp_, ev_sub_b_, 0));
-        sub_cur_ = q;
+        sub_cur_ = (ps.size() % 2) ? a : b;
     }
 
     const DevPlan& full_plan_stats() {
@@ -858,8 +847,8 @@ class HipEngine : public Engine {
                             const DevPlan& pl = sub_plan(sub, d, 0);
                             const Layout& Ls = sub_L_[sub];
                             hipk::StepParams sp{Ls.pitch, (i32)Ls.h, (i32)Ls.nw, Ls.R, sub_flags()};
-                            hipk::launch_step(d, sub_buf_[sub][sub_cur_], sub_buf_[sub][sub_cur_ ^ 1], pl.d, pl.waves, sp,
-                                              sub ? s_comm_ : s_comp_);
+                            hipk::launch_step(d, sub_buf_[sub][sub_cur_], sub_buf_[sub][(sub_cur_ + 1) % 3], pl.d,
+                                              pl.waves, sp, sub ? s_comm_ : s_comp_);
                         }
                     HIP_CHECK(hipEventRecord(ev_sub_b_, s_comm_));
                     HIP_CHECK(hipStreamWaitEvent(s_comp_, ev_sub_b_, 0));
@@ -1497,13 +1486,13 @@ class HipEngine : public Engine {
     bool dual_ = false;
     Layout sub_L_[2];
     i64 sub_r0_[2] = {0, 0};
-    u64* sub_buf_[2][2] = {{nullptr, nullptr}, {nullptr, nullptr}};
-    int sub_cur_ = 0;
+    u64* sub_buf_[2][3] = {{nullptr, nullptr, nullptr}, {nullptr, nullptr, nullptr}};
+    int sub_cur_ = 0;  // buffer (0..2) holding both halves' current generation
     bool sub_current_ = false;  // the halves hold the current board
     bool canon_stale_ = false;  // buf_[cur_] lags the halves (sync_canonical before reading it)
     std::map<int, DevPlan> sub_plans_;
-    std::map<int, DualCopies> dual_copies_;
-    hipEvent_t ev_sub_a_ = nullptr, ev_sub_b_ = nullptr;
+    hipEvent_t ev_sub_a_ = nullptr, ev_sub_b_ = nullptr;  // half 0 / half 1 done with its last superstep
+    hipEvent_t ev_sub_x_ = nullptr;                        // the rank's exchange (into both halves) done
     std::map<int, DevCopies> copies_;
     std::map<int, std::vector<HaloItem>> items_;
     std::map<i64, hipGraphExec_t> graphs_;

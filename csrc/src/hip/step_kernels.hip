@@ -108,34 +108,54 @@ __device__ __forceinline__ bool advance(Pipe<K>& P, u32& lo, u32& hi, int i) {
 // Row prefetch: a register triple loaded one row-triple ahead, pinned above the compute with a
 // sched_barrier (otherwise the scheduler sinks the loads to the end of the loop body).  (An LDS
 // DMA ring and a skewed level pipeline were built and measured slower; docs/PERFORMANCE.md §2.)
-template <int K, bool WRAPY>
+// Row sources of the load stream (kernel template ROWS):
+//   ROWS_GHOST  rows -R .. h+R-1 of the source buffer (ghost rows filled by exchanges / earlier passes)
+//   ROWS_WRAP   rows are periodic (the tile is its own N/S neighbour): row h is row 0
+//   ROWS_SEAM   rows < 0 come from p.above, rows >= h from p.below, rows 0..h-1 from the source
+//               buffer: the first pass of a sub-tile superstep reads the neighbouring half's edge rows
+//               in place (and the torus wrap), so no seam copy precedes it
+enum { ROWS_GHOST = 0, ROWS_WRAP = 1, ROWS_SEAM = 2 };
+
+template <int K, int ROWS>
 struct WaveRunner {
     const StepParams& p;
     const LaneDesc& d;
     const int n;   // row iterations: nrows + 2K
     const i64 hp;  // h * pitch
     const uint2* ld;
+    const u64* own0;  // ROWS_SEAM: row 0 of the source buffer
     uint2* st;
     i64 st_stride;  // pitch for output lanes, 0 for halo/idle lanes (they write a trash slot)
-    int lrow;       // tile row of the next load (WRAPY only)
+    int lrow;       // tile row of the next load (ROWS_WRAP, ROWS_SEAM; wave-uniform)
     uint2 pf[3];
     Pipe<K> P;
 
     __device__ __forceinline__ void next_row() {
         ld += p.pitch;
-        if (WRAPY) {  // rows are periodic: row h is row 0 (branch-free select)
+        if (ROWS == ROWS_WRAP) {  // rows are periodic: row h is row 0 (branch-free select)
             ++lrow;
             const bool w = lrow == p.h;
             lrow = w ? 0 : lrow;
             ld = w ? ld - hp : ld;
+        } else if (ROWS == ROWS_SEAM) {  // switch sources at rows 0 and h
+            ++lrow;
+            ld = lrow == 0 ? reinterpret_cast<const uint2*>(own0 + (d.col + 1)) : ld;
+            ld = lrow == p.h ? reinterpret_cast<const uint2*>(p.below + (d.col + 1)) : ld;
         }
     }
 
     __device__ __forceinline__ WaveRunner(const u64* src, u64* dst, const LaneDesc& d_, int nrows, const StepParams& p_)
         : p(p_), d(d_), n(nrows + 2 * K), hp((i64)p_.h * p_.pitch) {
         lrow = d.row0 - K;
-        if (WRAPY && lrow < 0) lrow += p.h;
-        ld = reinterpret_cast<const uint2*>(src + (i64)(lrow + p.R) * p.pitch + (d.col + 1));
+        if (ROWS == ROWS_WRAP && lrow < 0) lrow += p.h;
+        if (ROWS == ROWS_SEAM) {
+            own0 = src + (i64)p.R * p.pitch;
+            const u64* b = lrow < 0 ? p.above + (i64)lrow * p.pitch
+                                    : (lrow >= p.h ? p.below + (i64)(lrow - p.h) * p.pitch : own0 + (i64)lrow * p.pitch);
+            ld = reinterpret_cast<const uint2*>(b + (d.col + 1));
+        } else {
+            ld = reinterpret_cast<const uint2*>(src + (i64)(lrow + p.R) * p.pitch + (d.col + 1));
+        }
         // Every lane stores every row (no branch: the row loop stays one basic block, so the
         // scheduler can interleave consecutive rows).  Halo/idle lanes write their own column of the
         // last slack row of the allocation, which nothing reads.
@@ -210,7 +230,7 @@ struct WaveRunner {
 #else
 #define GOL_TEMPORAL_OCC
 #endif
-template <int K, bool WRAPY>
+template <int K, int ROWS>
 __global__ __launch_bounds__(256) GOL_TEMPORAL_OCC void step_temporal(const u64* __restrict__ src, u64* __restrict__ dst,
                                                                       const LaneDesc* __restrict__ plan, StepParams p) {
     const int wv = threadIdx.x >> 6;
@@ -219,13 +239,14 @@ __global__ __launch_bounds__(256) GOL_TEMPORAL_OCC void step_temporal(const u64*
     const LaneDesc d = plan[wave * kWaveLanes + lane];
     const int nrows = __builtin_amdgcn_readfirstlane(d.nrows);
     if (nrows <= 0) return;  // padding wave (uniform)
-    WaveRunner<K, WRAPY> w(src, dst, d, nrows, p);
+    WaveRunner<K, ROWS> w(src, dst, d, nrows, p);
     w.run();
 }
 
 template <int K>
 const void* kernel_for(u32 flags) {
-    return (flags & STEP_WRAP_Y) ? (const void*)step_temporal<K, true> : (const void*)step_temporal<K, false>;
+    if (flags & STEP_SEAM) return (const void*)step_temporal<K, ROWS_SEAM>;
+    return (flags & STEP_WRAP_Y) ? (const void*)step_temporal<K, ROWS_WRAP> : (const void*)step_temporal<K, ROWS_GHOST>;
 }
 
 typedef __attribute__((address_space(3))) void lds_void_t;

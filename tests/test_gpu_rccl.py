@@ -54,16 +54,14 @@ def test_rccl_self_auto_schedule(gol, rccl):
     assert np.array_equal(got, numpy_step(initial_board(5, N, 1, True, 5), gens))
 
 
-@pytest.mark.parametrize("graph_rccl", [False, True])
-def test_rccl_self_subtiles(gol, rccl, graph_rccl, monkeypatch):
-    """Two sub-tiles per rank: the rank's north / south halos go through RCCL straight into the halves."""
-    monkeypatch.setenv("GOL_GRAPH_RCCL", "1" if graph_rccl else "0")
-    monkeypatch.setenv("GOL_GRAPH_SUBTILES", "1" if graph_rccl else "0")
-    N, gens = 1024, 2 * 32 + 20
-    got, st = _run(gol, rccl, N, gens, 9, halo_depth=32, subtiles=2, run_hint=gens)
+@pytest.mark.parametrize("R,gens", [(32, 2 * 32 + 20), (16, 5 * 16 + 3)])
+def test_rccl_self_subtiles(gol, rccl, R, gens):
+    """Two sub-tiles per rank: the rank's north / south halos go through RCCL straight into the halves;
+    the seam between the halves is read in place by each half's first pass."""
+    N = 1024
+    got, st = _run(gol, rccl, N, gens, 9, halo_depth=R, subtiles=2, run_hint=gens)
     assert st["schedule"].endswith("+subtiles2"), st
-    if graph_rccl:
-        assert st["graph_launches"] >= 1, st
+    assert st["exchanges"] >= gens // R, st
     assert np.array_equal(got, numpy_step(initial_board(5, N, 1, True, 9), gens))
 
 
