@@ -191,5 +191,6 @@ std::unique_ptr<Engine> make_hip_engine(const Geometry& g, const EngineConfig& c
 // HIP runtime helpers used by the CLI / bindings (no-ops without a GPU).
 int hip_device_count(int* err = nullptr);
 void hip_set_device(int dev);
+int hip_try_set_device(int dev);  // hipError_t of hipSetDevice (0 = success)
 
 }  // namespace gol

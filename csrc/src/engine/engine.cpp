@@ -38,9 +38,9 @@ Engine::Engine(const Geometry& g, const EngineConfig& c, std::shared_ptr<Transpo
     // exchange it can drive): it synchronises its two streams once per superstep, so longer
     // supersteps keep more of the overlap.  Rank-invariant inputs only.
     const bool sub_transport = cfg_.transport != "host" && (g_.dec.P == 1 || t_->device_buffers());
-    const bool sub_tall = cfg_.backend == "hip" && cfg_.subtiles != 0 && !two_d() && strip_rows >= kSubtileMinRows &&
+    const bool sub_tall = cfg_.backend == "hip" && (cfg_.subtiles == 2 || cfg_.subtiles < 0) && !two_d() && strip_rows >= kSubtileMinRows &&
                           g_.dec.W % 64 == 0 && !cfg_.force_split && !cfg_.profile && cfg_.watchdog_s <= 0 &&
-                          !cfg_.compat && cfg_.kernel != "lds" && sub_transport;
+                          !cfg_.compat && cfg_.kernel != "lds" && cfg_.kernel != "tile" && sub_transport;
     const int want = cfg_.halo_depth > 0 ? cfg_.halo_depth : ((g_.dec.P > 1 && tall_strips) || sub_tall ? 64 : 32);
     int R = clamp_halo_depth(g_.dec, want);
     if (two_d()) R = std::min(R, 63);  // the column halo is one 64-cell word

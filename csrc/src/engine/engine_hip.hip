@@ -41,6 +41,7 @@ int hip_device_count(int* err) {
 }
 
 void hip_set_device(int dev) { HIP_CHECK(hipSetDevice(dev)); }
+int hip_try_set_device(int dev) { return (int)hipSetDevice(dev); }
 
 namespace {
 

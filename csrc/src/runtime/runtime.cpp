@@ -14,6 +14,7 @@
 #include <fstream>
 #include <thread>
 
+#include <fcntl.h>
 #include <unistd.h>
 
 #include "gol/io.hpp"
@@ -95,12 +96,10 @@ std::string select_backend(const Options& o, int rank, int local_rank) {
     if (n <= 0)
         throw ContractError(strprintf(" Unable to determine cuda device count, error is %d, count is %d\n", err, n), 255);
     int dev = (local_rank >= 0 ? local_rank : rank) % n;
-    try {
-        hip_set_device(dev);
-    } catch (const Error&) {
-        throw ContractError(strprintf(" Unable to have rank %d set to cuda device %d, error is %d \n", rank, dev, 1),
+    // the real hipError_t, as the reference prints its cudaError_t (gol-with-cuda.cu:298-299)
+    if (const int e = hip_try_set_device(dev))
+        throw ContractError(strprintf(" Unable to have rank %d set to cuda device %d, error is %d \n", rank, dev, e),
                             255);
-    }
     return b;
 }
 
@@ -196,94 +195,180 @@ void write_dumps(Engine& eng, FILE* fp) {
     const int r = g.rank;
     io::write_header(fp, r);
     std::vector<u64> words = eng.tile_words();
+    const i64 nw = eng.layout().nw;
     const bool tile_is_strip = d.Px == 1 && d.strip_starts[r] == g.row0 && d.strip_starts[r + 1] == g.row0 + g.h;
     bool all_strips = t.allreduce_min(tile_is_strip ? 1.0 : 0.0) > 0.5;
     if (all_strips) {
-        io::write_rows(fp, words.data(), g.h, g.w, eng.layout().nw, g.row0);
+        io::write_rows(fp, words.data(), g.h, g.w, nw, g.row0);
         return;
     }
-    // General case (2-D blocks): gather packed tiles to rank 0, assemble, send each rank its strip.
+    // General case (2-D blocks): the dump of rank q is global rows strip_starts[q..q+1) at full width
+    // (the reference's per-rank files, gol-main.c:17-28).  Every tile/strip overlap is one rectangle,
+    // sent point to point from the tile's owner to the strip's owner in ONE exchange (no rank-0
+    // funnel: each rank sends and receives only its own ~h x w cells).
     const i64 gw = g.global_words();
-    std::vector<std::vector<u8>> tiles;
-    t.gatherv(words.data(), words.size() * 8, &tiles, 0);
-    if (r == 0) {
-        std::vector<u64> board((size_t)(d.H * gw), 0);
-        for (int q = 0; q < d.P; ++q) {
-            Geometry gq = make_geometry(d, q);
-            const i64 nwq = ceil_div(gq.w, 64);
-            const u64* src = (const u64*)tiles[q].data();
-            for (i64 rr = 0; rr < gq.h; ++rr)
-                memcpy(&board[(size_t)((gq.row0 + rr) * gw + gq.word0())], src + rr * nwq, (size_t)nwq * 8);
+    const i64 s0 = d.strip_starts[r], s1 = d.strip_starts[r + 1];
+    std::vector<u64> strip((size_t)((s1 - s0) * gw), 0);
+    std::vector<std::vector<u64>> out_blocks, in_blocks;
+    std::vector<Message> sends, recvs;
+    struct InBlock {
+        size_t idx;
+        i64 r0, rows, word0, nwq;
+    };
+    std::vector<InBlock> ins;
+    // what this rank's tile contributes to every strip
+    for (int q = 0; q < d.P; ++q) {
+        const i64 a = std::max(g.row0, d.strip_starts[q]), b = std::min(g.row0 + g.h, d.strip_starts[q + 1]);
+        if (a >= b) continue;
+        if (q == r) {
+            for (i64 rr = a; rr < b; ++rr)
+                memcpy(&strip[(size_t)((rr - s0) * gw + g.word0())], &words[(size_t)((rr - g.row0) * nw)],
+                       (size_t)nw * 8);
+            continue;
         }
-        for (int q = 0; q < d.P; ++q) {
-            const u64* strip = &board[(size_t)(d.strip_starts[q] * gw)];
-            const i64 rows = d.strip_starts[q + 1] - d.strip_starts[q];
-            if (q == 0)
-                io::write_rows(fp, strip, rows, d.W, gw, d.strip_starts[0]);
-            else
-                t.send_bytes(q, strip, (size_t)(rows * gw) * 8);
-        }
-    } else {
-        const i64 rows = d.strip_starts[r + 1] - d.strip_starts[r];
-        std::vector<u64> strip((size_t)(rows * gw));
-        t.recv_bytes(0, strip.data(), strip.size() * 8);
-        io::write_rows(fp, strip.data(), rows, d.W, gw, d.strip_starts[r]);
+        out_blocks.emplace_back(words.begin() + (a - g.row0) * nw, words.begin() + (b - g.row0) * nw);
     }
+    size_t ob = 0;
+    for (int q = 0; q < d.P; ++q) {
+        const i64 a = std::max(g.row0, d.strip_starts[q]), b = std::min(g.row0 + g.h, d.strip_starts[q + 1]);
+        if (a >= b || q == r) continue;
+        sends.push_back({q, out_blocks[ob].data(), out_blocks[ob].size() * 8});
+        ++ob;
+    }
+    // what every other rank's tile contributes to this rank's strip
+    for (int q = 0; q < d.P; ++q) {
+        if (q == r) continue;
+        const Geometry gq = make_geometry(d, q);
+        const i64 a = std::max(gq.row0, s0), b = std::min(gq.row0 + gq.h, s1);
+        if (a >= b) continue;
+        const i64 nwq = ceil_div(gq.w, 64);
+        in_blocks.emplace_back((size_t)((b - a) * nwq));
+        ins.push_back({in_blocks.size() - 1, a, b - a, gq.word0(), nwq});
+        recvs.push_back({q, in_blocks.back().data(), in_blocks.back().size() * 8});
+    }
+    t.exchange_host(sends, recvs);
+    for (const InBlock& ib : ins)
+        for (i64 rr = 0; rr < ib.rows; ++rr)
+            memcpy(&strip[(size_t)((ib.r0 - s0 + rr) * gw + ib.word0)], &in_blocks[ib.idx][(size_t)(rr * ib.nwq)],
+                   (size_t)ib.nwq * 8);
+    io::write_rows(fp, strip.data(), s1 - s0, d.W, gw, s0);
 }
 
 // ---------------------------------------------------------------------------------------------
 // Checkpoints
 // ---------------------------------------------------------------------------------------------
+//
+// One file per checkpoint, independent of the decomposition: a header, then the GLOBAL board as
+// H rows of ceil(W/64) natural-order u64 words (bit b of word c = column 64c+b).  Every rank writes
+// its own rectangle in place (pwrite at its rows' / words' offsets) and, on restart, reads its own
+// rectangle whatever grid wrote the file: a snapshot taken by 8 ranks in 2-D resumes on 1 rank, or
+// on 3 ranks in 1-D.  Rank 0 creates and sizes the file; the other ranks write after a barrier, and
+// rank 0 renames it into place after a second one (a crash leaves only the .tmp file).
 
 namespace {
 struct CkptHeader {
     char magic[8];
-    u64 version, H, W, P, Px, Py, rank, row0, col0, h, w, generation, seed;
+    u64 version, H, W, words_per_row, generation, seed, reserved[2];
 };
-std::string ckpt_name(const std::string& prefix, int rank, int P) {
-    return strprintf("%s.rank%d.of%d.gol", prefix.c_str(), rank, P);
+constexpr u64 kCkptVersion = 2;
+std::string ckpt_name(const std::string& prefix) { return prefix + ".gol"; }
+
+void pwrite_all(int fd, const void* buf, size_t n, off_t off, const std::string& name) {
+    const char* p = (const char*)buf;
+    while (n > 0) {
+        const ssize_t w = pwrite(fd, p, n, off);
+        if (w <= 0) throw Error("cannot write checkpoint " + name);
+        p += w;
+        n -= (size_t)w;
+        off += w;
+    }
+}
+void pread_all(int fd, void* buf, size_t n, off_t off, const std::string& name) {
+    char* p = (char*)buf;
+    while (n > 0) {
+        const ssize_t got = pread(fd, p, n, off);
+        if (got <= 0) throw Error("truncated checkpoint " + name);
+        p += got;
+        n -= (size_t)got;
+        off += got;
+    }
 }
 }  // namespace
 
 void save_checkpoint(Engine& eng, const std::string& prefix, u64 seed) {
     trace::Range range("gol.checkpoint");
     const Geometry& g = eng.geometry();
+    Transport& t = eng.transport();
     std::vector<u64> words = eng.tile_words();
-    CkptHeader hd{};
-    memcpy(hd.magic, "GOLCKPT1", 8);
-    hd = CkptHeader{{'G', 'O', 'L', 'C', 'K', 'P', 'T', '1'}, 1, (u64)g.dec.H, (u64)g.dec.W, (u64)g.dec.P,
-                    (u64)g.dec.Px, (u64)g.dec.Py, (u64)g.rank, (u64)g.row0, (u64)g.col0, (u64)g.h, (u64)g.w,
-                    eng.generation(), seed};
-    std::string name = ckpt_name(prefix, g.rank, g.dec.P), tmp = name + ".tmp";
-    FILE* f = fopen(tmp.c_str(), "wb");
-    if (!f) throw Error("cannot write checkpoint " + tmp);
-    fwrite(&hd, sizeof(hd), 1, f);
-    fwrite(words.data(), 8, words.size(), f);
-    fclose(f);
-    if (rename(tmp.c_str(), name.c_str()) != 0) throw Error("cannot rename checkpoint " + tmp);
-    eng.transport().barrier();
+    const i64 nw = eng.layout().nw, gw = g.global_words();
+    const std::string name = ckpt_name(prefix), tmp = name + ".tmp";
+    u8 ok = 1;
+    if (g.rank == 0) {
+        CkptHeader hd{};
+        memcpy(hd.magic, "GOLCKPT2", 8);
+        hd.version = kCkptVersion;
+        hd.H = (u64)g.dec.H;
+        hd.W = (u64)g.dec.W;
+        hd.words_per_row = (u64)gw;
+        hd.generation = eng.generation();
+        hd.seed = seed;
+        const int fd = open(tmp.c_str(), O_CREAT | O_TRUNC | O_WRONLY, 0644);
+        ok = fd >= 0 && ftruncate(fd, (off_t)(sizeof(hd) + (size_t)(g.dec.H * gw) * 8)) == 0 &&
+             pwrite(fd, &hd, sizeof(hd), 0) == (ssize_t)sizeof(hd);
+        if (fd >= 0) close(fd);
+    }
+    t.broadcast(&ok, 1, 0);
+    if (!ok) throw Error("cannot create checkpoint " + tmp);
+    const int fd = open(tmp.c_str(), O_WRONLY);
+    if (fd < 0) throw Error("cannot open checkpoint " + tmp);
+    const off_t base = (off_t)sizeof(CkptHeader);
+    if (nw == gw) {  // full-width rows: one contiguous write
+        pwrite_all(fd, words.data(), words.size() * 8, base + (off_t)(g.row0 * gw) * 8, tmp);
+    } else {
+        for (i64 r = 0; r < g.h; ++r)
+            pwrite_all(fd, &words[(size_t)(r * nw)], (size_t)nw * 8, base + (off_t)((g.row0 + r) * gw + g.word0()) * 8,
+                       tmp);
+    }
+    if (fsync(fd) != 0) {
+        close(fd);
+        throw Error("cannot flush checkpoint " + tmp);
+    }
+    close(fd);
+    t.barrier();
+    if (g.rank == 0 && rename(tmp.c_str(), name.c_str()) != 0) throw Error("cannot rename checkpoint " + tmp);
+    t.barrier();
 }
 
 u64 load_checkpoint(Engine& eng, const std::string& prefix) {
     const Geometry& g = eng.geometry();
-    std::string name = ckpt_name(prefix, g.rank, g.dec.P);
-    FILE* f = fopen(name.c_str(), "rb");
-    if (!f) throw Error("cannot open checkpoint " + name);
+    const std::string name = ckpt_name(prefix);
+    const int fd = open(name.c_str(), O_RDONLY);
+    if (fd < 0) throw Error("cannot open checkpoint " + name);
     CkptHeader hd{};
-    if (fread(&hd, sizeof(hd), 1, f) != 1 || memcmp(hd.magic, "GOLCKPT1", 8) != 0) {
-        fclose(f);
-        throw Error("bad checkpoint header in " + name);
+    const i64 nw = eng.layout().nw, gw = g.global_words();
+    try {
+        pread_all(fd, &hd, sizeof(hd), 0, name);
+        if (memcmp(hd.magic, "GOLCKPT2", 8) != 0 || hd.version != kCkptVersion)
+            throw Error("bad checkpoint header in " + name);
+        if (hd.H != (u64)g.dec.H || hd.W != (u64)g.dec.W || hd.words_per_row != (u64)gw)
+            throw Error(strprintf("checkpoint %s holds a %llux%llu board, this run has %lldx%lld", name.c_str(),
+                                  (unsigned long long)hd.H, (unsigned long long)hd.W, (long long)g.dec.H,
+                                  (long long)g.dec.W));
+        std::vector<u64> words((size_t)(g.h * nw));
+        const off_t base = (off_t)sizeof(CkptHeader);
+        if (nw == gw) {
+            pread_all(fd, words.data(), words.size() * 8, base + (off_t)(g.row0 * gw) * 8, name);
+        } else {
+            for (i64 r = 0; r < g.h; ++r)
+                pread_all(fd, &words[(size_t)(r * nw)], (size_t)nw * 8,
+                          base + (off_t)((g.row0 + r) * gw + g.word0()) * 8, name);
+        }
+        close(fd);
+        eng.set_tile_words(words);
+    } catch (...) {
+        close(fd);
+        throw;
     }
-    if (hd.H != (u64)g.dec.H || hd.W != (u64)g.dec.W || hd.P != (u64)g.dec.P || hd.row0 != (u64)g.row0 ||
-        hd.col0 != (u64)g.col0 || hd.h != (u64)g.h || hd.w != (u64)g.w) {
-        fclose(f);
-        throw Error("checkpoint " + name + " was written for a different board or decomposition");
-    }
-    std::vector<u64> words((size_t)(g.h * ceil_div(g.w, 64)));
-    size_t got = fread(words.data(), 8, words.size(), f);
-    fclose(f);
-    if (got != words.size()) throw Error("truncated checkpoint " + name);
-    eng.set_tile_words(words);
     return hd.generation;
 }
 

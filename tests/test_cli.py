@@ -172,6 +172,44 @@ def test_checkpoint_restart(gol_bin, tmp_path):
         assert (a / f"Rank_{q}_of_{P}.txt").read_text() == (b / f"Rank_{q}_of_{P}.txt").read_text()
 
 
+@pytest.mark.parametrize("restart_env,P2", [({}, 1), ({}, 3), ({"GOL_DECOMP": "2d", "GOL_GRID": "3x2"}, 6)])
+def test_checkpoint_any_decomposition(gol_bin, tmp_path, restart_env, P2):
+    """A checkpoint is the global board: written by a 2x2 grid, resumed on 1 rank, 3 strips or a 3x2 grid."""
+    N = 192
+    a = tmp_path / "a"
+    b = tmp_path / "b"
+    a.mkdir()
+    b.mkdir()
+    ck = str(tmp_path / "ck")
+    r = run(gol_bin, [5, N, 16, 256, 0], a, nranks=4, env={"GOL_GLOBAL": "1", "GOL_DECOMP": "2d", "GOL_GRID": "2x2",
+                                                          "GOL_CHECKPOINT_EVERY": "8", "GOL_CHECKPOINT_PATH": ck})
+    assert r.returncode == 0, r.stderr
+    assert os.path.exists(ck + ".gol") and not os.path.exists(ck + ".gol.tmp")
+    r2 = run(gol_bin, [5, N, 21, 256, 1], b, nranks=P2, env={"GOL_GLOBAL": "1", "GOL_RESTART": ck, **restart_env})
+    assert r2.returncode == 0, r2.stderr
+    # the restarted run did the remaining 5 generations
+    assert r2.stdout.startswith("TOTAL DURATION") and f"number of cell updates = {N * N * 5}" in r2.stdout
+    assert np.array_equal(load_board(b, P2), numpy_step(initial_board(5, N, 1, False), 21))
+
+
+def test_checkpoint_rejects_other_board(gol_bin, tmp_path):
+    ck = str(tmp_path / "ck")
+    r = run(gol_bin, [5, 64, 8, 256, 0], tmp_path, env={"GOL_CHECKPOINT_EVERY": "8", "GOL_CHECKPOINT_PATH": ck})
+    assert r.returncode == 0, r.stderr
+    r2 = run(gol_bin, [5, 128, 8, 256, 0], tmp_path, env={"GOL_RESTART": ck})
+    assert r2.returncode != 0 and "holds a 64x64 board" in r2.stderr
+
+
+@pytest.mark.parametrize("grid,P", [("3x2", 6), ("2x4", 8), ("4x1", 4)])
+def test_2d_dumps_point_to_point(gol_bin, tmp_path, grid, P):
+    """2-D dumps: tile/strip overlaps routed point to point (strips cut across several tile rows)."""
+    N, gens = 256, 9
+    r = run(gol_bin, [5, N, gens, 256, 1], tmp_path, nranks=P,
+            env={"GOL_GLOBAL": "1", "GOL_DECOMP": "2d", "GOL_GRID": grid})
+    assert r.returncode == 0, r.stderr
+    assert np.array_equal(load_board(tmp_path, P), numpy_step(initial_board(5, N, 1, False), gens))
+
+
 def test_fault_injection_aborts_all_ranks(gol_bin, tmp_path):
     r = run(gol_bin, [5, 64, 40, 256, 0], tmp_path, nranks=3, env={"GOL_FAULT": "1:16"})
     assert r.returncode == 3
