@@ -33,10 +33,12 @@ def main() -> int:
     ap.add_argument("--steps", type=int, default=4000, help="timed generations")
     ap.add_argument("--warmup", type=int, default=400, help="untimed generations")
     ap.add_argument("--size", type=int, default=32768, help="tile side per GPU (weak) / board side (strong)")
+    ap.add_argument("--width", type=int, default=0,
+                    help="board columns (0 = --size: square); e.g. one GPU holding another config's per-rank tile")
     ap.add_argument("--scaling", choices=["weak", "strong"], default="weak")
     ap.add_argument("--decomp", default="1d", help="1d | 2d | auto")
     ap.add_argument("--halo-depth", type=int, default=int(os.environ.get("GOL_HALO_DEPTH", "0")),
-                    help="generations per halo exchange (0 = auto: 32; 64 for tall multi-GPU strips)")
+                    help="generations per halo exchange (0 = auto: 32; 64 / 56 for multi-GPU strips / 2-D tiles of >= 2048 rows)")
     ap.add_argument("--kernel-depth", type=int, default=int(os.environ.get("GOL_KERNEL_DEPTH", "0")),
                     help="generations per kernel pass (0 = auto)")
     ap.add_argument("--kernel", default=os.environ.get("GOL_KERNEL", "auto"),
@@ -111,6 +113,7 @@ def main() -> int:
         device=local if backend == "hip" else None,
         run_hint=steps,  # the timed run replays one captured graph (graph boundaries idle the GPU)
         self_exchange=args.self_exchange,
+        width=args.width if have_gpu else 0,
     )
     sim.init(pattern=5, seed=args.seed)
     dec = sim.decomposition

@@ -58,8 +58,10 @@ struct Decomposition {
 };
 
 // N: CLI worldSize.  grid: "" / "auto" / "PxxPy" (e.g. "4x2").  decomp: "1d" / "2d" / "auto".
+// width: board columns (0 = N, the reference's square tiles; the CLI is always square).  Per-rank
+// mode: every rank's strip is N rows; global mode: the board is N rows x width columns.
 Decomposition make_decomposition(i64 N, int P, bool global_mode, const std::string& decomp,
-                                 const std::string& grid);
+                                 const std::string& grid, i64 width = 0);
 
 // This rank's view: tile extent, offsets and neighbours.
 struct Geometry {

@@ -29,6 +29,7 @@ enum : u32 {
                             // kernel gets x-wrap from its plan (build_plan(..., xwrap = true))
     STEP_WRAP_Y = 1u << 1,  // tile is its own N/S neighbour: rows are read modulo h, no ghost rows
     STEP_TILE_L2 = 1u << 4, // tile kernel: two generations per LDS pass (half the barriers)
+    STEP_TILE_L4 = 1u << 6, // tile kernel: four generations per LDS pass
     STEP_SEAM = 1u << 5,    // temporal kernel: rows < 0 are read from StepParams::above, rows >= h
                             // from StepParams::below (sub-tile first pass: the other half's edges)
 };

@@ -132,7 +132,7 @@ PYBIND11_MODULE(_gol, m) {
         .def("two_d", &Decomposition::two_d)
         .def("describe", &Decomposition::describe);
     m.def("make_decomposition", &make_decomposition, py::arg("N"), py::arg("P"), py::arg("global_mode") = false,
-          py::arg("decomp") = "1d", py::arg("grid") = "");
+          py::arg("decomp") = "1d", py::arg("grid") = "", py::arg("width") = 0);
 
     py::class_<Geometry>(m, "Geometry")
         .def_readonly("dec", &Geometry::dec)

@@ -54,13 +54,14 @@ static void choose_grid(int P, i64 H, i64 W, int& Px, int& Py) {
 }
 
 Decomposition make_decomposition(i64 N, int P, bool global_mode, const std::string& decomp,
-                                 const std::string& grid) {
+                                 const std::string& grid, i64 width) {
     if (P < 1) throw Error("number of ranks must be >= 1");
     if (N < 1) throw Error(strprintf("world size must be >= 1 (got %lld)", (long long)N));
+    if (width < 0) throw Error(strprintf("board width must be >= 1 (got %lld)", (long long)width));
     Decomposition d;
     d.P = P;
     d.per_rank = !global_mode;
-    d.W = N;
+    d.W = width > 0 ? width : N;
     d.H = global_mode ? N : N * (i64)P;
     if (global_mode && d.H < P) throw Error("global board has fewer rows than ranks");
 

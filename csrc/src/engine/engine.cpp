@@ -25,14 +25,19 @@ Engine::Engine(const Geometry& g, const EngineConfig& c, std::shared_ptr<Transpo
         throw Error(strprintf("transport (rank %d of %d) does not match the geometry (rank %d of %d)", t_->rank(),
                               t_->size(), g_.rank, g_.dec.P));
     // auto depth: 32 generations per superstep (the tile-kernel autotune tries passes of up to 32
-    // on one rank), 64 for 1-D strips of >= 8192 rows with neighbours: half the exchanges and
-    // cross-stream events per generation for < 0.5% of ghost-row recompute; measured +1.7% on the
-    // eager multi-GPU schedule, docs/PERFORMANCE.md.
+    // on one rank); with neighbours (or self-exchange, which stands in for them on one GPU), 64 for
+    // 1-D strips of >= 2048 rows and 56 for 2-D tiles of >= 2048 rows (the column halo is one word:
+    // <= 63): an exchange costs an RCCL kernel plus ~15 us of cross-stream event latency however
+    // small it is (kernel traces of the 4096 x 32768 strip of config 3 strong-scaled over 8 GPUs:
+    // 11-13 us RCCL + 14 us event wait per superstep, profiles/), while the ghost rows a deeper
+    // superstep recomputes cost < 1.5% at 2048 rows.
     // The HIP backend runs a superstep as kernel passes of K (auto 8) generations (deep halos).
     // (from the average strip height, identical on every rank: all ranks must cut the same
     // supersteps, and uneven strips differ by a row)
     const i64 strip_rows = g_.dec.H / std::max(1, g_.dec.Py);
-    const bool tall_strips = !two_d() && strip_rows >= 8192;
+    const bool nbrs = g_.dec.P > 1 || xchg_self_;
+    const bool tall_strips = nbrs && !two_d() && strip_rows >= 2048;
+    const bool tall_tiles = nbrs && two_d() && strip_rows >= 2048;
     // ... and 64 when the two-sub-tile mode can run (HIP, GOL_SUBTILES auto or 2, 1-D tiles of >=
     // 24576 rows, aligned width, no measurement / watchdog / compat mode, and a transport whose
     // exchange it can drive): it synchronises its two streams once per superstep, so longer
@@ -41,7 +46,7 @@ Engine::Engine(const Geometry& g, const EngineConfig& c, std::shared_ptr<Transpo
     const bool sub_tall = cfg_.backend == "hip" && (cfg_.subtiles == 2 || cfg_.subtiles < 0) && !two_d() && strip_rows >= kSubtileMinRows &&
                           g_.dec.W % 64 == 0 && !cfg_.force_split && !cfg_.profile && cfg_.watchdog_s <= 0 &&
                           !cfg_.compat && cfg_.kernel != "lds" && cfg_.kernel != "tile" && sub_transport;
-    const int want = cfg_.halo_depth > 0 ? cfg_.halo_depth : ((g_.dec.P > 1 && tall_strips) || sub_tall ? 64 : 32);
+    const int want = cfg_.halo_depth > 0 ? cfg_.halo_depth : (tall_strips || sub_tall ? 64 : (tall_tiles ? 56 : 32));
     int R = clamp_halo_depth(g_.dec, want);
     if (two_d()) R = std::min(R, 63);  // the column halo is one 64-cell word
     if (cfg_.compat) {

@@ -93,7 +93,7 @@ class HipEngine : public Engine {
         tdepth_ = supported_kernel_depth(std::min(K, hipk::max_step_depth()));
         if (R != L_.R) L_ = Layout(L_.h, L_.w, R);
         stats_.depth = R;
-        // slack rows: the temporal kernel prefetches 3 rows past a segment's last input row
+        // slack rows: the temporal kernel prefetches 3 (shallow passes: 6) rows past a segment's last input row
         const size_t bytes = (size_t)(L_.words() + hipk::kSlackRows * L_.pitch) * 8;
         for (int i = 0; i < 2; ++i) HIP_CHECK(hipMalloc(&buf_[i], bytes));
         alloc_bytes_ = bytes;
@@ -517,27 +517,35 @@ class HipEngine : public Engine {
             HIP_CHECK(hipStreamWaitEvent(s_comm_, ev_sub_a_, 0));  // half 0's previous superstep is done
         }
         const std::vector<int>& ps = pass_depths(k);
+        hipk::StepParams sp[2], sp0[2];
         for (int s = 0; s < 2; ++s) {
             const Layout& Ls = sub_L_[s];
             const int o = 1 - s;  // the other half
-            hipk::StepParams sp{Ls.pitch, (i32)Ls.h, (i32)Ls.nw, Ls.R, sub_flags()};
-            hipk::StepParams sp0 = sp;
-            sp0.flags |= hipk::STEP_SEAM;
+            sp[s] = hipk::StepParams{Ls.pitch, (i32)Ls.h, (i32)Ls.nw, Ls.R, sub_flags()};
+            sp0[s] = sp[s];
+            sp0[s].flags |= hipk::STEP_SEAM;
             // rows above half 0 / below half 1: the rank's ghost rows (exchanged) or, on a torus
             // without neighbours, the other half's far edge; between the halves: the other's edge
             const bool wrap = self_y();
-            sp0.above = s == 0 ? (wrap ? sub_rows(o, p, sub_L_[o].h) : sub_rows(s, p, 0)) : sub_rows(o, p, h0);
-            sp0.below = s == 1 ? (wrap ? sub_rows(o, p, 0) : sub_rows(s, p, h1)) : sub_rows(o, p, 0);
-            int q = p;
-            for (size_t j = 0; j < ps.size(); ++j) {
-                const int dsti = (j % 2 == 0) ? a : b;
-                const DevPlan& pl = sub_plan(s, ps[j], ext_after(ps, j));
-                hipk::launch_step(ps[j], sub_buf_[s][q], sub_buf_[s][dsti], pl.d, pl.waves, j == 0 ? sp0 : sp,
-                                  s ? s_comm_ : s_comp_);
-                q = dsti;
-            }
-            HIP_CHECK(hipEventRecord(s ? ev_sub_b_ : ev_sub_a_, s ? s_comm_ : s_comp_));
+            sp0[s].above = s == 0 ? (wrap ? sub_rows(o, p, sub_L_[o].h) : sub_rows(s, p, 0)) : sub_rows(o, p, h0);
+            sp0[s].below = s == 1 ? (wrap ? sub_rows(o, p, 0) : sub_rows(s, p, h1)) : sub_rows(o, p, 0);
         }
+        // Launches alternate between the halves (pass j of half 0, pass j of half 1, ...): issued half
+        // by half, the second stream's first kernel started ~18 us after the first's (three host
+        // launches later), and the superstep ended on one half's lone tail (kernel trace of the
+        // driver's 20-generation bench, profiles/).
+        int q = p;
+        for (size_t j = 0; j < ps.size(); ++j) {
+            const int dsti = (j % 2 == 0) ? a : b;
+            for (int s = 0; s < 2; ++s) {
+                const DevPlan& pl = sub_plan(s, ps[j], ext_after(ps, j));
+                hipk::launch_step(ps[j], sub_buf_[s][q], sub_buf_[s][dsti], pl.d, pl.waves, j == 0 ? sp0[s] : sp[s],
+                                  s ? s_comm_ : s_comp_);
+            }
+            q = dsti;
+        }
+        HIP_CHECK(hipEventRecord(ev_sub_a_, s_comp_));
+        HIP_CHECK(hipEventRecord(ev_sub_b_, s_comm_));
         HIP_CHECK(hipGetLastError());
         sub_cur_ = (ps.size() % 2) ? a : b;
     }
@@ -970,6 +978,10 @@ class HipEngine : public Engine {
                 launch(0, ps[j], e, buf_[cur_], buf_[cur_ ^ 1], s_comp_);
                 post(buf_[cur_ ^ 1], s_comp_, e);
             }
+            // the next exchange waits for the whole superstep, as in tile_superstep (without this
+            // record the timed split schedule overlapped each exchange with the previous superstep's
+            // later passes, which a real run cannot: 2.78 timed vs 3.26 us/gen run, 4096 x 32768)
+            if (ps.size() > 1) mark_ready();
         }
         split_ = false;
     }
@@ -1012,7 +1024,12 @@ class HipEngine : public Engine {
         u32 f = 0;
         if (self_y() && !cfg_.compat) f |= hipk::STEP_WRAP_Y;
         if (xwrap_by_plan()) f |= hipk::STEP_WRAP_X;
-        if (tile_l2_) f |= hipk::STEP_TILE_L2;  // tile kernel: 2 generations per LDS pass
+        // tile kernel: generations per LDS pass (GOL_TILE_LEVELS 1, 2 or 4; default 4 for workgroups
+        // of <= 8 waves, 2 above: kbench 8192^2 / 16384^2, K 16-32, 8 waves: 4 levels 0.4-2% faster,
+        // 16 waves: 3-7% slower, profiles/tile_levels_ab.txt)
+        const int lv = tile_lv_ > 0 ? tile_lv_ : (cfg_.tile_waves <= 8 ? 4 : 2);
+        if (lv == 2) f |= hipk::STEP_TILE_L2;
+        if (lv == 4) f |= hipk::STEP_TILE_L4;
         return f;
     }
 
@@ -1469,7 +1486,7 @@ class HipEngine : public Engine {
     // occupancy).  Small tiles pay (K+1)/S of vertical halo with S rows per wave, so fewer, taller
     // waves can win there; the autotuner tries 2 per SIMD against the full occupancy (3 at K=8).
     int occ_ = 0;
-    bool tile_l2_ = env_int("GOL_TILE_LEVELS", 2) == 2;  // tile kernel: generations per LDS pass
+    int tile_lv_ = (int)env_int("GOL_TILE_LEVELS", 0);  // tile kernel: generations per LDS pass (1, 2, 4; 0 auto)
     bool multipass_ = false;
     std::map<int, std::vector<int>> passes_;
     bool split_ = false;   // superstep schedule: interior/boundary split with overlapped exchange

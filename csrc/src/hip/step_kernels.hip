@@ -116,8 +116,21 @@ __device__ __forceinline__ bool advance(Pipe<K>& P, u32& lo, u32& hi, int i) {
 //               in place (and the torus wrap), so no seam copy precedes it
 enum { ROWS_GHOST = 0, ROWS_WRAP = 1, ROWS_SEAM = 2 };
 
+// Prefetch depth in rows.  Deep passes (K >= 5) are VALU bound and keep one row-triple in flight
+// (registers are what limits their occupancy).  Shallow passes are memory bound: a whole-board pass
+// at K <= 4 costs ~70 us at 32768^2 whatever K is, i.e. ~3.8 TB/s, limited by the bytes each wave
+// keeps in flight, so they prefetch two row-triples ahead (GOL_SHALLOW_PF=0 at build time: one).
+#ifndef GOL_SHALLOW_PF
+#define GOL_SHALLOW_PF 1
+#endif
+template <int K>
+constexpr int prefetch_rows() {
+    return (GOL_SHALLOW_PF && K <= 4) ? 6 : 3;
+}
+
 template <int K, int ROWS>
 struct WaveRunner {
+    static constexpr int D = prefetch_rows<K>();
     const StepParams& p;
     const LaneDesc& d;
     const int n;   // row iterations: nrows + 2K
@@ -127,7 +140,7 @@ struct WaveRunner {
     uint2* st;
     i64 st_stride;  // pitch for output lanes, 0 for halo/idle lanes (they write a trash slot)
     int lrow;       // tile row of the next load (ROWS_WRAP, ROWS_SEAM; wave-uniform)
-    uint2 pf[3];
+    uint2 pf[D];
     Pipe<K> P;
 
     __device__ __forceinline__ void next_row() {
@@ -163,19 +176,26 @@ struct WaveRunner {
         const i64 srow = out ? (i64)(d.row0 + p.R) : (i64)(p.h + 2 * p.R + kSlackRows - 1);
         st = reinterpret_cast<uint2*>(dst + srow * p.pitch + (d.col + 1));
         st_stride = out ? p.pitch : 0;
-        pf[0] = *ld;
-        next_row();
-        pf[1] = *ld;
-        next_row();
-        pf[2] = *ld;
-        next_row();
+#pragma unroll
+        for (int j = 0; j < D; ++j) {
+            pf[j] = *ld;
+            next_row();
+        }
     }
 
     // Next input row (lo, hi) in order.
     template <int PH>
     __device__ __forceinline__ void fetch(u32& lo, u32& hi) {
-        const uint2 x = pf[PH];
-        pf[PH] = *ld;  // prefetch 3 rows ahead (the allocation has slack rows past the halo)
+        uint2 x;
+        if constexpr (D == 3) {
+            x = pf[PH];
+            pf[PH] = *ld;  // prefetch 3 rows ahead (the allocation has slack rows past the halo)
+        } else {
+            x = pf[0];  // a queue of D rows (the shift is register renaming in the unrolled code)
+#pragma unroll
+            for (int j = 0; j + 1 < D; ++j) pf[j] = pf[j + 1];
+            pf[D - 1] = *ld;
+        }
         next_row();
         lo = x.x;
         hi = x.y;
@@ -207,12 +227,13 @@ struct WaveRunner {
         for (; i + 3 <= n; i += 3) {
             // hoist the whole next triple's loads above this triple's compute
             const uint2 x0 = pf[0], x1 = pf[1], x2 = pf[2];
-            pf[0] = *ld;
-            next_row();
-            pf[1] = *ld;
-            next_row();
-            pf[2] = *ld;
-            next_row();
+#pragma unroll
+            for (int j = 0; j + 3 < D; ++j) pf[j] = pf[j + 3];
+#pragma unroll
+            for (int j = D - 3; j < D; ++j) {
+                pf[j] = *ld;
+                next_row();
+            }
             __builtin_amdgcn_sched_barrier(0);
             compute_store<0, false>(x0.x, x0.y, i);
             compute_store<1, false>(x1.x, x1.y, i + 1);
@@ -309,24 +330,34 @@ __device__ __forceinline__ void tile_band(const u32* __restrict__ in, int n, Ban
             GOL_TILE_ROW(2, true, i + 2)
         }
     }
+    // Steady state, software-pipelined: the next triple's LDS reads are issued before this triple's
+    // compute, so their latency hides behind it (a workgroup of 8 waves leaves 2 waves per SIMD,
+    // too few to hide it by switching waves: 35% of wave time was s_waitcnt, PMC at 8192^2).  The
+    // last prefetch reads up to 3 rows past the band: still inside the tile buffers or the LDS slack
+    // rows (tile_lds_bytes), and never used.
+    u32 l0 = in[i * kTileRowU32 + lane], h0 = in[i * kTileRowU32 + 64 + lane];
+    u32 l1 = in[(i + 1) * kTileRowU32 + lane], h1 = in[(i + 1) * kTileRowU32 + 64 + lane];
+    u32 l2 = in[(i + 2) * kTileRowU32 + lane], h2 = in[(i + 2) * kTileRowU32 + 64 + lane];
     for (; i + 3 <= n; i += 3) {
-        // hoist the triple's LDS reads above its compute (stores to the other buffer do not alias)
-        const u32 l0 = in[i * kTileRowU32 + lane], h0 = in[i * kTileRowU32 + 64 + lane];
-        const u32 l1 = in[(i + 1) * kTileRowU32 + lane], h1 = in[(i + 1) * kTileRowU32 + 64 + lane];
-        const u32 l2 = in[(i + 2) * kTileRowU32 + lane], h2 = in[(i + 2) * kTileRowU32 + 64 + lane];
+        const u32 a0 = l0, b0 = h0, a1 = l1, b1 = h1, a2 = l2, b2 = h2;
+        l0 = in[(i + 3) * kTileRowU32 + lane], h0 = in[(i + 3) * kTileRowU32 + 64 + lane];
+        l1 = in[(i + 4) * kTileRowU32 + lane], h1 = in[(i + 4) * kTileRowU32 + 64 + lane];
+        l2 = in[(i + 5) * kTileRowU32 + lane], h2 = in[(i + 5) * kTileRowU32 + 64 + lane];
         __builtin_amdgcn_sched_barrier(0);
-        lo = l0, hi = h0;
+        lo = a0, hi = b0;
         if (advance<LV, 0, false>(P, lo, hi, i)) out.put(lo, hi);
-        lo = l1, hi = h1;
+        lo = a1, hi = b1;
         if (advance<LV, 1, false>(P, lo, hi, i + 1)) out.put(lo, hi);
-        lo = l2, hi = h2;
+        lo = a2, hi = b2;
         if (advance<LV, 2, false>(P, lo, hi, i + 2)) out.put(lo, hi);
     }
     if (i < n) {
-        GOL_TILE_ROW(0, false, i)
+        lo = l0, hi = h0;
+        if (advance<LV, 0, false>(P, lo, hi, i)) out.put(lo, hi);
     }
     if (i + 1 < n) {
-        GOL_TILE_ROW(1, false, i + 1)
+        lo = l1, hi = h1;
+        if (advance<LV, 1, false>(P, lo, hi, i + 1)) out.put(lo, hi);
     }
 #undef GOL_TILE_ROW
 }
@@ -355,6 +386,23 @@ __device__ __forceinline__ void tile_pass(const u32* A, u32* B, u64* dst, const 
     }
 }
 
+#ifdef GOL_TILE_STAMPS
+// Diagnostic build only (tools/kbench with -DGOL_TILE_STAMPS): s_memtime stamps per workgroup at
+// the kernel start, after the staging barrier and after every LDS pass, for a time breakdown.
+constexpr int kStampSlots = 48, kStampSlotsLast = kStampSlots - 1;
+__device__ unsigned long long g_tile_stamps[4096 * kStampSlots];
+__device__ __forceinline__ void tile_stamp(int wv, int lane, int slot) {
+    unsigned long long t;
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+    __builtin_amdgcn_sched_barrier(0);
+    if (wv == 0 && lane == 0 && blockIdx.x < 4096 && slot < kStampSlots) g_tile_stamps[blockIdx.x * kStampSlots + slot] = t;
+}
+#define GOL_STAMP(slot) tile_stamp(wv, lane, (slot))
+#else
+#define GOL_STAMP(slot) ((void)0)
+#endif
+
 template <int NW, bool WRAPY, int LV>
 __global__ __launch_bounds__(64 * NW) void step_tile(const u64* __restrict__ src, u64* __restrict__ dst,
                                                      const LaneDesc* __restrict__ plan, StepParams p, int K) {
@@ -364,6 +412,7 @@ __global__ __launch_bounds__(64 * NW) void step_tile(const u64* __restrict__ src
     const LaneDesc d = plan[(i64)blockIdx.x * kWaveLanes + lane];
     const int nrows = __builtin_amdgcn_readfirstlane(d.nrows);
     if (nrows <= 0) return;  // padding tile (uniform over the workgroup)
+    GOL_STAMP(0);
     const int n_in = nrows + 2 * K;
     u32* A = tile_lds;
     u32* B = tile_lds + n_in * kTileRowU32;
@@ -379,23 +428,37 @@ __global__ __launch_bounds__(64 * NW) void step_tile(const u64* __restrict__ src
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
+    GOL_STAMP(1);
+    int npass = 0;
+    (void)npass;
 
-    // 2. K generations in passes of LV (a final odd generation runs a one-level pass); the pass
-    // starting at generation g computes tile rows [g+lv, n_in-g-lv)
+    // 2. K generations in LDS passes of up to LV levels (the last passes take what is left); the pass
+    // starting at generation g with lv levels computes tile rows [g+lv, n_in-g-lv).  More levels per
+    // pass: more independent work per wave (the level pipeline) and fewer barriers, at 2*lv rows of
+    // band overlap per wave.
     for (int g = 0; g < K;) {
-        const int lv = (LV == 2 && g + 2 <= K) ? 2 : 1;
-        if (lv == 2)
-            tile_pass<NW, (LV == 2 ? 2 : 1)>(A, B, dst, d, p, K, g, n_in, wv, lane);
-        else
+        const int left = K - g;
+        int lv = 1;
+        if (LV >= 4 && left >= 4) {
+            lv = 4;
+            tile_pass<NW, (LV >= 4 ? 4 : 1)>(A, B, dst, d, p, K, g, n_in, wv, lane);
+        } else if (LV >= 2 && left >= 2) {
+            lv = 2;
+            tile_pass<NW, (LV >= 2 ? 2 : 1)>(A, B, dst, d, p, K, g, n_in, wv, lane);
+        } else {
             tile_pass<NW, 1>(A, B, dst, d, p, K, g, n_in, wv, lane);
+        }
         g += lv;
+        ++npass;
         if (g < K) {
             __syncthreads();
+            GOL_STAMP(1 + npass);
             u32* t = A;
             A = B;
             B = t;
         }
     }
+    GOL_STAMP(kStampSlotsLast);
 }
 
 // LDS bytes of a tile with `rows` output rows at depth k (+4 rows of over-read slack).
@@ -403,6 +466,8 @@ inline size_t tile_lds_bytes(i64 rows, int k) { return (size_t)(2 * (rows + 2 * 
 
 template <int NW>
 const void* tile_kernel(u32 flags) {
+    if (flags & STEP_TILE_L4)
+        return (flags & STEP_WRAP_Y) ? (const void*)step_tile<NW, true, 4> : (const void*)step_tile<NW, false, 4>;
     if (flags & STEP_TILE_L2)
         return (flags & STEP_WRAP_Y) ? (const void*)step_tile<NW, true, 2> : (const void*)step_tile<NW, false, 2>;
     return (flags & STEP_WRAP_Y) ? (const void*)step_tile<NW, true, 1> : (const void*)step_tile<NW, false, 1>;
@@ -513,8 +578,9 @@ i64 tile_max_rows(int k) {
 static const void* tile_kernel_checked(int nw_per_wg, u32 flags) {
     const void* f = tile_kernel_for(nw_per_wg, flags);
     if (!f) throw Error(strprintf("step_tile: unsupported waves per workgroup %d (4, 8 or 16)", nw_per_wg));
-    static bool attr_set[64] = {};
-    const int key = ((nw_per_wg & 15) * 2 + ((flags & STEP_WRAP_Y) ? 1 : 0)) * 2 + ((flags & STEP_TILE_L2) ? 1 : 0);
+    static bool attr_set[128] = {};
+    const int lvk = (flags & STEP_TILE_L4) ? 2 : ((flags & STEP_TILE_L2) ? 1 : 0);
+    const int key = ((nw_per_wg & 15) * 2 + ((flags & STEP_WRAP_Y) ? 1 : 0)) * 3 + lvk;
     if (!attr_set[key]) {  // allow the full 160 KiB of dynamic LDS
         hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kMaxLdsBytes);
         if (e != hipSuccess) throw Error(strprintf("step_tile: hipFuncSetAttribute: %s", hipGetErrorString(e)));
@@ -545,6 +611,12 @@ void launch_step_tile(int nw_per_wg, int k, const u64* src, u64* dst, const Lane
     hipError_t e = hipLaunchKernel(f, dim3((unsigned)n_tiles), dim3(64 * nw_per_wg), args, tile_lds_bytes(rows, k), s);
     if (e != hipSuccess) throw Error(strprintf("step_tile launch failed: %s", hipGetErrorString(e)));
 }
+
+#ifdef GOL_TILE_STAMPS
+void read_tile_stamps(unsigned long long* out, size_t n) {
+    (void)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_tile_stamps), n * sizeof(unsigned long long));
+}
+#endif
 
 void launch_step_lds(const u64* src, u64* dst, const Layout& L, i64 r0, i64 r1, u32 flags, hipStream_t s) {
     if (r1 <= r0) return;

@@ -57,10 +57,13 @@ class Simulation:
     transport:    a ``_gol.Transport``; defaults to a single-rank transport.  See
                   :mod:`gol_amd.parallel` for torch.distributed / RCCL / thread transports.
     backend:      ``"hip"``, ``"cpu"`` or ``"auto"``.
-    halo_depth:   generations per halo exchange (<= 64; 0 = auto: 16 on one rank, 32 with neighbours, 64 for 1-D strips of >= 8192 rows).
+    halo_depth:   generations per halo exchange (<= 128 in 1-D, <= 63 in 2-D; 0 = auto: 32, with
+                  neighbours 64 for 1-D strips / 56 for 2-D tiles of >= 2048 rows).
     kernel_depth: generations per kernel pass (HIP; 0 = auto).  A superstep of halo_depth
                   generations runs as several kernel passes in 1-D (communication-avoiding halos).
     decomp/grid:  ``"1d"`` row strips (reference) or ``"2d"`` blocks, optional ``"PxxPy"`` grid.
+    width:        board columns (0 = N: the reference's square tiles).  With ``width`` the per-rank
+                  strip (or, in global mode, the board) is N rows x ``width`` columns.
     compat:       reproduce the reference's halo quirks (frozen gen-0 halos, P<=2 swap).
     watchdog:     seconds without progress before the job is aborted (0 = off; GOL_WATCHDOG).
     """
@@ -92,11 +95,12 @@ class Simulation:
         sub_occ: int = int(os.environ.get("GOL_SUB_OCC", "2")),
         self_exchange: bool = os.environ.get("GOL_SELF_EXCHANGE", "0") == "1",
         subtiles: int = -1 if os.environ.get("GOL_SUBTILES", "auto") == "auto" else int(os.environ["GOL_SUBTILES"]),
+        width: int = 0,
     ):
         self.transport = transport if transport is not None else _gol.SelfTransport()
         P, rank = self.transport.size(), self.transport.rank()
         self.backend = default_backend() if backend == "auto" else backend
-        self.decomposition = _gol.make_decomposition(N, P, global_mode, decomp, grid)
+        self.decomposition = _gol.make_decomposition(N, P, global_mode, decomp, grid, int(width))
         self.geometry = _gol.make_geometry(self.decomposition, rank)
         cfg = _gol.EngineConfig()
         cfg.backend = self.backend
@@ -188,7 +192,13 @@ class Simulation:
         return path
 
     def checkpoint(self, prefix: str) -> None:
+        """Write ``<prefix>.gol`` (collective): the global board, each rank writing its own rectangle.
+
+        The file does not depend on the decomposition: :meth:`restore` works on any rank count or
+        grid with the same global board size.
+        """
         _gol.save_checkpoint(self.engine, prefix, self.pattern.seed if self.pattern else 0)
 
     def restore(self, prefix: str) -> int:
+        """Load this rank's rectangle of ``<prefix>.gol``; returns the snapshot's generation."""
         return int(_gol.load_checkpoint(self.engine, prefix))

@@ -12,6 +12,6 @@ from .dist import (  # noqa: F401
 from .._native import _gol as _native
 
 
-def decomposition(N: int, P: int, global_mode: bool = False, decomp: str = "1d", grid: str = ""):
-    """The native decomposition (tile extents per rank, process grid, dump strips)."""
-    return _native.make_decomposition(N, P, global_mode, decomp, grid)
+def decomposition(N: int, P: int, global_mode: bool = False, decomp: str = "1d", grid: str = "", width: int = 0):
+    """The native decomposition (tile extents per rank, process grid, dump strips); width 0 = square."""
+    return _native.make_decomposition(N, P, global_mode, decomp, grid, width)

@@ -64,7 +64,8 @@ def _run_threads(gol, N, P, gens, **kw):
         t.start()
     for t in th:
         t.join()
-    dec = gol.parallel.decomposition(N, P, kw.get("global_mode", False), kw.get("decomp", "1d"), kw.get("grid", ""))
+    dec = gol.parallel.decomposition(N, P, kw.get("global_mode", False), kw.get("decomp", "1d"), kw.get("grid", ""),
+                                     kw.get("width", 0))
     full = np.zeros((dec.H, dec.W), np.uint8)
     for r0, c0, b in boards:
         full[r0 : r0 + b.shape[0], c0 : c0 + b.shape[1]] = b
@@ -79,6 +80,20 @@ def test_thread_ranks(gol, P, kw):
     full, fps = _run_threads(gol, N, P, gens, **kw)
     per_rank = not kw.get("global_mode", False)
     assert np.array_equal(full, numpy_step(initial_board(5, N, P, per_rank, 99), gens))
+    assert len(set(fps)) == 1
+
+
+@pytest.mark.parametrize("P,kw", [(1, {"width": 200}), (3, {"width": 130}), (1, {"width": 64 * 5, "global_mode": True}),
+                                  (4, {"width": 64 * 6, "decomp": "2d", "grid": "2x2", "global_mode": True})])
+def test_rectangular_boards(gol, P, kw):
+    """Boards of N rows x `width` columns (per-rank strips or global boards) vs the numpy torus."""
+    from gol_amd.ops.oracle import random_board
+
+    N, gens = 96, 13
+    full, fps = _run_threads(gol, N, P, gens, **kw)
+    H = N if kw.get("global_mode") else N * P
+    assert full.shape == (H, kw["width"])
+    assert np.array_equal(full, numpy_step(random_board(H, kw["width"], 99), gens))
     assert len(set(fps)) == 1
 
 

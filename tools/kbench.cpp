@@ -26,6 +26,14 @@ using namespace gol;
         }                                                                       \
     } while (0)
 
+#ifdef GOL_TILE_STAMPS
+namespace gol {
+namespace hipk {
+void read_tile_stamps(unsigned long long* out, size_t n);
+}
+}  // namespace gol
+#endif
+
 int main(int argc, char** argv) {
     const i64 N = argc > 1 ? atoll(argv[1]) : 32768;
     const int K = argc > 2 ? atoi(argv[2]) : 8;
@@ -49,7 +57,7 @@ int main(int argc, char** argv) {
     (void)pf;
     (void)skew;  // the LDS-ring prefetch and skewed pipeline variants were removed (measured slower)
     const u32 flags = hipk::STEP_WRAP_Y |
-                      (tile_lv == 2 ? hipk::STEP_TILE_L2 : 0u);
+                      (tile_lv == 2 ? hipk::STEP_TILE_L2 : 0u) | (tile_lv == 4 ? hipk::STEP_TILE_L4 : 0u);
     std::vector<Region> rg = {{0, N, 0, L.nw}};
     i64 rows = rows_arg;
     if (tile_nw > 0) {
@@ -131,6 +139,28 @@ int main(int argc, char** argv) {
         if (ms < best) best = ms;
     }
     CK(hipGetLastError());
+#ifdef GOL_TILE_STAMPS
+    if (tile_nw > 0) {  // time breakdown of the last launch: cycles from the kernel start, median over workgroups
+        const int slots = 48;
+        std::vector<unsigned long long> ts((size_t)4096 * slots);
+        gol::hipk::read_tile_stamps(ts.data(), ts.size());
+        const int nt = (int)std::min<i64>(st.waves, 4096);
+        std::vector<std::vector<double>> seg(slots);
+        for (int b = 0; b < nt; ++b) {
+            const unsigned long long* t = &ts[(size_t)b * slots];
+            if (!t[0]) continue;
+            for (int s = 1; s < slots; ++s)
+                if (t[s] >= t[0] && t[s] - t[0] < (1ull << 40)) seg[s].push_back((double)(t[s] - t[0]));
+        }
+        printf("stamps (median cycles since start):");
+        for (int s = 1; s < slots; ++s) {
+            if (seg[s].empty()) continue;
+            std::sort(seg[s].begin(), seg[s].end());
+            printf(" %d:%.0f", s, seg[s][seg[s].size() / 2]);
+        }
+        printf("\n");
+    }
+#endif
     const double per_gen_us = best * 1e3 / (steps * K);
     const int bpc = tile_nw > 0 ? hipk::tile_blocks_per_cu(tile_nw, rows, K, flags) : hipk::step_blocks_per_cu(K, flags);
     printf("{\"N\": %lld, \"K\": %d, \"skew\": %d, \"pf\": %d, \"tile_nw\": %d, \"rows\": %lld, \"waves\": %lld, "
