@@ -49,6 +49,7 @@ struct DevPlan {
     LaneDesc* d = nullptr;
     i64 waves = 0;
     i64 rows = 0;  // rows per chunk
+    u32 tflags = 0;  // tile kernel: variant bits (LDS levels per pass, in place)
     PlanStats st;
 };
 
@@ -1024,13 +1025,20 @@ class HipEngine : public Engine {
         u32 f = 0;
         if (self_y() && !cfg_.compat) f |= hipk::STEP_WRAP_Y;
         if (xwrap_by_plan()) f |= hipk::STEP_WRAP_X;
-        // tile kernel: generations per LDS pass (GOL_TILE_LEVELS 1, 2 or 4; default 4 for workgroups
-        // of <= 8 waves, 2 above: kbench 8192^2 / 16384^2, K 16-32, 8 waves: 4 levels 0.4-2% faster,
-        // 16 waves: 3-7% slower, profiles/tile_levels_ab.txt)
-        const int lv = tile_lv_ > 0 ? tile_lv_ : (cfg_.tile_waves <= 8 ? 4 : 2);
-        if (lv == 2) f |= hipk::STEP_TILE_L2;
-        if (lv == 4) f |= hipk::STEP_TILE_L4;
         return f;
+    }
+    // Tile-kernel variant bits of a plan (tile_plan_flags).  Generations per LDS pass (GOL_TILE_LEVELS
+    // 1, 2 or 4): auto 4 for a double-buffered tile of <= 8 waves, else 2 (kbench, 8 waves: 4 levels
+    // 0.4-2% faster double-buffered, 1-2% slower in place; 16 waves: 3-7% slower;
+    // profiles/tile_levels_ab.txt, profiles/tile_inplace_ab.txt).
+    u32 tile_bits(bool inplace) const {
+        const int lv = tile_lv_ > 0 ? tile_lv_ : (!inplace && cfg_.tile_waves <= 8 ? 4 : 2);
+        return (lv == 2 ? hipk::STEP_TILE_L2 : 0u) | (lv == 4 ? hipk::STEP_TILE_L4 : 0u) |
+               (inplace ? hipk::STEP_TILE_INPLACE : 0u);
+    }
+    // Most rows a tile may hold at depth k (the in-place variant's capacity unless GOL_TILE_INPLACE=0).
+    i64 tile_rows_cap(int k) const {
+        return hipk::tile_max_rows(k, cfg_.tile_waves, step_flags() | tile_bits(tile_inplace_ != 0));
     }
 
     bool tile_kernel(int kind) const { return kern_[kind] == "tile"; }
@@ -1039,7 +1047,7 @@ class HipEngine : public Engine {
     // Plans are explicit (one descriptor row per tile), so huge boards are left to step_temporal.
     static constexpr i64 kMaxTileRounds = 16;
     i64 tile_rounds(int kind, int k, i64 e) const {
-        const i64 rmax = std::max<i64>(1, hipk::tile_max_rows(k));
+        const i64 rmax = std::max<i64>(1, tile_rows_cap(k));
         i64 tiles = 0;
         for (const Region& r : regions(kind, k, e))
             tiles += ceil_div(r.r1 - r.r0, rmax) * ceil_div(r.c1 - r.c0, (i64)kSegWords);
@@ -1066,7 +1074,7 @@ class HipEngine : public Engine {
         // board is ~0.1 s of host work, long enough for the clock to drop again.
         auto time_pass = [&](int kind, const char* kern, int k, bool build_only = false) -> float {
             kern_[kind] = kern;
-            if (kern_[kind] == "tile" && (hipk::tile_max_rows(k) < 1 || tile_rounds(kind, k, 0) > kMaxTileRounds))
+            if (kern_[kind] == "tile" && (tile_rows_cap(k) < 1 || tile_rounds(kind, k, 0) > kMaxTileRounds))
                 return 1e30f;  // LDS tiles only pay off for small regions (docs/PERFORMANCE.md)
             if (kern_[kind] == "temporal" && !hipk::step_depth_supported(k)) return 1e30f;
             if (build_only) {
@@ -1210,7 +1218,9 @@ class HipEngine : public Engine {
         // plans depend on e only through regions(): rows beyond the tile when y has neighbours,
         // ghost words when x has neighbours (so one plan serves every e of a local rank)
         const i64 ek = self_y() ? (self_x() ? 0 : (e > 0 ? 1 : 0)) : e;
-        const int key = occ_ * 10000000 + (tile_kernel(kind) ? 1000000 : 0) + kind * 100000 + (int)ek * 100 + k;
+        // tile plans also depend on the workgroup size (the LDS rows a tile may hold)
+        const i64 key = ((((i64)occ_ * 2 + (tile_kernel(kind) ? 1 : 0)) * 32 + (tile_kernel(kind) ? cfg_.tile_waves : 0)) * 4 +
+                         kind) * 100000 + (i64)ek * 100 + k;
         auto it = plans_.find(key);
         if (it != plans_.end()) return it->second;
         std::vector<Region> rg = regions(kind, k, e);
@@ -1218,8 +1228,18 @@ class HipEngine : public Engine {
         i64 rows = cfg_.rows_per_wave;
         if (tile_kernel(kind)) {
             // step_tile: one workgroup per plan wave, one tile per CU per round; rows are capped by
-            // the 160 KiB of LDS (double-buffered tile + 2k halo rows), extra rounds beyond that
-            const i64 rmax = hipk::tile_max_rows(k);
+            // the 160 KiB of LDS (2k halo rows + the tile, double-buffered or in place), extra rounds
+            // beyond that.  The double-buffered tile is used when one round of tiles fits it (cheaper:
+            // no halo copies, one barrier per LDS pass; 8192^2: 1.45 vs 1.65 us/gen), the in-place one
+            // (twice the rows) when the double buffer would need more rounds (4096 x 32768: 2.36 vs
+            // 2.70, 16384^2: 4.58 vs 4.69; profiles/tile_inplace_ab.txt).  GOL_TILE_INPLACE=0/1 forces.
+            const i64 rdb = hipk::tile_max_rows(k, cfg_.tile_waves, step_flags() | tile_bits(false));
+            const i64 rip = hipk::tile_max_rows(k, cfg_.tile_waves, step_flags() | tile_bits(true));
+            const i64 r1 = balanced_rows_per_chunk(rg, L_.nw, L_.h, k, cus_, 1, xwrap_by_plan());
+            bool ip = tile_inplace_ > 0 || (tile_inplace_ < 0 && r1 > rdb && rip > rdb);
+            if (tile_inplace_ < 0 && rows > 0) ip = rows > rdb;
+            const i64 rmax = ip ? rip : rdb;
+            p.tflags = tile_bits(ip);
             if (rmax < 1) throw Error(strprintf("GOL_KERNEL=tile: depth %d leaves no LDS rows", k));
             if (rows > rmax) rows = rmax;
             if (tile_rounds(kind, k, e) > kMaxTileRounds)
@@ -1227,7 +1247,6 @@ class HipEngine : public Engine {
                                       "kernel for boards this large",
                                       (long long)tile_rounds(kind, k, e)));
             if (rows <= 0) {
-                const i64 r1 = balanced_rows_per_chunk(rg, L_.nw, L_.h, k, cus_, 1, xwrap_by_plan());
                 const i64 rounds = ceil_div(r1, rmax);
                 rows = rounds <= 1 ? r1
                                    : std::min(rmax, balanced_rows_per_chunk(rg, L_.nw, L_.h, k, rounds * cus_, 1,
@@ -1266,7 +1285,7 @@ class HipEngine : public Engine {
         } else {
             const DevPlan& p = plan(kind, k, e);
             if (p.st.out_words == 0) return;
-            hipk::StepParams sp{L_.pitch, (i32)L_.h, (i32)L_.nw, L_.R, step_flags()};
+            hipk::StepParams sp{L_.pitch, (i32)L_.h, (i32)L_.nw, L_.R, step_flags() | p.tflags};
             if (tile_kernel(kind))
                 hipk::launch_step_tile(cfg_.tile_waves, k, src, dst, p.d, p.waves, p.rows, sp, s);
             else
@@ -1486,6 +1505,8 @@ class HipEngine : public Engine {
     // occupancy).  Small tiles pay (K+1)/S of vertical halo with S rows per wave, so fewer, taller
     // waves can win there; the autotuner tries 2 per SIMD against the full occupancy (3 at K=8).
     int occ_ = 0;
+    // tile kernel: one LDS buffer updated in place (1), double-buffered (0), or per plan (-1, auto)
+    int tile_inplace_ = (int)env_int("GOL_TILE_INPLACE", -1);
     int tile_lv_ = (int)env_int("GOL_TILE_LEVELS", 0);  // tile kernel: generations per LDS pass (1, 2, 4; 0 auto)
     bool multipass_ = false;
     std::map<int, std::vector<int>> passes_;
@@ -1510,7 +1531,7 @@ class HipEngine : public Engine {
     bool graph_ok_ = true;
     bool events_needed_ = true;  // another stream waits on ev_ready_
     std::vector<void*> deferred_free_;
-    std::map<int, DevPlan> plans_;
+    std::map<i64, DevPlan> plans_;
     // GOL_SUBTILES=2 state
     bool dual_ = false;
     Layout sub_L_[2];

@@ -290,6 +290,7 @@ constexpr int kTileRowU32 = 128;  // one LDS row: 64 lo words then 64 hi words
 
 template <bool LAST>
 struct BandSink {
+    static constexpr bool kLast = LAST;
     u32* lds;       // !LAST: destination buffer (row-major, kTileRowU32 per row)
     uint2* st;      // LAST: global store pointer of the band's first output row
     i64 st_stride;  // LAST: pitch, or 0 for halo/idle lanes (trash row)
@@ -307,15 +308,32 @@ struct BandSink {
     }
 };
 
-// Stream input rows in[0 .. n) (n >= 2*LV+1) through an LV-level register window (LV generations
-// per LDS pass); outputs rows LV .. n-LV-1.
-template <bool LAST, int LV>
-__device__ __forceinline__ void tile_band(const u32* __restrict__ in, int n, BandSink<LAST>& out, int lane) {
+// Input rows of a band: consecutive LDS rows (double-buffered tile), or (in-place tile) the band's
+// LV halo rows above from a private copy, its own rows from the tile, its LV halo rows below from
+// the copy.  Row indices are wave-uniform, so the select is scalar.
+struct RowsLinear {
+    const u32* base;
+    __device__ __forceinline__ const u32* row(int i) const { return base + i * kTileRowU32; }
+};
+struct RowsSplit {
+    const u32* above;  // LV rows, then the rows below (and over-read slack)
+    const u32* mid;    // the band's own rows in the tile
+    int lv, m;         // halo depth, own rows
+    __device__ __forceinline__ const u32* row(int i) const {
+        return i < lv ? above + i * kTileRowU32
+                      : (i < lv + m ? mid + (i - lv) * kTileRowU32 : above + (i - m) * kTileRowU32);
+    }
+};
+
+// Stream input rows 0 .. n-1 of `in` (n >= 2*LV+1) through an LV-level register window (LV
+// generations per LDS pass); outputs rows LV .. n-LV-1.
+template <bool LAST, int LV, typename SRC>
+__device__ __forceinline__ void tile_band(const SRC& in, int n, BandSink<LAST>& out, int lane) {
     Pipe<LV> P;
     u32 lo, hi;
 #define GOL_TILE_ROW(PH, GUARD, IDX)                                   \
-    lo = in[(IDX) * kTileRowU32 + lane];                               \
-    hi = in[(IDX) * kTileRowU32 + 64 + lane];                          \
+    lo = in.row(IDX)[lane];                                            \
+    hi = in.row(IDX)[64 + lane];                                       \
     if (advance<LV, PH, GUARD>(P, lo, hi, (IDX))) out.put(lo, hi);
     constexpr int i0 = ((2 * LV + 2) / 3) * 3;  // first multiple of 3 with the window full
     int i = 0;
@@ -335,14 +353,14 @@ __device__ __forceinline__ void tile_band(const u32* __restrict__ in, int n, Ban
     // too few to hide it by switching waves: 35% of wave time was s_waitcnt, PMC at 8192^2).  The
     // last prefetch reads up to 3 rows past the band: still inside the tile buffers or the LDS slack
     // rows (tile_lds_bytes), and never used.
-    u32 l0 = in[i * kTileRowU32 + lane], h0 = in[i * kTileRowU32 + 64 + lane];
-    u32 l1 = in[(i + 1) * kTileRowU32 + lane], h1 = in[(i + 1) * kTileRowU32 + 64 + lane];
-    u32 l2 = in[(i + 2) * kTileRowU32 + lane], h2 = in[(i + 2) * kTileRowU32 + 64 + lane];
+    u32 l0 = in.row(i)[lane], h0 = in.row(i)[64 + lane];
+    u32 l1 = in.row(i + 1)[lane], h1 = in.row(i + 1)[64 + lane];
+    u32 l2 = in.row(i + 2)[lane], h2 = in.row(i + 2)[64 + lane];
     for (; i + 3 <= n; i += 3) {
         const u32 a0 = l0, b0 = h0, a1 = l1, b1 = h1, a2 = l2, b2 = h2;
-        l0 = in[(i + 3) * kTileRowU32 + lane], h0 = in[(i + 3) * kTileRowU32 + 64 + lane];
-        l1 = in[(i + 4) * kTileRowU32 + lane], h1 = in[(i + 4) * kTileRowU32 + 64 + lane];
-        l2 = in[(i + 5) * kTileRowU32 + lane], h2 = in[(i + 5) * kTileRowU32 + 64 + lane];
+        l0 = in.row(i + 3)[lane], h0 = in.row(i + 3)[64 + lane];
+        l1 = in.row(i + 4)[lane], h1 = in.row(i + 4)[64 + lane];
+        l2 = in.row(i + 5)[lane], h2 = in.row(i + 5)[64 + lane];
         __builtin_amdgcn_sched_barrier(0);
         lo = a0, hi = b0;
         if (advance<LV, 0, false>(P, lo, hi, i)) out.put(lo, hi);
@@ -362,27 +380,57 @@ __device__ __forceinline__ void tile_band(const u32* __restrict__ in, int n, Ban
 #undef GOL_TILE_ROW
 }
 
+// Side rows per wave of the in-place tile: its 2*LV halo rows plus the band stream's over-read.
+__host__ __device__ constexpr int tile_side_rows(int lv) { return 2 * lv + 4; }
+
 // One LDS pass of `lv` generations: wave `wv` streams its band of the pass's output rows.
-template <int NW, int LV>
-__device__ __forceinline__ void tile_pass(const u32* A, u32* B, u64* dst, const LaneDesc& d, const StepParams& p,
-                                          int K, int g, int n_in, int wv, int lane) {
+//   double-buffered (IP false): reads A, writes B.
+//   in place (IP true): every wave first copies its band's LV halo rows above and below (rows other
+//   waves are about to overwrite) into its private side rows, then, after a barrier, streams the band
+//   and writes its output rows back into A.  A wave only ever writes its own band's rows and reads
+//   other bands' rows only from its copy, so one tile buffer suffices: twice the rows per tile in the
+//   160 KiB of LDS (one round of tiles where the double buffer needed two or three).
+template <int NW, int LV, bool IP>
+__device__ __forceinline__ void tile_pass(u32* A, u32* B, u32* side, u64* dst, const LaneDesc& d,
+                                          const StepParams& p, int K, int g, int n_in, int wv, int lane) {
     const int lo_r = g + LV, cnt = n_in - 2 * g - 2 * LV;
     const int b = (cnt + NW - 1) / NW;
     const int r0 = lo_r + wv * b;
     const int r1 = min(r0 + b, lo_r + cnt);
-    if (r1 <= r0) return;
-    const u32* in = A + (r0 - LV) * kTileRowU32;
     const int n = r1 - r0 + 2 * LV;
+    u32* sw = side + wv * tile_side_rows(LV) * kTileRowU32;
+    if constexpr (IP) {
+        if (r1 > r0) {
+#pragma unroll
+            for (int j = 0; j < LV; ++j) {
+                sw[j * kTileRowU32 + lane] = A[(r0 - LV + j) * kTileRowU32 + lane];
+                sw[j * kTileRowU32 + 64 + lane] = A[(r0 - LV + j) * kTileRowU32 + 64 + lane];
+                sw[(LV + j) * kTileRowU32 + lane] = A[(r1 + j) * kTileRowU32 + lane];
+                sw[(LV + j) * kTileRowU32 + 64 + lane] = A[(r1 + j) * kTileRowU32 + 64 + lane];
+            }
+        }
+        __syncthreads();  // every wave's copy is taken before any band is overwritten
+    }
+    if (r1 <= r0) return;
+    auto stream = [&](auto& sink) {
+        if constexpr (IP) {
+            const RowsSplit in{sw, A + r0 * kTileRowU32, LV, r1 - r0};
+            tile_band<std::remove_reference_t<decltype(sink)>::kLast, LV>(in, n, sink, lane);
+        } else {
+            const RowsLinear in{A + (r0 - LV) * kTileRowU32};
+            tile_band<std::remove_reference_t<decltype(sink)>::kLast, LV>(in, n, sink, lane);
+        }
+    };
     if (g + LV < K) {
-        BandSink<false> s{B, nullptr, 0, r0, lane};
-        tile_band<false, LV>(in, n, s, lane);
+        BandSink<false> s{IP ? A : B, nullptr, 0, r0, lane};
+        stream(s);
     } else {
         // tile row r0 is output row row0 + r0 - K; halo/idle lanes write the trash row
         const bool out_lane = d.flags & LANE_STORE;
         const i64 srow = out_lane ? (i64)(d.row0 + r0 - K + p.R) : (i64)(p.h + 2 * p.R + kSlackRows - 1);
         BandSink<true> s{nullptr, reinterpret_cast<uint2*>(dst + srow * p.pitch + (d.col + 1)), out_lane ? p.pitch : 0,
                          0, lane};
-        tile_band<true, LV>(in, n, s, lane);
+        stream(s);
     }
 }
 
@@ -403,7 +451,7 @@ __device__ __forceinline__ void tile_stamp(int wv, int lane, int slot) {
 #define GOL_STAMP(slot) ((void)0)
 #endif
 
-template <int NW, bool WRAPY, int LV>
+template <int NW, bool WRAPY, int LV, bool IP>
 __global__ __launch_bounds__(64 * NW) void step_tile(const u64* __restrict__ src, u64* __restrict__ dst,
                                                      const LaneDesc* __restrict__ plan, StepParams p, int K) {
     extern __shared__ __attribute__((aligned(16))) u32 tile_lds[];
@@ -415,7 +463,8 @@ __global__ __launch_bounds__(64 * NW) void step_tile(const u64* __restrict__ src
     GOL_STAMP(0);
     const int n_in = nrows + 2 * K;
     u32* A = tile_lds;
-    u32* B = tile_lds + n_in * kTileRowU32;
+    u32* B = tile_lds + n_in * kTileRowU32;  // double-buffered: the second tile buffer
+    u32* side = tile_lds + n_in * kTileRowU32;  // in place: NW x tile_side_rows(LV) private rows
 
     // 1. stage rows row0-K .. row0+nrows+K-1 (two 4-byte DMAs per row: lo plane, hi plane)
     for (int i = wv; i < n_in; i += NW) {
@@ -441,36 +490,51 @@ __global__ __launch_bounds__(64 * NW) void step_tile(const u64* __restrict__ src
         int lv = 1;
         if (LV >= 4 && left >= 4) {
             lv = 4;
-            tile_pass<NW, (LV >= 4 ? 4 : 1)>(A, B, dst, d, p, K, g, n_in, wv, lane);
+            tile_pass<NW, (LV >= 4 ? 4 : 1), IP>(A, B, side, dst, d, p, K, g, n_in, wv, lane);
         } else if (LV >= 2 && left >= 2) {
             lv = 2;
-            tile_pass<NW, (LV >= 2 ? 2 : 1)>(A, B, dst, d, p, K, g, n_in, wv, lane);
+            tile_pass<NW, (LV >= 2 ? 2 : 1), IP>(A, B, side, dst, d, p, K, g, n_in, wv, lane);
         } else {
-            tile_pass<NW, 1>(A, B, dst, d, p, K, g, n_in, wv, lane);
+            tile_pass<NW, 1, IP>(A, B, side, dst, d, p, K, g, n_in, wv, lane);
         }
         g += lv;
         ++npass;
         if (g < K) {
             __syncthreads();
             GOL_STAMP(1 + npass);
-            u32* t = A;
-            A = B;
-            B = t;
+            if constexpr (!IP) {
+                u32* t = A;
+                A = B;
+                B = t;
+            }
         }
     }
     GOL_STAMP(kStampSlotsLast);
 }
 
-// LDS bytes of a tile with `rows` output rows at depth k (+4 rows of over-read slack).
-inline size_t tile_lds_bytes(i64 rows, int k) { return (size_t)(2 * (rows + 2 * k) + 4) * kTileRowU32 * 4; }
+int tile_levels(u32 flags) { return (flags & STEP_TILE_L4) ? 4 : ((flags & STEP_TILE_L2) ? 2 : 1); }
 
+// LDS rows of a tile with `rows` output rows at depth k: double-buffered, two copies of the tile
+// (+4 rows of over-read slack); in place, one copy plus NW private side rows per wave.
+i64 tile_lds_rows(i64 rows, int k, int nw, u32 flags) {
+    if (flags & STEP_TILE_INPLACE) return rows + 2 * (i64)k + (i64)nw * tile_side_rows(tile_levels(flags));
+    return 2 * (rows + 2 * (i64)k) + 4;
+}
+inline size_t tile_lds_bytes(i64 rows, int k, int nw, u32 flags) {
+    return (size_t)tile_lds_rows(rows, k, nw, flags) * kTileRowU32 * 4;
+}
+
+template <int NW, bool IP>
+const void* tile_kernel_ip(u32 flags) {
+    if (flags & STEP_TILE_L4)
+        return (flags & STEP_WRAP_Y) ? (const void*)step_tile<NW, true, 4, IP> : (const void*)step_tile<NW, false, 4, IP>;
+    if (flags & STEP_TILE_L2)
+        return (flags & STEP_WRAP_Y) ? (const void*)step_tile<NW, true, 2, IP> : (const void*)step_tile<NW, false, 2, IP>;
+    return (flags & STEP_WRAP_Y) ? (const void*)step_tile<NW, true, 1, IP> : (const void*)step_tile<NW, false, 1, IP>;
+}
 template <int NW>
 const void* tile_kernel(u32 flags) {
-    if (flags & STEP_TILE_L4)
-        return (flags & STEP_WRAP_Y) ? (const void*)step_tile<NW, true, 4> : (const void*)step_tile<NW, false, 4>;
-    if (flags & STEP_TILE_L2)
-        return (flags & STEP_WRAP_Y) ? (const void*)step_tile<NW, true, 2> : (const void*)step_tile<NW, false, 2>;
-    return (flags & STEP_WRAP_Y) ? (const void*)step_tile<NW, true, 1> : (const void*)step_tile<NW, false, 1>;
+    return (flags & STEP_TILE_INPLACE) ? tile_kernel_ip<NW, true>(flags) : tile_kernel_ip<NW, false>(flags);
 }
 
 const void* tile_kernel_for(int nw_per_wg, u32 flags) {
@@ -570,17 +634,19 @@ void launch_step(int k, const u64* src, u64* dst, const LaneDesc* plan, i64 n_wa
     if (e != hipSuccess) throw Error(strprintf("step kernel launch failed: %s", hipGetErrorString(e)));
 }
 
-i64 tile_max_rows(int k) {
+i64 tile_max_rows(int k, int nw_per_wg, u32 flags) {
     const i64 lds_rows = kMaxLdsBytes / (kTileRowU32 * 4);  // 320 rows of 512 B
+    if (flags & STEP_TILE_INPLACE) return lds_rows - (i64)nw_per_wg * tile_side_rows(tile_levels(flags)) - 2 * (i64)k;
     return (lds_rows - 4) / 2 - 2 * (i64)k;
 }
 
 static const void* tile_kernel_checked(int nw_per_wg, u32 flags) {
     const void* f = tile_kernel_for(nw_per_wg, flags);
     if (!f) throw Error(strprintf("step_tile: unsupported waves per workgroup %d (4, 8 or 16)", nw_per_wg));
-    static bool attr_set[128] = {};
+    static bool attr_set[256] = {};
     const int lvk = (flags & STEP_TILE_L4) ? 2 : ((flags & STEP_TILE_L2) ? 1 : 0);
-    const int key = ((nw_per_wg & 15) * 2 + ((flags & STEP_WRAP_Y) ? 1 : 0)) * 3 + lvk;
+    const int key = (((nw_per_wg & 15) * 2 + ((flags & STEP_WRAP_Y) ? 1 : 0)) * 3 + lvk) * 2 +
+                    ((flags & STEP_TILE_INPLACE) ? 1 : 0);
     if (!attr_set[key]) {  // allow the full 160 KiB of dynamic LDS
         hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kMaxLdsBytes);
         if (e != hipSuccess) throw Error(strprintf("step_tile: hipFuncSetAttribute: %s", hipGetErrorString(e)));
@@ -592,7 +658,8 @@ static const void* tile_kernel_checked(int nw_per_wg, u32 flags) {
 int tile_blocks_per_cu(int nw_per_wg, i64 rows, int k, u32 flags) {
     const void* f = tile_kernel_checked(nw_per_wg, flags);
     int nb = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, f, 64 * nw_per_wg, tile_lds_bytes(rows, k)) != hipSuccess ||
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, f, 64 * nw_per_wg, tile_lds_bytes(rows, k, nw_per_wg, flags)) !=
+            hipSuccess ||
         nb < 1)
         return 1;
     return std::min(nb, 8);
@@ -601,14 +668,16 @@ int tile_blocks_per_cu(int nw_per_wg, i64 rows, int k, u32 flags) {
 void launch_step_tile(int nw_per_wg, int k, const u64* src, u64* dst, const LaneDesc* plan, i64 n_tiles, i64 rows,
                       const StepParams& p, hipStream_t s) {
     if (k < 1 || k > 64) throw Error(strprintf("step_tile: depth %d outside 1..64", k));
-    if (rows < 1 || rows > tile_max_rows(k))
+    const i64 rmax = tile_max_rows(k, nw_per_wg, p.flags);
+    if (rows < 1 || rows > rmax)
         throw Error(strprintf("step_tile: %lld rows per tile exceed the LDS capacity (max %lld at depth %d)",
-                              (long long)rows, (long long)tile_max_rows(k), k));
+                              (long long)rows, (long long)rmax, k));
     const void* f = tile_kernel_checked(nw_per_wg, p.flags);
     StepParams pp = p;
     int kk = k;
     void* args[] = {(void*)&src, (void*)&dst, (void*)&plan, (void*)&pp, (void*)&kk};
-    hipError_t e = hipLaunchKernel(f, dim3((unsigned)n_tiles), dim3(64 * nw_per_wg), args, tile_lds_bytes(rows, k), s);
+    hipError_t e = hipLaunchKernel(f, dim3((unsigned)n_tiles), dim3(64 * nw_per_wg), args,
+                                   tile_lds_bytes(rows, k, nw_per_wg, p.flags), s);
     if (e != hipSuccess) throw Error(strprintf("step_tile launch failed: %s", hipGetErrorString(e)));
 }
 

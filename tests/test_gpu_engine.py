@@ -384,3 +384,69 @@ def test_known_physics_gpu(gol, kernel):
     s.set_board(np.ones((N, N), np.uint8))
     s.step(1)
     assert s.population() == 0
+
+
+@pytest.mark.parametrize("H,W,kernel", [(300, 1000, "temporal"), (130, 4096, "tile"), (2048, 192, "auto"),
+                                        (517, 333, "temporal")])
+def test_rectangular_boards(gol, H, W, kernel):
+    """N rows x width columns (the per-rank tiles of multi-GPU configs, measured on one GPU)."""
+    gens = 29
+    s = _sim(gol, H, width=W, kernel=kernel).init(5, seed=H)
+    s.step(gens)
+    assert s.board().shape == (H, W)
+    assert np.array_equal(s.board(), numpy_step(random_board(H, W, H), gens))
+
+
+@pytest.mark.parametrize("inplace", ["0", "1"])
+@pytest.mark.parametrize("levels", ["1", "2", "4"])
+@pytest.mark.parametrize("tile_waves", [4, 8, 16])
+def test_tile_variants(gol, monkeypatch, inplace, levels, tile_waves):
+    """Tile kernel: double-buffered or in place (private halo copies), 1/2/4 generations per LDS
+    pass, every workgroup size; depth 13 leaves a pass of each smaller level count."""
+    monkeypatch.setenv("GOL_TILE_INPLACE", inplace)
+    monkeypatch.setenv("GOL_TILE_LEVELS", levels)
+    N, gens = 700, 13 * 3 + 5
+    s = _sim(gol, N, kernel="tile", halo_depth=13, kernel_depth=13, tile_waves=tile_waves).init(5, seed=21)
+    s.step(gens)
+    assert np.array_equal(s.board(), numpy_step(initial_board(5, N, 1, True, 21), gens))
+
+
+def test_tile_inplace_auto_tall_tiles(gol):
+    """A board whose one-round tiles exceed the double buffer: the planner switches to the in-place
+    tile (one round of ~137-row tiles at 4096 x 32768), checked against the torch oracle."""
+    import torch
+
+    H, W, gens = 4096, 32768, 64
+    s = _sim(gol, H, width=W, kernel="tile", kernel_depth=32).init(5, seed=4)
+    s.step(gens)
+    ref = torch_step(random_board(H, W, 4), gens, device="cuda").cpu().numpy()
+    assert np.array_equal(s.board(), ref)
+    del torch
+
+
+def test_checkpoint_across_decompositions_hip(gol, tmp_path):
+    """A HIP engine's checkpoint (one global board file) resumed by 2 thread ranks in a 2x1 grid on
+    the CPU backend: the file depends on neither the decomposition nor the backend."""
+    import threading
+
+    N, g1, g2 = 512, 40, 23
+    prefix = str(tmp_path / "ck")
+    a = _sim(gol, N, global_mode=True).init(5, seed=8)
+    a.step(g1)
+    a.checkpoint(prefix)
+    ts = gol.parallel.thread_transports(2)
+    parts = [None, None]
+
+    def rank(r):
+        b = gol.Simulation(N, ts[r], backend="cpu", global_mode=True, decomp="2d", grid="2x1").init(0)
+        assert b.restore(prefix) == g1
+        b.step(g2)
+        parts[r] = (b.geometry.col0, b.board())
+
+    th = [threading.Thread(target=rank, args=(r,)) for r in range(2)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    full = np.hstack([p[1] for p in sorted(parts, key=lambda p: p[0])])
+    assert np.array_equal(full, numpy_step(initial_board(5, N, 1, False, 8), g1 + g2))

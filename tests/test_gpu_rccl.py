@@ -10,7 +10,7 @@ against the numpy torus oracle.
 import numpy as np
 import pytest
 
-from gol_amd.ops import initial_board, numpy_step
+from gol_amd.ops import initial_board, numpy_step, random_board
 
 pytestmark = pytest.mark.gpu
 
@@ -84,3 +84,14 @@ def test_rccl_self_graph_capture(gol, rccl, decomp, monkeypatch):
     got, st = _run(gol, rccl, N, gens, 17, halo_depth=8, decomp=decomp, subtiles=0)
     assert st["graph_launches"] >= 1, st
     assert np.array_equal(got, numpy_step(initial_board(5, N, 1, True, 17), gens))
+
+
+@pytest.mark.parametrize("H,W,decomp", [(2304, 1024, "2d"), (2048, 1536, "1d")])
+def test_rccl_self_auto_depth_rectangular(gol, rccl, H, W, decomp):
+    """Rectangular per-rank tiles with the auto halo depth of a rank with neighbours (56 in 2-D,
+    64 in 1-D for >= 2048 rows): every superstep's halos through RCCL."""
+    gens = 2 * 64 + 9
+    got, st = _run(gol, rccl, H, gens, 6, width=W, decomp=decomp)
+    assert st["depth"] == (56 if decomp == "2d" else 64), st
+    assert st["exchanges"] >= 2, st
+    assert np.array_equal(got, numpy_step(random_board(H, W, 6), gens))

@@ -42,7 +42,8 @@ int main(int argc, char** argv) {
     const int skew = argc > 5 ? atoi(argv[5]) : 0;
     const int tile_nw = argc > 6 ? atoi(argv[6]) : 0;  // >0: step_tile with this many waves per workgroup
     const i64 rows_arg = argc > 7 ? atoll(argv[7]) : 0;
-    Layout L(N, N, K);
+    const i64 W = getenv("KB_W") ? atoll(getenv("KB_W")) : N;  // board columns (default square)
+    Layout L(N, W, K);
     const size_t bytes = (size_t)(L.words() + hipk::kSlackRows * L.pitch) * 8;
     u64 *a, *b;
     CK(hipMalloc(&a, bytes));
@@ -57,11 +58,12 @@ int main(int argc, char** argv) {
     (void)pf;
     (void)skew;  // the LDS-ring prefetch and skewed pipeline variants were removed (measured slower)
     const u32 flags = hipk::STEP_WRAP_Y |
-                      (tile_lv == 2 ? hipk::STEP_TILE_L2 : 0u) | (tile_lv == 4 ? hipk::STEP_TILE_L4 : 0u);
+                      (tile_lv == 2 ? hipk::STEP_TILE_L2 : 0u) | (tile_lv == 4 ? hipk::STEP_TILE_L4 : 0u) |
+                      (getenv("KB_INPLACE") && atoi(getenv("KB_INPLACE")) ? hipk::STEP_TILE_INPLACE : 0u);
     std::vector<Region> rg = {{0, N, 0, L.nw}};
     i64 rows = rows_arg;
     if (tile_nw > 0) {
-        const i64 rmax = hipk::tile_max_rows(K);
+        const i64 rmax = hipk::tile_max_rows(K, tile_nw, flags);
         if (rows > rmax) rows = rmax;
         for (i64 rounds = 1; rows <= 0; ++rounds) {
             const i64 r = balanced_rows_per_chunk(rg, L.nw, N, K, rounds * prop.multiProcessorCount, 1, true);
@@ -166,6 +168,6 @@ int main(int argc, char** argv) {
     printf("{\"N\": %lld, \"K\": %d, \"skew\": %d, \"pf\": %d, \"tile_nw\": %d, \"rows\": %lld, \"waves\": %lld, "
            "\"blocks_per_cu\": %d, \"us_per_gen\": %.3f, \"cells_per_s\": %.4e}\n",
            (long long)N, K, skew, pf, tile_nw, (long long)rows, (long long)st.waves, bpc, per_gen_us,
-           (double)N * N / (per_gen_us * 1e-6));
+           (double)N * W / (per_gen_us * 1e-6));
     return 0;
 }
