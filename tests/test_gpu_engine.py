@@ -450,3 +450,34 @@ def test_checkpoint_across_decompositions_hip(gol, tmp_path):
         t.join()
     full = np.hstack([p[1] for p in sorted(parts, key=lambda p: p[0])])
     assert np.array_equal(full, numpy_step(initial_board(5, N, 1, False, 8), g1 + g2))
+
+
+@pytest.mark.parametrize("N,R", [(385, 64), (388, 64), (259, 43)])
+def test_uneven_strips_collective_schedule(gol, N, R):
+    """Strips of 129/128/128 rows with R = 64 (and neighbours of it): whether the split schedule is
+    possible is decided from the smallest strip on every rank, so the collective schedule timing is
+    entered by all ranks or none (a per-rank decision would hang or mismatch the exchanges)."""
+    import threading
+
+    P, gens = 3, 2 * R + 11
+    ts = gol.parallel.p2p_thread_transports(P)
+    out, errs = [None] * P, []
+
+    def rank_main(r):
+        try:
+            s = gol.Simulation(N, ts[r], backend="hip", device=0, global_mode=True, halo_depth=R, width=320)
+            s.init(5, seed=31)
+            s.step(gens)
+            out[r] = (s.geometry.row0, s.board(), s.stats()["schedule"])
+        except Exception as e:  # pragma: no cover - reported below
+            errs.append(repr(e))
+
+    th = [threading.Thread(target=rank_main, args=(r,)) for r in range(P)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=300)
+    assert not errs, errs
+    assert len({o[2] for o in out}) == 1, [o[2] for o in out]  # one schedule on every rank
+    board = np.vstack([b for _, b, _ in sorted(out, key=lambda o: o[0])])
+    assert np.array_equal(board, numpy_step(random_board(N, 320, 31), gens))
