@@ -49,7 +49,14 @@ struct StepParams {
     // (word c at + c + 1, like the source buffer's rows)
     const u64* above = nullptr;
     const u64* below = nullptr;
+    // Where lanes that store nothing (halo / idle lanes) write instead: kTrashWaves x 64 words, one
+    // word per (wave mod kTrashWaves, lane).  Filled in by the launch functions (ensure_trash).
+    u64* trash = nullptr;
 };
+constexpr int kTrashWaves = 1024;
+// Allocate the current device's trash buffer (call once per device before any launch or capture;
+// thread safe).
+void ensure_trash();
 
 // Supported temporal depths (template instantiations).
 bool step_depth_supported(int k);

@@ -70,6 +70,7 @@ class HipEngine : public Engine {
         cus_ = prop.multiProcessorCount;
         int R = L_.R;
         kernel_ = cfg_.kernel;
+        hipk::ensure_trash();  // before any launch or graph capture
         // Kernel pass depth K (generations per HBM pass) vs halo depth R (generations per
         // exchange).  In 1-D (and on a single rank) a superstep of R generations runs as several
         // passes of <= K, the earlier ones also producing the ghost rows the later ones read, so

@@ -29,6 +29,8 @@
 //
 // step_lds — single-generation LDS-tiled variant: a 256-thread workgroup stages a (16+2) x (64+2)
 // word tile + ghost ring in LDS and computes 16 x 64 output words.  Kept as a measured alternative.
+#include <mutex>
+
 #include "gol/bits.hpp"
 #include "gol/hip_kernels.hpp"
 
@@ -157,7 +159,8 @@ struct WaveRunner {
         }
     }
 
-    __device__ __forceinline__ WaveRunner(const u64* src, u64* dst, const LaneDesc& d_, int nrows, const StepParams& p_)
+    __device__ __forceinline__ WaveRunner(const u64* src, u64* dst, const LaneDesc& d_, int nrows, const StepParams& p_,
+                                          i64 wave_id)
         : p(p_), d(d_), n(nrows + 2 * K), hp((i64)p_.h * p_.pitch) {
         lrow = d.row0 - K;
         if (ROWS == ROWS_WRAP && lrow < 0) lrow += p.h;
@@ -170,11 +173,13 @@ struct WaveRunner {
             ld = reinterpret_cast<const uint2*>(src + (i64)(lrow + p.R) * p.pitch + (d.col + 1));
         }
         // Every lane stores every row (no branch: the row loop stays one basic block, so the
-        // scheduler can interleave consecutive rows).  Halo/idle lanes write their own column of the
-        // last slack row of the allocation, which nothing reads.
+        // scheduler can interleave consecutive rows).  Halo/idle lanes write a trash word of their
+        // own (wave mod kTrashWaves, lane), which nothing reads.  (They used to share one trash row
+        // per plan column: thousands of waves storing to the same few words every row, a hot spot
+        // that held shallow memory-bound passes at ~55% of the HBM streaming rate.)
         const bool out = d.flags & LANE_STORE;
-        const i64 srow = out ? (i64)(d.row0 + p.R) : (i64)(p.h + 2 * p.R + kSlackRows - 1);
-        st = reinterpret_cast<uint2*>(dst + srow * p.pitch + (d.col + 1));
+        st = out ? reinterpret_cast<uint2*>(dst + (i64)(d.row0 + p.R) * p.pitch + (d.col + 1))
+                 : reinterpret_cast<uint2*>(p.trash + ((i64)(wave_id & (kTrashWaves - 1)) * 64 + (threadIdx.x & 63)));
         st_stride = out ? p.pitch : 0;
 #pragma unroll
         for (int j = 0; j < D; ++j) {
@@ -224,23 +229,44 @@ struct WaveRunner {
             body<1, true>(i + 1);
             body<2, true>(i + 2);
         }
-        for (; i + 3 <= n; i += 3) {
-            // hoist the whole next triple's loads above this triple's compute
-            const uint2 x0 = pf[0], x1 = pf[1], x2 = pf[2];
-#pragma unroll
-            for (int j = 0; j + 3 < D; ++j) pf[j] = pf[j + 3];
-#pragma unroll
-            for (int j = D - 3; j < D; ++j) {
-                pf[j] = *ld;
-                next_row();
+        if constexpr (D == 6) {
+            // Shallow (memory-bound) passes: each row's registers are consumed and then refilled with
+            // the row six ahead, so six loads stay in flight per wave and no register copy has to
+            // wait for an outstanding load (copying a prefetched register forces the wait: the
+            // queue shift of the fill phase collapses the prefetch distance to one triple).
+#define GOL_ROW6(J)                                          \
+    compute_store<(J) % 3, false>(pf[J].x, pf[J].y, i + (J)); \
+    pf[J] = *ld;                                             \
+    next_row();                                              \
+    __builtin_amdgcn_sched_barrier(0);
+            for (; i + 6 <= n; i += 6) {
+                GOL_ROW6(0) GOL_ROW6(1) GOL_ROW6(2) GOL_ROW6(3) GOL_ROW6(4) GOL_ROW6(5)
             }
-            __builtin_amdgcn_sched_barrier(0);
-            compute_store<0, false>(x0.x, x0.y, i);
-            compute_store<1, false>(x1.x, x1.y, i + 1);
-            compute_store<2, false>(x2.x, x2.y, i + 2);
+#undef GOL_ROW6
+            // fewer than six rows left, in pf[0..] in order
+            if (i < n) compute_store<0, false>(pf[0].x, pf[0].y, i);
+            if (i + 1 < n) compute_store<1, false>(pf[1].x, pf[1].y, i + 1);
+            if (i + 2 < n) compute_store<2, false>(pf[2].x, pf[2].y, i + 2);
+            if (i + 3 < n) compute_store<0, false>(pf[3].x, pf[3].y, i + 3);
+            if (i + 4 < n) compute_store<1, false>(pf[4].x, pf[4].y, i + 4);
+        } else {
+            for (; i + 3 <= n; i += 3) {
+                // hoist the whole next triple's loads above this triple's compute
+                const uint2 x0 = pf[0], x1 = pf[1], x2 = pf[2];
+                pf[0] = *ld;
+                next_row();
+                pf[1] = *ld;
+                next_row();
+                pf[2] = *ld;
+                next_row();
+                __builtin_amdgcn_sched_barrier(0);
+                compute_store<0, false>(x0.x, x0.y, i);
+                compute_store<1, false>(x1.x, x1.y, i + 1);
+                compute_store<2, false>(x2.x, x2.y, i + 2);
+            }
+            if (i < n) body<0, false>(i);
+            if (i + 1 < n) body<1, false>(i + 1);
         }
-        if (i < n) body<0, false>(i);
-        if (i + 1 < n) body<1, false>(i + 1);
     }
 };
 
@@ -260,7 +286,7 @@ __global__ __launch_bounds__(256) GOL_TEMPORAL_OCC void step_temporal(const u64*
     const LaneDesc d = plan[wave * kWaveLanes + lane];
     const int nrows = __builtin_amdgcn_readfirstlane(d.nrows);
     if (nrows <= 0) return;  // padding wave (uniform)
-    WaveRunner<K, ROWS> w(src, dst, d, nrows, p);
+    WaveRunner<K, ROWS> w(src, dst, d, nrows, p, wave);
     w.run();
 }
 
@@ -425,11 +451,11 @@ __device__ __forceinline__ void tile_pass(u32* A, u32* B, u32* side, u64* dst, c
         BandSink<false> s{IP ? A : B, nullptr, 0, r0, lane};
         stream(s);
     } else {
-        // tile row r0 is output row row0 + r0 - K; halo/idle lanes write the trash row
+        // tile row r0 is output row row0 + r0 - K; halo/idle lanes write their own trash word
         const bool out_lane = d.flags & LANE_STORE;
-        const i64 srow = out_lane ? (i64)(d.row0 + r0 - K + p.R) : (i64)(p.h + 2 * p.R + kSlackRows - 1);
-        BandSink<true> s{nullptr, reinterpret_cast<uint2*>(dst + srow * p.pitch + (d.col + 1)), out_lane ? p.pitch : 0,
-                         0, lane};
+        uint2* st = out_lane ? reinterpret_cast<uint2*>(dst + (i64)(d.row0 + r0 - K + p.R) * p.pitch + (d.col + 1))
+                             : reinterpret_cast<uint2*>(p.trash + ((i64)((blockIdx.x * NW + wv) & (kTrashWaves - 1)) * 64 + lane));
+        BandSink<true> s{nullptr, st, out_lane ? p.pitch : 0, 0, lane};
         stream(s);
     }
 }
@@ -623,12 +649,32 @@ int step_blocks_per_cu(int k, u32 flags) {
     return std::min(nb, 8);
 }
 
+// Per-device trash buffers (StepParams::trash).
+static std::mutex g_trash_mu;
+static u64* g_trash[64] = {};
+void ensure_trash() {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) throw Error("ensure_trash: no current HIP device");
+    std::lock_guard<std::mutex> lk(g_trash_mu);
+    if (g_trash[dev]) return;
+    void* t = nullptr;
+    if (hipMalloc(&t, (size_t)kTrashWaves * 64 * sizeof(u64)) != hipSuccess) throw Error("ensure_trash: hipMalloc failed");
+    g_trash[dev] = (u64*)t;
+}
+static u64* trash_of_current_device() {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64 || !g_trash[dev])
+        throw Error("step kernels: the device's trash buffer is not allocated (hipk::ensure_trash)");
+    return g_trash[dev];
+}
+
 void launch_step(int k, const u64* src, u64* dst, const LaneDesc* plan, i64 n_waves, const StepParams& p,
                  hipStream_t s) {
     const void* f = kernel_of(k, p.flags);
     if (!f) throw Error(strprintf("no step kernel instantiated for depth %d", k));
     const dim3 grid((unsigned)(n_waves / kWavesPerBlock)), block(256);
     StepParams pp = p;
+    if (!pp.trash) pp.trash = trash_of_current_device();
     void* args[] = {(void*)&src, (void*)&dst, (void*)&plan, (void*)&pp};
     hipError_t e = hipLaunchKernel(f, grid, block, args, 0, s);
     if (e != hipSuccess) throw Error(strprintf("step kernel launch failed: %s", hipGetErrorString(e)));
@@ -674,6 +720,7 @@ void launch_step_tile(int nw_per_wg, int k, const u64* src, u64* dst, const Lane
                               (long long)rows, (long long)rmax, k));
     const void* f = tile_kernel_checked(nw_per_wg, p.flags);
     StepParams pp = p;
+    if (!pp.trash) pp.trash = trash_of_current_device();
     int kk = k;
     void* args[] = {(void*)&src, (void*)&dst, (void*)&plan, (void*)&pp, (void*)&kk};
     hipError_t e = hipLaunchKernel(f, dim3((unsigned)n_tiles), dim3(64 * nw_per_wg), args,

@@ -81,6 +81,7 @@ int main(int argc, char** argv) {
     LaneDesc* dplan;
     CK(hipMalloc(&dplan, lanes.size() * sizeof(LaneDesc)));
     CK(hipMemcpy(dplan, lanes.data(), lanes.size() * sizeof(LaneDesc), hipMemcpyHostToDevice));
+    hipk::ensure_trash();
     hipk::StepParams sp{L.pitch, (i32)L.h, (i32)L.nw, L.R, flags};
     const int steps = gens / K;
     // KB_SPLIT2=1 (temporal only, timing experiment): the board as two half-height regions, each
