@@ -34,6 +34,29 @@ __global__ void colwalk(const uint2* __restrict__ a, uint2* __restrict__ b, long
     const int n = (int)(r0 + rows <= H ? rows : H - r0);
     for (int i = 0; i < n; ++i) q[(long)i * pitch] = p[(long)i * pitch];
 }
+// The same, but like step_temporal's plan: lanes 0 and 63 are halo lanes that load and do not
+// store (62-word output segments, 1 + 62 s .. 62 s + 62), and every row's store waits for the
+// load two rows ahead (the 3-row window).
+__global__ void colwalk62(const uint2* __restrict__ a, uint2* __restrict__ b, long pitch, int nseg, int rows, int H) {
+    const int wave = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+    const int seg = wave % nseg, band = wave / nseg;
+    const long r0 = (long)band * rows;
+    if (r0 >= H) return;
+    const long c = (long)seg * 62 + lane;
+    if (c >= pitch) return;
+    const uint2* p = a + r0 * pitch + c;
+    uint2* q = b + r0 * pitch + c;
+    const int n = (int)(r0 + rows <= H ? rows : H - r0);
+    const bool out = lane != 0 && lane != 63;
+    uint2 w0 = p[0], w1 = p[pitch];
+    for (int i = 0; i < n; ++i) {
+        const uint2 w2 = p[(long)(i + 2) * pitch];
+        const uint2 v = make_uint2(w0.x ^ w1.x ^ w2.x, w0.y ^ w1.y ^ w2.y);
+        if (out) q[(long)i * pitch] = v;
+        w0 = w1;
+        w1 = w2;
+    }
+}
 
 int main() {
     const size_t bytes = (size_t)128 << 20;
@@ -83,6 +106,24 @@ int main() {
             }
             printf("colwalk pitch %ld rows/wave %5d waves %6d: %7.1f us\n", pitch, rows, waves, best * 1e3);
         }
+    }
+    for (int rows : {34, 45, 90}) {
+        const long pitch = 514;
+        // rows the 128 MiB buffer holds, minus the two rows the window reads ahead
+        const int H = (int)((bytes / 8) / pitch) - 2, nseg = (int)((pitch - 2 + 61) / 62);
+        const int waves = nseg * ((H + rows - 1) / rows);
+        float best = 1e30f;
+        for (int rep = 0; rep < 10; ++rep) {
+            CK(hipEventRecord(e0, 0));
+            hipLaunchKernelGGL(colwalk62, dim3((waves + 3) / 4), dim3(256), 0, 0, (const uint2*)a, (uint2*)b, pitch, nseg,
+                               rows, H);
+            CK(hipEventRecord(e1, 0));
+            CK(hipEventSynchronize(e1));
+            float ms = 0;
+            CK(hipEventElapsedTime(&ms, e0, e1));
+            if (ms < best) best = ms;
+        }
+        printf("colwalk62 (halo lanes do not store, 3-row window) rows/wave %d waves %d: %7.1f us\n", rows, waves, best * 1e3);
     }
     return 0;
 }
