@@ -153,6 +153,7 @@ class HipEngine : public Engine {
     ~HipEngine() override {
         hipStreamSynchronize(s_comp_);
         hipStreamSynchronize(s_comm_);
+        destroy_dual_graphs();
         for (auto& kv : sub_plans_) hipFree(kv.second.d);
         for (auto& sb : sub_buf_)
             for (u64* b : sb)
@@ -254,9 +255,10 @@ class HipEngine : public Engine {
     // Graph shape of run(): m supersteps of k generations per replay; false when run() stays eager.
     bool graph_shape(int& k, int& m) {
         if (!cfg_.graph || cfg_.profile) return false;
-        // Sub-tile supersteps stay eager: captured (fork/join across two streams) they replayed
-        // slower than eager launches on MI355X / ROCm 7.2 (32768^2: 14.2 vs 12.8 us/gen over 20
-        // generations, 13.0 vs 10.4 over 256; profiles/short_run_probe.txt).
+        // Sub-tile supersteps are not captured as a whole: captured with their fork/join across two
+        // streams they replayed slower than eager launches on MI355X / ROCm 7.2 (32768^2: 14.2 vs
+        // 12.8 us/gen over 20 generations, 13.0 vs 10.4 over 256; profiles/short_run_probe.txt).
+        // A single-stream graph per half and superstep is available (GOL_SUBTILE_GRAPHS=1), also slower.
         if (dual_) return false;
         k = cfg_.compat ? 1 : superstep_depth();
         m = cfg_.graph_supersteps;
@@ -430,6 +432,7 @@ class HipEngine : public Engine {
     // Free the sub-tile buffers, plans and copy lists (the measurement chose one tile).
     void teardown_dual() {
         synchronize();
+        destroy_dual_graphs();
         for (auto& kv : sub_plans_) hipFree(kv.second.d);
         sub_plans_.clear();
         for (auto& sb : sub_buf_)
@@ -445,6 +448,10 @@ class HipEngine : public Engine {
         const std::vector<int>& ps = pass_depths(k);
         for (size_t j = 0; j < ps.size(); ++j)
             for (int s = 0; s < 2; ++s) sub_plan(s, ps[j], ext_after(ps, j));
+    }
+    void destroy_dual_graphs() {
+        for (auto& kv : dual_graphs_) hipGraphExecDestroy(kv.second);
+        dual_graphs_.clear();
     }
 
     const DevPlan& sub_plan(int s, int k, i64 e) {
@@ -501,7 +508,7 @@ class HipEngine : public Engine {
         prepare_dual(k);
         const int p = sub_cur_;
         const int a = (p + 1) % 3, b = (p + 2) % 3;  // the passes alternate a, b, a, ... (never p)
-        const i64 h0 = sub_L_[0].h, h1 = sub_L_[1].h;
+        const i64 h1 = sub_L_[1].h;
         HIP_CHECK(hipStreamWaitEvent(s_comp_, ev_sub_b_, 0));  // half 1's previous superstep is done
         if (!self_y()) {
             // the one-tile engine's canonical messages (Engine::halo_items, 1-D): N then S
@@ -518,38 +525,86 @@ class HipEngine : public Engine {
         } else {
             HIP_CHECK(hipStreamWaitEvent(s_comm_, ev_sub_a_, 0));  // half 0's previous superstep is done
         }
-        const std::vector<int>& ps = pass_depths(k);
-        hipk::StepParams sp[2], sp0[2];
+        // Each half's passes: eager launches on its stream, or (GOL_SUBTILE_GRAPHS=1) one replay of a
+        // graph captured at init per half, start buffer and depth.  The cross-half order stays in
+        // the events around them.
         for (int s = 0; s < 2; ++s) {
-            const Layout& Ls = sub_L_[s];
-            const int o = 1 - s;  // the other half
-            sp[s] = hipk::StepParams{Ls.pitch, (i32)Ls.h, (i32)Ls.nw, Ls.R, sub_flags()};
-            sp0[s] = sp[s];
-            sp0[s].flags |= hipk::STEP_SEAM;
-            // rows above half 0 / below half 1: the rank's ghost rows (exchanged) or, on a torus
-            // without neighbours, the other half's far edge; between the halves: the other's edge
-            const bool wrap = self_y();
-            sp0[s].above = s == 0 ? (wrap ? sub_rows(o, p, sub_L_[o].h) : sub_rows(s, p, 0)) : sub_rows(o, p, h0);
-            sp0[s].below = s == 1 ? (wrap ? sub_rows(o, p, 0) : sub_rows(s, p, h1)) : sub_rows(o, p, 0);
-        }
-        // Launches alternate between the halves (pass j of half 0, pass j of half 1, ...): issued half
-        // by half, the second stream's first kernel started ~18 us after the first's (three host
-        // launches later), and the superstep ended on one half's lone tail (kernel trace of the
-        // driver's 20-generation bench, profiles/).
-        int q = p;
-        for (size_t j = 0; j < ps.size(); ++j) {
-            const int dsti = (j % 2 == 0) ? a : b;
-            for (int s = 0; s < 2; ++s) {
-                const DevPlan& pl = sub_plan(s, ps[j], ext_after(ps, j));
-                hipk::launch_step(ps[j], sub_buf_[s][q], sub_buf_[s][dsti], pl.d, pl.waves, j == 0 ? sp0[s] : sp[s],
-                                  s ? s_comm_ : s_comp_);
+            hipStream_t st = s ? s_comm_ : s_comp_;
+            if (hipGraphExec_t ex = dual_graph(s, p, k)) {
+                HIP_CHECK(hipGraphLaunch(ex, st));
+                stats_.graph_launches += 1;
+            } else {
+                launch_half(s, p, k, st);
             }
-            q = dsti;
         }
         HIP_CHECK(hipEventRecord(ev_sub_a_, s_comp_));
         HIP_CHECK(hipEventRecord(ev_sub_b_, s_comm_));
         HIP_CHECK(hipGetLastError());
-        sub_cur_ = (ps.size() % 2) ? a : b;
+        sub_cur_ = (pass_depths(k).size() % 2) ? a : b;
+    }
+
+    // The kernel passes of half s in a superstep of k generations that starts from buffer p.
+    void launch_half(int s, int p, int k, hipStream_t st) {
+        const std::vector<int>& ps = pass_depths(k);
+        const int a = (p + 1) % 3, b = (p + 2) % 3;  // the passes alternate a, b, a, ... (never p)
+        const Layout& Ls = sub_L_[s];
+        const int o = 1 - s;  // the other half
+        hipk::StepParams sp{Ls.pitch, (i32)Ls.h, (i32)Ls.nw, Ls.R, sub_flags()};
+        hipk::StepParams sp0 = sp;
+        sp0.flags |= hipk::STEP_SEAM;
+        // rows above half 0 / below half 1: the rank's ghost rows (exchanged) or, on a torus without
+        // neighbours, the other half's far edge; between the halves: the other half's edge
+        const bool wrap = self_y();
+        const i64 h0 = sub_L_[0].h, h1 = sub_L_[1].h;
+        sp0.above = s == 0 ? (wrap ? sub_rows(o, p, sub_L_[o].h) : sub_rows(s, p, 0)) : sub_rows(o, p, h0);
+        sp0.below = s == 1 ? (wrap ? sub_rows(o, p, 0) : sub_rows(s, p, h1)) : sub_rows(o, p, 0);
+        int q = p;
+        for (size_t j = 0; j < ps.size(); ++j) {
+            const int dsti = (j % 2 == 0) ? a : b;
+            const DevPlan& pl = sub_plan(s, ps[j], ext_after(ps, j));
+            hipk::launch_step(ps[j], sub_buf_[s][q], sub_buf_[s][dsti], pl.d, pl.waves, j == 0 ? sp0 : sp, st);
+            q = dsti;
+        }
+    }
+
+    // Graph of launch_half(s, p, k): captured at init only (capture_dual_graphs), nullptr otherwise.
+    // Opt-in (GOL_SUBTILE_GRAPHS=1): replayed per half and superstep, these measured slower than the
+    // eager launches on MI355X / ROCm 7.2 (32768^2, same box, alternating: 20 generations 13.06-13.23
+    // vs 12.75-12.96 us/gen, 2000 generations 10.35 vs 10.24; profiles/subtile_graphs_ab.txt), as did
+    // one graph of both halves with fork/join events (see graph_shape).
+    bool dual_graphs_on() const { return cfg_.graph && !cfg_.profile && graph_ok_ && env_int("GOL_SUBTILE_GRAPHS", 0) != 0; }
+    hipGraphExec_t dual_graph(int s, int p, int k) {
+        if (!dual_graphs_on()) return nullptr;
+        auto it = dual_graphs_.find((s * 3 + p) * 1000 + k);
+        return it == dual_graphs_.end() ? nullptr : it->second;
+    }
+    void capture_dual_graphs(int k) {
+        if (!dual_graphs_on()) return;
+        for (int s = 0; s < 2; ++s)
+            for (int p = 0; p < 3; ++p) {
+                const int key = (s * 3 + p) * 1000 + k;
+                if (dual_graphs_.count(key)) continue;
+                hipStream_t st = s ? s_comm_ : s_comp_;
+                hipGraph_t graph = nullptr;
+                hipGraphExec_t exec = nullptr;
+                try {
+                    HIP_CHECK(hipStreamBeginCapture(st, hipStreamCaptureModeRelaxed));
+                    launch_half(s, p, k, st);
+                    HIP_CHECK(hipStreamEndCapture(st, &graph));
+                    HIP_CHECK(hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0));
+                    HIP_CHECK(hipGraphDestroy(graph));
+                    HIP_CHECK(hipGraphUpload(exec, st));
+                } catch (const Error& e) {
+                    hipGraph_t g2 = nullptr;
+                    hipStreamEndCapture(st, &g2);
+                    if (g2) hipGraphDestroy(g2);
+                    hipGetLastError();
+                    graph_ok_ = false;
+                    fprintf(stderr, "[gol] sub-tile graph capture disabled: %s\n", e.what());
+                    return;
+                }
+                dual_graphs_[key] = exec;
+            }
     }
 
     const DevPlan& full_plan_stats() {
@@ -624,10 +679,12 @@ class HipEngine : public Engine {
         // remainder of the hinted run length), so neither graph capture nor a hinted timed loop
         // builds or uploads a plan.  Other remainders are built on first use.
         for (int k : init_depths()) {
-            if (dual_)
+            if (dual_) {
                 prepare_dual(k);
-            else
+                capture_dual_graphs(k);
+            } else {
                 prepare(k);
+            }
         }
         prewarm_graph();
         if (dual_) {
@@ -640,6 +697,7 @@ class HipEngine : public Engine {
             synchronize();
             stats_.exchanges = 0;
             stats_.halo_bytes = 0;
+            stats_.graph_launches = 0;
         }
         spin_up();  // init ends with the GPU at its steady clock (plan building and captures idle it)
         const DevPlan& fp = full_plan_stats();
@@ -1542,6 +1600,7 @@ class HipEngine : public Engine {
     bool sub_current_ = false;  // the halves hold the current board
     bool canon_stale_ = false;  // buf_[cur_] lags the halves (sync_canonical before reading it)
     std::map<int, DevPlan> sub_plans_;
+    std::map<int, hipGraphExec_t> dual_graphs_;  // (half, start buffer, depth) -> launch_half graph
     hipEvent_t ev_sub_a_ = nullptr, ev_sub_b_ = nullptr;  // half 0 / half 1 done with its last superstep
     hipEvent_t ev_sub_x_ = nullptr;                        // the rank's exchange (into both halves) done
     std::map<int, DevCopies> copies_;

@@ -129,16 +129,30 @@ def test_run_hint_single_graph(gol):
 @pytest.mark.parametrize("subtiles", [0, 2])
 def test_run_hint_short_run(gol, subtiles):
     """A hinted run shorter than one superstep (the driver's bench: 20 generations, R = 64): one graph
-    replay in the one-tile mode; eager (never captured) in the sub-tile mode.  Exact either way."""
+    replay in the one-tile mode; eager in the sub-tile mode (its per-half graphs are opt-in: measured
+    slower).  Exact either way."""
     N, hint = 1024, 20
     s = _sim(gol, N, halo_depth=64, kernel="temporal", run_hint=hint, subtiles=subtiles).init(5, seed=23)
     assert s.stats()["schedule"].endswith("+subtiles2") == (subtiles == 2), s.stats()
     s.step(5)  # unhinted: eager
     g0 = s.stats()["graph_launches"]
+    assert g0 == 0, s.stats()
     s.step(hint)
     assert s.stats()["graph_launches"] - g0 == (0 if subtiles else 1), s.stats()
     s.step(hint)
     assert np.array_equal(s.board(), numpy_step(initial_board(5, N, 1, True, 23), 5 + 2 * hint))
+
+
+def test_subtile_graphs_opt_in(gol, monkeypatch):
+    """GOL_SUBTILE_GRAPHS=1: each half's passes replayed from a graph captured at init (per half,
+    start buffer and hinted depth), across the three-buffer rotation; exact against numpy."""
+    monkeypatch.setenv("GOL_SUBTILE_GRAPHS", "1")
+    N, hint = 1024, 40
+    s = _sim(gol, N, halo_depth=16, kernel="temporal", run_hint=hint, subtiles=2).init(5, seed=29)
+    for _ in range(4):
+        s.step(hint)
+    assert s.stats()["graph_launches"] >= 2 * 4 * (hint // 16), s.stats()
+    assert np.array_equal(s.board(), numpy_step(initial_board(5, N, 1, True, 29), 4 * hint))
 
 
 @pytest.mark.parametrize("N,R,gens", [(1024, 32, 200), (1088, 16, 77), (4096, 64, 150), (576, 8, 61)])
