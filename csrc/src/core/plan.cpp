@@ -2,6 +2,8 @@
 #include "gol/plan.hpp"
 
 #include <algorithm>
+#include <cstdlib>
+#include <string>
 #include <map>
 
 namespace gol {
@@ -116,14 +118,21 @@ std::vector<LaneDesc> build_plan(const std::vector<Region>& regions, i64 nw, i64
                                  bool xwrap, PlanStats* stats, int wg_waves, int xcds) {
     std::vector<std::vector<Item>> packed = pack_waves(regions, nw, h, rows_per_chunk);
     i64 nwaves = round_up(std::max<i64>(1, (i64)packed.size()), kWavesPerBlock);
-    // XCD-aware order.  Vertically adjacent segments of a column share 2k input rows, so the
-    // full-width segments are ordered column-major (narrow, packed waves stay last); then whole
-    // workgroups are permuted so that XCD x — workgroup b is dispatched to XCD b % xcds — runs a
-    // contiguous stretch of that order and the shared rows are hits in its own L2.
-    std::stable_sort(packed.begin(), packed.end(), [](const std::vector<Item>& a, const std::vector<Item>& b) {
+    // XCD-aware order.  The full-width segments are sorted (narrow, packed waves stay last), then
+    // whole workgroups are permuted so that XCD x — workgroup b is dispatched to XCD b % xcds — runs
+    // a contiguous stretch of that order: neighbouring segments, which share halo rows and words,
+    // are hits in its own L2.  Row-major (default): the full-width segments of a row band are consecutive, so an XCD's
+    // stretch of the order is a band of whole rows and its stores cover whole rows of HBM.  The
+    // column-major order (GOL_PLAN_ORDER=col, round 1's choice for vertical halo reuse in L2, which
+    // a band of rows keeps too) left each XCD writing one 496-byte piece of every row: measured
+    // 32768^2 K=1 passes 71 -> 61 us, K=4 17.5 -> 16.1 us/gen, K=8 11.49 -> 11.20 (two halves on two
+    // streams), 16384^2 K=8 4.20 -> 4.11 (profiles/plan_order_ab.txt).
+    const bool row_major = !(getenv("GOL_PLAN_ORDER") && std::string(getenv("GOL_PLAN_ORDER")) == "col");
+    std::stable_sort(packed.begin(), packed.end(), [row_major](const std::vector<Item>& a, const std::vector<Item>& b) {
         const bool fa = a.size() == 1 && a[0].lanes() == kWaveLanes, fb = b.size() == 1 && b[0].lanes() == kWaveLanes;
         if (fa != fb) return fa;
         if (!fa) return false;
+        if (row_major) return a[0].r0 != b[0].r0 ? a[0].r0 < b[0].r0 : a[0].c0 < b[0].c0;
         return a[0].c0 != b[0].c0 ? a[0].c0 < b[0].c0 : a[0].r0 < b[0].r0;
     });
     std::vector<std::vector<Item>> waves((size_t)nwaves);
