@@ -503,13 +503,25 @@ class HipEngine : public Engine {
         canon_stale_ = false;
     }
 
+    // Make `s` wait for `ev` unless it has completed already.  A cross-queue wait costs the waiting
+    // queue ~20 us even on a completed event (kernel trace of the driver's 20-generation bench: the
+    // second half's first kernel started 23 us after the first half's), and at the start of a run()
+    // that follows a synchronisation every event has completed.  (Never inside a graph capture: the
+    // sub-tile supersteps are not captured.)
+    void wait_pending(hipStream_t s, hipEvent_t ev) {
+        const hipError_t q = hipEventQuery(ev);
+        if (q == hipSuccess) return;
+        if (q != hipErrorNotReady) HIP_CHECK(q);
+        HIP_CHECK(hipStreamWaitEvent(s, ev, 0));
+    }
+
     // One sub-tile superstep: sub-tile 0 on the compute stream, 1 on the second stream.
     void dual_superstep(int k) {
         prepare_dual(k);
         const int p = sub_cur_;
         const int a = (p + 1) % 3, b = (p + 2) % 3;  // the passes alternate a, b, a, ... (never p)
         const i64 h1 = sub_L_[1].h;
-        HIP_CHECK(hipStreamWaitEvent(s_comp_, ev_sub_b_, 0));  // half 1's previous superstep is done
+        wait_pending(s_comp_, ev_sub_b_);  // half 1's previous superstep is done
         if (!self_y()) {
             // the one-tile engine's canonical messages (Engine::halo_items, 1-D): N then S
             std::vector<Message> sends, recvs;
@@ -523,19 +535,22 @@ class HipEngine : public Engine {
             HIP_CHECK(hipEventRecord(ev_sub_x_, s_comp_));  // also implies half 0's previous superstep
             HIP_CHECK(hipStreamWaitEvent(s_comm_, ev_sub_x_, 0));
         } else {
-            HIP_CHECK(hipStreamWaitEvent(s_comm_, ev_sub_a_, 0));  // half 0's previous superstep is done
+            wait_pending(s_comm_, ev_sub_a_);  // half 0's previous superstep is done
         }
-        // Each half's passes: eager launches on its stream, or (GOL_SUBTILE_GRAPHS=1) one replay of a
-        // graph captured at init per half, start buffer and depth.  The cross-half order stays in
-        // the events around them.
-        for (int s = 0; s < 2; ++s) {
-            hipStream_t st = s ? s_comm_ : s_comp_;
-            if (hipGraphExec_t ex = dual_graph(s, p, k)) {
-                HIP_CHECK(hipGraphLaunch(ex, st));
-                stats_.graph_launches += 1;
-            } else {
-                launch_half(s, p, k, st);
-            }
+        // Each half's passes: eager launches on its stream, alternating between the halves (pass j
+        // of half 0, pass j of half 1, ...: issued half by half, the second stream's first kernel
+        // started ~20 us after the first's, three host launches later, and the superstep ended on one
+        // half's lone tail; kernel traces of the driver's 20-generation bench), or
+        // (GOL_SUBTILE_GRAPHS=1) one replay per half of a graph captured at init per half, start
+        // buffer and depth.  The cross-half order stays in the events around them.
+        hipGraphExec_t gx[2] = {dual_graph(0, p, k), dual_graph(1, p, k)};
+        if (gx[0] && gx[1]) {
+            for (int s = 0; s < 2; ++s) HIP_CHECK(hipGraphLaunch(gx[s], s ? s_comm_ : s_comp_));
+            stats_.graph_launches += 2;
+        } else {
+            const int np = (int)pass_depths(k).size();
+            for (int j = 0; j < np; ++j)
+                for (int s = 0; s < 2; ++s) launch_half(s, p, k, s ? s_comm_ : s_comp_, j);
         }
         HIP_CHECK(hipEventRecord(ev_sub_a_, s_comp_));
         HIP_CHECK(hipEventRecord(ev_sub_b_, s_comm_));
@@ -543,8 +558,9 @@ class HipEngine : public Engine {
         sub_cur_ = (pass_depths(k).size() % 2) ? a : b;
     }
 
-    // The kernel passes of half s in a superstep of k generations that starts from buffer p.
-    void launch_half(int s, int p, int k, hipStream_t st) {
+    // The kernel passes of half s in a superstep of k generations that starts from buffer p (only
+    // pass `only` when >= 0).
+    void launch_half(int s, int p, int k, hipStream_t st, int only = -1) {
         const std::vector<int>& ps = pass_depths(k);
         const int a = (p + 1) % 3, b = (p + 2) % 3;  // the passes alternate a, b, a, ... (never p)
         const Layout& Ls = sub_L_[s];
@@ -561,8 +577,10 @@ class HipEngine : public Engine {
         int q = p;
         for (size_t j = 0; j < ps.size(); ++j) {
             const int dsti = (j % 2 == 0) ? a : b;
-            const DevPlan& pl = sub_plan(s, ps[j], ext_after(ps, j));
-            hipk::launch_step(ps[j], sub_buf_[s][q], sub_buf_[s][dsti], pl.d, pl.waves, j == 0 ? sp0 : sp, st);
+            if (only < 0 || (int)j == only) {
+                const DevPlan& pl = sub_plan(s, ps[j], ext_after(ps, j));
+                hipk::launch_step(ps[j], sub_buf_[s][q], sub_buf_[s][dsti], pl.d, pl.waves, j == 0 ? sp0 : sp, st);
+            }
             q = dsti;
         }
     }
