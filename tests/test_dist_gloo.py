@@ -37,7 +37,8 @@ def _free_port():
 
 
 @pytest.mark.parametrize("P,kw", [(2, {}), (2, {"decomp": "2d", "grid": "2x1", "global_mode": True, "halo_depth": 5}),
-                                  (4, {"decomp": "2d", "grid": "2x2", "global_mode": True})])
+                                  (4, {"decomp": "2d", "grid": "2x2", "global_mode": True}),
+                                  (6, {"decomp": "2d", "grid": "3x2", "global_mode": True})])
 def test_gloo_multiprocess(tmp_path, P, kw):
     import json
 
@@ -65,3 +66,8 @@ def test_gloo_multiprocess(tmp_path, P, kw):
         full[info["row0"] : info["row0"] + b.shape[0], info["col0"] : info["col0"] + b.shape[1]] = b
     assert np.array_equal(full, ref)
     assert len({i["fp"] for i in infos}) == 1
+    # the reference-format dumps (2-D: tile/strip blocks routed point to point over gloo)
+    from gol_amd.utils import read_dump
+
+    parts = sorted(read_dump(str(tmp_path / f"Rank_{r}_of_{P}.txt"))[1:] for r in range(P))
+    assert np.array_equal(np.vstack([c for _, c in parts]), ref)
