@@ -41,7 +41,10 @@ struct Region {
 
 static constexpr int kWaveLanes = 64;
 static constexpr int kSegWords = kWaveLanes - 2;  // output words of a full-width segment
-static constexpr int kWavesPerBlock = 4;          // 256-thread workgroups of independent waves
+#ifndef GOL_WAVES_PER_BLOCK  // measurement builds (kbench) may change it
+#define GOL_WAVES_PER_BLOCK 4
+#endif
+static constexpr int kWavesPerBlock = GOL_WAVES_PER_BLOCK;  // 256-thread workgroups of independent waves
 
 struct PlanStats {
     i64 waves = 0;        // including padding waves

@@ -278,7 +278,7 @@ struct WaveRunner {
 #define GOL_TEMPORAL_OCC
 #endif
 template <int K, int ROWS>
-__global__ __launch_bounds__(256) GOL_TEMPORAL_OCC void step_temporal(const u64* __restrict__ src, u64* __restrict__ dst,
+__global__ __launch_bounds__(64 * kWavesPerBlock) GOL_TEMPORAL_OCC void step_temporal(const u64* __restrict__ src, u64* __restrict__ dst,
                                                                       const LaneDesc* __restrict__ plan, StepParams p) {
     const int wv = threadIdx.x >> 6;
     const i64 wave = (i64)blockIdx.x * kWavesPerBlock + wv;
@@ -645,8 +645,8 @@ static const void* kernel_of(int k, u32 flags) {
 int step_blocks_per_cu(int k, u32 flags) {
     const void* f = kernel_of(k, flags);
     int nb = 0;
-    if (!f || hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, f, 256, 0) != hipSuccess || nb < 1) return 1;
-    return std::min(nb, 8);
+    if (!f || hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, f, 64 * kWavesPerBlock, 0) != hipSuccess || nb < 1) return 1;
+    return std::min(nb, 32 / kWavesPerBlock);
 }
 
 // Per-device trash buffers (StepParams::trash).
@@ -672,7 +672,7 @@ void launch_step(int k, const u64* src, u64* dst, const LaneDesc* plan, i64 n_wa
                  hipStream_t s) {
     const void* f = kernel_of(k, p.flags);
     if (!f) throw Error(strprintf("no step kernel instantiated for depth %d", k));
-    const dim3 grid((unsigned)(n_waves / kWavesPerBlock)), block(256);
+    const dim3 grid((unsigned)(n_waves / kWavesPerBlock)), block(64 * kWavesPerBlock);
     StepParams pp = p;
     if (!pp.trash) pp.trash = trash_of_current_device();
     void* args[] = {(void*)&src, (void*)&dst, (void*)&plan, (void*)&pp};
