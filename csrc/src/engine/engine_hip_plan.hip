@@ -1,0 +1,148 @@
+// gol-mi355x: HipEngine — work plans of the kernel passes, pass cuts and the interior/boundary regions of a tile.
+#include "hip_engine.hpp"
+
+namespace gol {
+namespace hipeng {
+
+// Kernel passes of a superstep of k generations.  Once the pass costs are measured
+// (measure_pass_costs), the cheapest cut over the instantiated depths <= K; before that (and with
+// an explicit GOL_KERNEL_DEPTH) the fewest passes of at most K with depths as equal as possible
+// (20 = 7 + 7 + 6, not 8 + 8 + 4).  A pass streams the board through HBM once whatever its
+// depth, so shallow passes cost nearly as much as deep ones (32768^2: ~70-80 us for any depth
+// <= 6, ~90 us at 8; profiles/kb_depth_sweep.txt).
+const std::vector<int>& HipEngine::pass_depths(int k) {
+    const int key = k + (dual_ ? (1 << 20) : 0);
+    auto it = passes_.find(key);
+    if (it != passes_.end()) return it->second;
+    // every kind may be temporal, unless only the (any-depth) tile kernel runs; sub-tiles always
+    // run the temporal kernel at its own depth
+    const bool any_depth = !dual_ && (cfg_.kernel == "tile" || (tuned_ && !split_ && tile_kernel(0)));
+    auto ok = [&](int d) { return any_depth || hipk::step_depth_supported(d); };
+    const int K = std::max(1, dual_ ? tdepth_ : kdepth_);
+    std::vector<int> ps;
+    if (tuned_ && !pass_us_.empty() && !any_depth) {
+        // cheapest cut by the measured per-depth pass times (dynamic programming over k)
+        std::vector<double> best((size_t)k + 1, 1e300);
+        std::vector<int> pick((size_t)k + 1, 0);
+        best[0] = 0;
+        for (int x = 1; x <= k; ++x)
+            for (const auto& dc : pass_us_)
+                if (dc.first <= x && best[(size_t)(x - dc.first)] + dc.second < best[(size_t)x]) {
+                    best[(size_t)x] = best[(size_t)(x - dc.first)] + dc.second;
+                    pick[(size_t)x] = dc.first;
+                }
+        for (int x = k; x > 0; x -= pick[(size_t)x]) ps.push_back(pick[(size_t)x]);
+        std::sort(ps.begin(), ps.end(), std::greater<int>());
+        return passes_.emplace(key, ps).first->second;
+    }
+    const int n = (k + K - 1) / K;
+    bool balanced = true;
+    for (int j = 0; j < n; ++j) {
+        const int d = k / n + (j < k % n ? 1 : 0);
+        if (!ok(d)) balanced = false;
+        ps.push_back(d);
+    }
+    if (!balanced) {  // greedy over the instantiated depths
+        ps.clear();
+        for (int left = k; left > 0;) {
+            int d = std::min(left, K);
+            if (!any_depth) d = supported_kernel_depth(d);
+            ps.push_back(d);
+            left -= d;
+        }
+    }
+    return passes_.emplace(key, ps).first->second;
+}
+
+// Output regions of a pass of depth k whose output rows extend e rows beyond the tile (into
+// the ghost rows, 1-D multi-pass supersteps): kind 0 full, 1 interior, 2 boundary bands.
+std::vector<Region> HipEngine::regions(int kind, int k, i64 rem) const {
+    const i64 h = L_.h, nw = L_.nw;
+    const bool two_d = this->two_d();
+    // multi-pass: earlier passes also produce the ghost rows (y neighbours) and the ghost
+    // words, columns -1 and nw (x neighbours), that later passes read
+    const i64 e = self_y() ? 0 : rem;
+    const i64 xe = (!self_x() && rem > 0) ? 1 : 0;
+    if (kind == 0 || h <= 2 * (i64)k)
+        return kind == 1 ? std::vector<Region>{} : std::vector<Region>{{-e, h + e, -xe, nw + xe}};
+    if (kind == 1) {
+        if (two_d) return nw > 2 ? std::vector<Region>{{k, h - k, 1, nw - 1}} : std::vector<Region>{};
+        return {{k, h - k, 0, nw}};
+    }
+    std::vector<Region> r = {{-e, k, -xe, nw + xe}, {h - k, h + e, -xe, nw + xe}};
+    if (two_d) {
+        if (nw > 2) {
+            r.push_back({k, h - k, -xe, 1});
+            r.push_back({k, h - k, nw - 1, nw + xe});
+        } else {
+            r.push_back({k, h - k, -xe, nw + xe});
+        }
+    }
+    return r;
+}
+
+const DevPlan& HipEngine::plan(int kind, int k, i64 e) {
+    // plans depend on e only through regions(): rows beyond the tile when y has neighbours,
+    // ghost words when x has neighbours (so one plan serves every e of a local rank)
+    const i64 ek = self_y() ? (self_x() ? 0 : (e > 0 ? 1 : 0)) : e;
+    // tile plans also depend on the workgroup size (the LDS rows a tile may hold)
+    const i64 key = ((((i64)occ_ * 2 + (tile_kernel(kind) ? 1 : 0)) * 32 + (tile_kernel(kind) ? cfg_.tile_waves : 0)) * 4 +
+                     kind) * 100000 + (i64)ek * 100 + k;
+    auto it = plans_.find(key);
+    if (it != plans_.end()) return it->second;
+    std::vector<Region> rg = regions(kind, k, e);
+    DevPlan p;
+    i64 rows = cfg_.rows_per_wave;
+    if (tile_kernel(kind)) {
+        // step_tile: one workgroup per plan wave, one tile per CU per round; rows are capped by
+        // the 160 KiB of LDS (2k halo rows + the tile, double-buffered or in place), extra rounds
+        // beyond that.  The double-buffered tile is used when one round of tiles fits it (cheaper:
+        // no halo copies, one barrier per LDS pass; 8192^2: 1.45 vs 1.65 us/gen), the in-place one
+        // (twice the rows) when the double buffer would need more rounds (4096 x 32768: 2.36 vs
+        // 2.70, 16384^2: 4.58 vs 4.69; profiles/tile_inplace_ab.txt).  GOL_TILE_INPLACE=0/1 forces.
+        const i64 rdb = hipk::tile_max_rows(k, cfg_.tile_waves, step_flags() | tile_bits(false));
+        const i64 rip = hipk::tile_max_rows(k, cfg_.tile_waves, step_flags() | tile_bits(true));
+        const i64 r1 = balanced_rows_per_chunk(rg, L_.nw, L_.h, k, cus_, 1, xwrap_by_plan());
+        bool ip = tile_inplace_ > 0 || (tile_inplace_ < 0 && r1 > rdb && rip > rdb);
+        if (tile_inplace_ < 0 && rows > 0) ip = rows > rdb;
+        const i64 rmax = ip ? rip : rdb;
+        p.tflags = tile_bits(ip);
+        if (rmax < 1) throw Error(strprintf("GOL_KERNEL=tile: depth %d leaves no LDS rows", k));
+        if (rows > rmax) rows = rmax;
+        if (tile_rounds(kind, k, e) > kMaxTileRounds)
+            throw Error(strprintf("GOL_KERNEL=tile: this tile needs %lld rounds of LDS tiles; use the temporal "
+                                  "kernel for boards this large",
+                                  (long long)tile_rounds(kind, k, e)));
+        if (rows <= 0) {
+            const i64 rounds = ceil_div(r1, rmax);
+            rows = rounds <= 1 ? r1
+                               : std::min(rmax, balanced_rows_per_chunk(rg, L_.nw, L_.h, k, rounds * cus_, 1,
+                                                                        xwrap_by_plan()));
+        }
+    } else {
+        if (rows <= 0 && cfg_.waves_target > 0)
+            rows = choose_rows_per_chunk(rg, k, cfg_.waves_target, 4 * (i64)k);
+        if (rows <= 0) {
+            // one full round of resident waves (occupancy of this kernel instantiation)
+            i64 bpc = hipk::step_blocks_per_cu(k, step_flags());
+            // 256-thread blocks per CU = waves per SIMD; the tuned cap applies to the tuned depth
+            // only (shallower passes are memory bound and want every resident wave)
+            if (occ_ > 0 && k == kdepth_) bpc = std::min<i64>(bpc, occ_);
+            const i64 resident = bpc * kWavesPerBlock * cus_;
+            rows = balanced_rows_per_chunk(rg, L_.nw, L_.h, k, resident, 2 * (i64)k, xwrap_by_plan());
+        }
+    }
+    std::vector<LaneDesc> lanes = build_plan(rg, L_.nw, L_.h, rows, k, xwrap_by_plan(), &p.st,
+                                             tile_kernel(kind) ? 1 : kWavesPerBlock, cfg_.plan_xcds);
+    const std::string bad = validate_plan(lanes, L_.nw, L_.h, L_.R, k, (step_flags() & hipk::STEP_WRAP_Y) != 0);
+    if (!bad.empty()) throw Error(strprintf("refusing to launch an unsafe plan (kind %d, k %d, e %lld): %s", kind, k,
+                                            (long long)e, bad.c_str()));
+    p.waves = (i64)lanes.size() / kWaveLanes;
+    p.rows = rows;
+    HIP_CHECK(hipMalloc(&p.d, lanes.size() * sizeof(LaneDesc)));
+    upload(p.d, lanes.data(), lanes.size() * sizeof(LaneDesc));
+    return plans_.emplace(key, p).first->second;
+}
+
+}  // namespace hipeng
+}  // namespace gol

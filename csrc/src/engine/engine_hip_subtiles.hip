@@ -1,0 +1,174 @@
+// gol-mi355x: HipEngine — two sub-tiles per rank (1-D), each half on its own stream.
+#include "hip_engine.hpp"
+
+namespace gol {
+namespace hipeng {
+
+void HipEngine::setup_dual() {
+    if (sub_buf_[0][0]) return;
+    const i64 h0 = L_.h / 2;
+    sub_r0_[0] = 0;
+    sub_r0_[1] = h0;
+    for (int s = 0; s < 2; ++s) {
+        const i64 hs = s == 0 ? h0 : L_.h - h0;
+        sub_L_[s] = Layout(hs, L_.w, L_.R);
+        const size_t bytes = (size_t)(sub_L_[s].words() + hipk::kSlackRows * sub_L_[s].pitch) * 8;
+        for (int i = 0; i < 3; ++i) {
+            HIP_CHECK(hipMalloc(&sub_buf_[s][i], bytes));
+            HIP_CHECK(hipMemsetAsync(sub_buf_[s][i], 0, bytes, s_comp_));
+        }
+    }
+    if (!ev_sub_a_) {
+        HIP_CHECK(hipEventCreateWithFlags(&ev_sub_a_, hipEventDisableTiming));
+        HIP_CHECK(hipEventCreateWithFlags(&ev_sub_b_, hipEventDisableTiming));
+        HIP_CHECK(hipEventCreateWithFlags(&ev_sub_x_, hipEventDisableTiming));
+    }
+    HIP_CHECK(hipStreamSynchronize(s_comp_));
+}
+
+// Free the sub-tile buffers, plans and copy lists (the measurement chose one tile).
+void HipEngine::teardown_dual() {
+    synchronize();
+    destroy_dual_graphs();
+    for (auto& kv : sub_plans_) hipFree(kv.second.d);
+    sub_plans_.clear();
+    for (auto& sb : sub_buf_)
+        for (u64*& b : sb) {
+            if (b) hipFree(b);
+            b = nullptr;
+        }
+    dual_ = false;
+    sub_current_ = canon_stale_ = false;
+}
+
+const DevPlan& HipEngine::sub_plan(int s, int k, i64 e) {
+    const int key = (s * 100000 + (int)e * 100 + k);
+    auto it = sub_plans_.find(key);
+    if (it != sub_plans_.end()) return it->second;
+    const Layout& L = sub_L_[s];
+    std::vector<Region> rg = {{-e, L.h + e, 0, L.nw}};
+    i64 bpc = hipk::step_blocks_per_cu(k, sub_flags());
+    // waves/SIMD each half's plan is sized for: two concurrent halves fill the SIMDs between
+    // them, so 2-wave plans (taller segments, less halo) measured best (kbench: 9.85 vs 10.11
+    // us/gen at 32768^2); GOL_SUB_OCC overrides (0 = the single-tile tuned occupancy)
+    // (at the temporal pass depth; shallower passes are memory bound and want every resident
+    // wave: profiles/kb_depth_sweep.txt)
+    if (k >= tdepth_) {
+        if (cfg_.sub_occ > 0)
+            bpc = std::min<i64>(bpc, cfg_.sub_occ);
+        else if (occ_ > 0)
+            bpc = std::min<i64>(bpc, occ_);
+    }
+    const i64 rows = balanced_rows_per_chunk(rg, L.nw, L.h, k, bpc * kWavesPerBlock * cus_, 2 * (i64)k, true);
+    DevPlan p;
+    std::vector<LaneDesc> lanes = build_plan(rg, L.nw, L.h, rows, k, true, &p.st, kWavesPerBlock, cfg_.plan_xcds);
+    const std::string bad = validate_plan(lanes, L.nw, L.h, L.R, k, false);
+    if (!bad.empty()) throw Error(strprintf("refusing to launch an unsafe sub-tile plan: %s", bad.c_str()));
+    p.waves = (i64)lanes.size() / kWaveLanes;
+    p.rows = rows;
+    HIP_CHECK(hipMalloc(&p.d, lanes.size() * sizeof(LaneDesc)));
+    upload(p.d, lanes.data(), lanes.size() * sizeof(LaneDesc));
+    return sub_plans_.emplace(key, p).first->second;
+}
+
+// One sub-tile superstep: sub-tile 0 on the compute stream, 1 on the second stream.
+void HipEngine::dual_superstep(int k) {
+    prepare_dual(k);
+    const int p = sub_cur_;
+    const int a = (p + 1) % 3, b = (p + 2) % 3;  // the passes alternate a, b, a, ... (never p)
+    const i64 h1 = sub_L_[1].h;
+    wait_pending(s_comp_, ev_sub_b_);  // half 1's previous superstep is done
+    if (!self_y()) {
+        // the one-tile engine's canonical messages (Engine::halo_items, 1-D): N then S
+        std::vector<Message> sends, recvs;
+        sends.push_back({g_.nbr[DIR_N], sub_rows(0, p, 0), rows_bytes(0, k)});
+        recvs.push_back({g_.nbr[DIR_S], sub_rows(1, p, h1), rows_bytes(1, k)});
+        sends.push_back({g_.nbr[DIR_S], sub_rows(1, p, h1 - k), rows_bytes(1, k)});
+        recvs.push_back({g_.nbr[DIR_N], sub_rows(0, p, -k), rows_bytes(0, k)});
+        t_->exchange(sends, recvs, (void*)s_comp_);
+        stats_.exchanges += 1;
+        stats_.halo_bytes += (u64)(rows_bytes(0, k) + rows_bytes(1, k));
+        HIP_CHECK(hipEventRecord(ev_sub_x_, s_comp_));  // also implies half 0's previous superstep
+        HIP_CHECK(hipStreamWaitEvent(s_comm_, ev_sub_x_, 0));
+    } else {
+        wait_pending(s_comm_, ev_sub_a_);  // half 0's previous superstep is done
+    }
+    // Each half's passes: eager launches on its stream, alternating between the halves (pass j
+    // of half 0, pass j of half 1, ...: issued half by half, the second stream's first kernel
+    // started ~20 us after the first's, three host launches later, and the superstep ended on one
+    // half's lone tail; kernel traces of the driver's 20-generation bench), or
+    // (GOL_SUBTILE_GRAPHS=1) one replay per half of a graph captured at init per half, start
+    // buffer and depth.  The cross-half order stays in the events around them.
+    hipGraphExec_t gx[2] = {dual_graph(0, p, k), dual_graph(1, p, k)};
+    if (gx[0] && gx[1]) {
+        for (int s = 0; s < 2; ++s) HIP_CHECK(hipGraphLaunch(gx[s], s ? s_comm_ : s_comp_));
+        stats_.graph_launches += 2;
+    } else {
+        const int np = (int)pass_depths(k).size();
+        for (int j = 0; j < np; ++j)
+            for (int s = 0; s < 2; ++s) launch_half(s, p, k, s ? s_comm_ : s_comp_, j);
+    }
+    HIP_CHECK(hipEventRecord(ev_sub_a_, s_comp_));
+    HIP_CHECK(hipEventRecord(ev_sub_b_, s_comm_));
+    HIP_CHECK(hipGetLastError());
+    sub_cur_ = (pass_depths(k).size() % 2) ? a : b;
+}
+
+// The kernel passes of half s in a superstep of k generations that starts from buffer p (only
+// pass `only` when >= 0).
+void HipEngine::launch_half(int s, int p, int k, hipStream_t st, int only) {
+    const std::vector<int>& ps = pass_depths(k);
+    const int a = (p + 1) % 3, b = (p + 2) % 3;  // the passes alternate a, b, a, ... (never p)
+    const Layout& Ls = sub_L_[s];
+    const int o = 1 - s;  // the other half
+    hipk::StepParams sp{Ls.pitch, (i32)Ls.h, (i32)Ls.nw, Ls.R, sub_flags()};
+    hipk::StepParams sp0 = sp;
+    sp0.flags |= hipk::STEP_SEAM;
+    // rows above half 0 / below half 1: the rank's ghost rows (exchanged) or, on a torus without
+    // neighbours, the other half's far edge; between the halves: the other half's edge
+    const bool wrap = self_y();
+    const i64 h0 = sub_L_[0].h, h1 = sub_L_[1].h;
+    sp0.above = s == 0 ? (wrap ? sub_rows(o, p, sub_L_[o].h) : sub_rows(s, p, 0)) : sub_rows(o, p, h0);
+    sp0.below = s == 1 ? (wrap ? sub_rows(o, p, 0) : sub_rows(s, p, h1)) : sub_rows(o, p, 0);
+    int q = p;
+    for (size_t j = 0; j < ps.size(); ++j) {
+        const int dsti = (j % 2 == 0) ? a : b;
+        if (only < 0 || (int)j == only) {
+            const DevPlan& pl = sub_plan(s, ps[j], ext_after(ps, j));
+            hipk::launch_step(ps[j], sub_buf_[s][q], sub_buf_[s][dsti], pl.d, pl.waves, j == 0 ? sp0 : sp, st);
+        }
+        q = dsti;
+    }
+}
+
+void HipEngine::capture_dual_graphs(int k) {
+    if (!dual_graphs_on()) return;
+    for (int s = 0; s < 2; ++s)
+        for (int p = 0; p < 3; ++p) {
+            const int key = (s * 3 + p) * 1000 + k;
+            if (dual_graphs_.count(key)) continue;
+            hipStream_t st = s ? s_comm_ : s_comp_;
+            hipGraph_t graph = nullptr;
+            hipGraphExec_t exec = nullptr;
+            try {
+                HIP_CHECK(hipStreamBeginCapture(st, hipStreamCaptureModeRelaxed));
+                launch_half(s, p, k, st);
+                HIP_CHECK(hipStreamEndCapture(st, &graph));
+                HIP_CHECK(hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0));
+                HIP_CHECK(hipGraphDestroy(graph));
+                HIP_CHECK(hipGraphUpload(exec, st));
+            } catch (const Error& e) {
+                hipGraph_t g2 = nullptr;
+                hipStreamEndCapture(st, &g2);
+                if (g2) hipGraphDestroy(g2);
+                hipGetLastError();
+                graph_ok_ = false;
+                fprintf(stderr, "[gol] sub-tile graph capture disabled: %s\n", e.what());
+                return;
+            }
+            dual_graphs_[key] = exec;
+        }
+}
+
+}  // namespace hipeng
+}  // namespace gol

@@ -1,0 +1,293 @@
+// gol-mi355x: HipEngine — measurement at init: kernel autotune, superstep schedule choice, per-depth pass costs.
+#include "hip_engine.hpp"
+
+namespace gol {
+namespace hipeng {
+
+// Bring the GPU to its steady clock before anything is timed.  From idle, sclk ramps up over
+// the first ~20-30 ms of load (measured on MI355X: 32768^2 passes shrink from ~97 to ~87 us
+// while rocm-smi shows sclk rising to 2.4 GHz), which would bias the kernel autotune towards
+// whichever candidate runs last and make the first generations of a run slower than the rest.
+// The full-board kernel runs on the scratch buffer (the board is untouched) for GOL_SPINUP_MS
+// (default 100 ms for boards of >= 2^24 cells, 20 ms below; 0 = off).
+void HipEngine::spin_up() {
+    const bool big = (double)L_.h * (double)L_.w >= (double)(1 << 24);
+    const double budget_ms = (double)env_int("GOL_SPINUP_MS", big ? 100 : 20);
+    if (budget_ms <= 0 || cfg_.compat || kernel_ == "lds") return;
+    const std::string saved = kern_[0];
+    if (cfg_.kernel != "tile") kern_[0] = "temporal";  // the register kernel runs on any board
+    const int k = tile_kernel(0) ? kdepth_ : supported_kernel_depth(std::min(kdepth_, hipk::max_step_depth()));
+    const auto t0 = std::chrono::steady_clock::now();
+    for (int it = 0; it < 100000; ++it) {
+        for (int j = 0; j < 4; ++j) launch(0, k, 0, buf_[cur_], buf_[cur_ ^ 1], s_comp_);
+        HIP_CHECK(hipStreamSynchronize(s_comp_));
+        const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+        if (ms >= budget_ms) break;
+    }
+    kern_[0] = saved;
+}
+
+// Per-depth pass times of the chosen mode (temporal kernel: one tile, or the two halves on two
+// streams without joins between passes, as inside a superstep), for the pass cuts of supersteps
+// (pass_depths).  Measured rather than modelled: the cost is an HBM streaming floor plus the
+// VALU work of the depth, and code generation differs per depth (32768^2 one tile: depth 7 is
+// slower per pass than depth 8; profiles/kb_depth_sweep.txt).  Rank-local: the cut only changes
+// kernel passes, never the exchanges.
+void HipEngine::measure_pass_costs() {
+    pass_us_.clear();
+    if (cfg_.compat || cfg_.kernel_depth > 0 || kernel_ == "lds" || (!dual_ && tile_kernel(0))) return;
+    const int K = dual_ ? tdepth_ : kdepth_;
+    std::vector<int> ds;
+    for (int d = 1; d <= K; ++d)
+        if (hipk::step_depth_supported(d)) ds.push_back(d);
+    if (ds.size() < 2) return;
+    for (int d : ds) {  // every plan first: plan building idles the GPU and drops its clock
+        if (dual_) {
+            sub_plan(0, d, 0);
+            sub_plan(1, d, 0);
+        } else {
+            plan(0, d, 0);
+        }
+    }
+    hipEvent_t e0, e1;
+    HIP_CHECK(hipEventCreate(&e0));
+    HIP_CHECK(hipEventCreate(&e1));
+    spin_up();
+    const int reps = 4;
+    std::map<int, double> best;
+    for (int round = 0; round < 3; ++round)
+        for (int d : ds) {
+            HIP_CHECK(hipEventRecord(e0, s_comp_));
+            if (dual_) {
+                HIP_CHECK(hipStreamWaitEvent(s_comm_, e0, 0));
+                for (int i = 0; i < reps; ++i)
+                    for (int sub = 0; sub < 2; ++sub) {
+                        const DevPlan& pl = sub_plan(sub, d, 0);
+                        const Layout& Ls = sub_L_[sub];
+                        hipk::StepParams sp{Ls.pitch, (i32)Ls.h, (i32)Ls.nw, Ls.R, sub_flags()};
+                        hipk::launch_step(d, sub_buf_[sub][sub_cur_], sub_buf_[sub][(sub_cur_ + 1) % 3], pl.d,
+                                          pl.waves, sp, sub ? s_comm_ : s_comp_);
+                    }
+                HIP_CHECK(hipEventRecord(ev_sub_b_, s_comm_));
+                HIP_CHECK(hipStreamWaitEvent(s_comp_, ev_sub_b_, 0));
+            } else {
+                for (int i = 0; i < reps; ++i) launch(0, d, 0, buf_[cur_], buf_[cur_ ^ 1], s_comp_);
+            }
+            HIP_CHECK(hipEventRecord(e1, s_comp_));
+            HIP_CHECK(hipEventSynchronize(e1));
+            float ms = 0;
+            HIP_CHECK(hipEventElapsedTime(&ms, e0, e1));
+            const double us = ms * 1e3 / reps;
+            best[d] = round == 0 ? us : std::min(best[d], us);
+        }
+    HIP_CHECK(hipEventDestroy(e0));
+    HIP_CHECK(hipEventDestroy(e1));
+    HIP_CHECK(hipGetLastError());
+    pass_us_ = best;
+    passes_.clear();
+}
+
+void HipEngine::choose_schedule() {
+    const bool nbrs = !halo_items(L_.R).empty();  // identical on every rank (uniform grid)
+    std::vector<std::string> cands;
+    if (cfg_.force_split || (cfg_.sched == "split" && split_used())) {
+        cands = {"split"};
+    } else {
+        cands.push_back(nbrs ? "full" : "local");
+        if (cfg_.sched == "auto" && split_used()) cands.push_back("split");
+    }
+    bool dual_ok = cfg_.subtiles != 0 && cands[0] != "split" && dual_wanted();
+    if (dual_ok) {
+        double ok = dual_local_ok() ? 1.0 : 0.0;
+        if (t_->size() > 1) ok = t_->allreduce_min(ok);
+        dual_ok = ok > 0;
+    }
+    if (dual_ok) {
+        if (cfg_.subtiles == 2)
+            cands = {"subtiles"};
+        else
+            cands.push_back("subtiles");
+    }
+    std::string pick = cands[0];
+    if (cands.size() > 1) {
+        const int k = L_.R;
+        std::vector<double> best(cands.size(), 1e30);
+        spin_up();
+        for (int round = 0; round < 3; ++round)
+            for (size_t c = 0; c < cands.size(); ++c) {
+                if (round == 0) time_schedule(cands[c], k, 1);  // warm-up: connections, plans
+                synchronize();
+                t_->barrier();
+                const auto t0 = std::chrono::steady_clock::now();
+                time_schedule(cands[c], k, kSchedReps);
+                synchronize();
+                const double dt = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+                best[c] = std::min(best[c], t_->allreduce_max(dt) * 1e6 / (kSchedReps * k));
+            }
+        size_t bi = 0;
+        for (size_t c = 0; c < cands.size(); ++c) {
+            sched_us_[cands[c]] = best[c];
+            if (best[c] < best[bi]) bi = c;
+        }
+        pick = cands[bi];
+        stats_.exchanges = 0;  // the timing exchanges are not part of the run
+        stats_.halo_bytes = 0;
+    }
+    split_ = pick == "split";
+    dual_ = pick == "subtiles";
+    if (dual_) {
+        setup_dual();
+        sub_current_ = false;  // the halves hold timing scratch: load the board at the next run
+    } else if (sub_buf_[0][0]) {
+        teardown_dual();
+    }
+    passes_.clear();
+}
+
+// `reps` supersteps of k generations of schedule `c` on scratch state (see choose_schedule).
+void HipEngine::time_schedule(const std::string& c, int k, int reps) {
+    if (c == "subtiles") {
+        setup_dual();
+        dual_ = true;
+        for (int i = 0; i < reps; ++i) dual_superstep(k);
+        dual_ = false;
+        return;
+    }
+    split_ = c == "split";
+    const std::vector<int>& ps = pass_depths(k);
+    for (int i = 0; i < reps; ++i) {
+        first_pass(k, ps[0], ext_after(ps, 0), split_);
+        for (size_t j = 1; j < ps.size(); ++j) {
+            const i64 e = ext_after(ps, j);
+            launch(0, ps[j], e, buf_[cur_], buf_[cur_ ^ 1], s_comp_);
+            post(buf_[cur_ ^ 1], s_comp_, e);
+        }
+        // the next exchange waits for the whole superstep, as in tile_superstep (without this
+        // record the timed split schedule overlapped each exchange with the previous superstep's
+        // later passes, which a real run cannot: 2.78 timed vs 3.26 us/gen run, 4096 x 32768)
+        if (ps.size() > 1) mark_ready();
+    }
+    split_ = false;
+}
+
+// GOL_KERNEL=auto: for every plan kind a run uses (full tile; interior + boundary bands when
+// split), time one superstep of each candidate kernel (into the scratch buffer, so the board is
+// untouched) and keep the faster one.  The register pipeline wins on big regions; the
+// LDS-resident tile kernel on small ones — its vertical halo is shared by a whole workgroup and
+// its dependency chains are short, which is what the k-row boundary bands need.
+void HipEngine::autotune_kernel() {
+    hipEvent_t e0, e1;
+    HIP_CHECK(hipEventCreate(&e0));
+    HIP_CHECK(hipEventCreate(&e1));
+    // time one pass of kernel `kern` at depth k on plan `kind`; returns ms per generation
+    // build_only: construct (and upload) the plan only.  Every plan of a tuning round is built
+    // before the GPU is spun up and the kernels are timed: building a tile plan for a large
+    // board is ~0.1 s of host work, long enough for the clock to drop again.
+    auto time_pass = [&](int kind, const char* kern, int k, bool build_only = false) -> float {
+        kern_[kind] = kern;
+        if (kern_[kind] == "tile" && (tile_rows_cap(k) < 1 || tile_rounds(kind, k, 0) > kMaxTileRounds))
+            return 1e30f;  // LDS tiles only pay off for small regions (docs/PERFORMANCE.md)
+        if (kern_[kind] == "temporal" && !hipk::step_depth_supported(k)) return 1e30f;
+        if (build_only) {
+            plan(kind, k, 0);
+            return 0.f;
+        }
+        const bool tile = kern_[kind] == "tile";
+        hipStream_t s = s_comp_;
+        launch(kind, k, 0, buf_[cur_], buf_[cur_ ^ 1], s);  // warm-up (and plan build)
+        HIP_CHECK(hipEventRecord(e0, s));
+        for (int i = 0; i < 3; ++i) launch(kind, k, 0, buf_[cur_], buf_[cur_ ^ 1], s);
+        HIP_CHECK(hipEventRecord(e1, s));
+        HIP_CHECK(hipEventSynchronize(e1));
+        float ms = 0;
+        HIP_CHECK(hipEventElapsedTime(&ms, e0, e1));
+        const float per_gen = ms / 3 / (float)k;
+        const std::string key = tile ? strprintf("%d:%s@%dx%dw", kind, kern, k, cfg_.tile_waves)
+                                     : (occ_ ? strprintf("%d:%s@%d/%dw", kind, kern, k, occ_)
+                                             : strprintf("%d:%s@%d", kind, kern, k));
+        auto it = tune_ms_.find(key);
+        tune_ms_[key] = it == tune_ms_.end() ? per_gen : std::min(it->second, per_gen);  // best round
+        return per_gen;
+    };
+    // full-tile kernel and pass depth: the register pipeline at the auto depth, the LDS tile
+    // kernel at that depth and (deeper passes amortise its staging) twice that depth
+    // The tile workgroup size (the threadsPerBlock hint, or GOL_TILE_WAVES) is a candidate
+    // dimension too unless GOL_TILE_WAVES fixed it: the measured default, 8 waves, is also tried.
+    struct Cand {
+        const char* kern;
+        int k, nw;
+        int occ = 0;  // temporal: waves per SIMD of the plan (0 = full occupancy)
+    };
+    const int k0 = cfg_.compat ? 1 : kdepth_;
+    const int nw0 = cfg_.tile_waves;
+    std::vector<int> nws = {nw0};
+    if (cfg_.tune_tile_waves && nw0 != 8) nws.push_back(8);
+    std::vector<Cand> cands = {{"temporal", k0, nw0}};
+    // fewer, taller temporal waves (2 per SIMD instead of 3) for small tiles: less vertical halo
+    if (!cfg_.compat && cfg_.rows_per_wave <= 0 && cfg_.waves_target <= 0 &&
+        hipk::step_blocks_per_cu(k0, step_flags()) > 2)
+        cands.push_back({"temporal", k0, nw0, 2});
+    // Deeper tile passes: 2 k0 always; 3 k0 and 4 k0 (any depth) when the full-tile plan is the
+    // only kind a superstep runs (no split), so the passes need not suit the register kernel.
+    // 8192^2 on one GPU: tile@16 1.51-1.52, tile@24 1.475, tile@32 1.496 us/gen.
+    std::vector<int> kts = {k0};
+    if (!cfg_.compat && cfg_.kernel_depth == 0) {
+        const int kmax = std::min(L_.R, 32);
+        const int k2 = supported_kernel_depth(std::min(2 * k0, kmax));
+        if (k2 > k0) kts.push_back(k2);
+        if (!split_used())
+            for (int m = 3; m <= 4 && m * k0 <= kmax; ++m) kts.push_back(m * k0);
+    }
+    for (int nw : nws)
+        for (int k : kts) cands.push_back({"tile", k, nw});
+    for (const auto& c : cands) {
+        occ_ = c.occ;
+        time_pass(0, c.kern, c.k, true);
+    }
+    spin_up();
+    // Three interleaved rounds, best of each candidate: some candidates are within 1-2% of each
+    // other (32768^2: the 3- and 2-waves/SIMD plans), and one 3-pass sample picks on noise.
+    std::vector<float> tbest(cands.size(), 1e30f);
+    for (int round = 0; round < 3; ++round)
+        for (size_t i = 0; i < cands.size(); ++i) {
+            cfg_.tile_waves = cands[i].nw;
+            occ_ = cands[i].occ;
+            tbest[i] = std::min(tbest[i], time_pass(0, cands[i].kern, cands[i].k));
+        }
+    float best = 1e30f;
+    Cand pick = cands[0];
+    for (size_t i = 0; i < cands.size(); ++i)
+        if (tbest[i] < best) {
+            best = tbest[i];
+            pick = cands[i];
+        }
+    kern_[0] = pick.kern;
+    kdepth_ = pick.k;
+    cfg_.tile_waves = pick.nw;
+    occ_ = pick.occ;
+    passes_.clear();
+    // interior / boundary plans of split supersteps, at the chosen pass depth
+    if (split_used()) {
+        for (int kind : {1, 2})
+            for (const char* c : {"temporal", "tile"}) time_pass(kind, c, kdepth_, true);
+        spin_up();
+        for (int kind : {1, 2}) {
+            float bk = 1e30f;
+            const char* pk = "temporal";
+            for (const char* c : {"temporal", "tile"}) {
+                const float t = time_pass(kind, c, kdepth_);
+                if (t < bk) {
+                    bk = t;
+                    pk = c;
+                }
+            }
+            kern_[kind] = pk;
+        }
+    }
+    HIP_CHECK(hipEventDestroy(e0));
+    HIP_CHECK(hipEventDestroy(e1));
+    kernel_ = kern_[0];
+}
+
+}  // namespace hipeng
+}  // namespace gol

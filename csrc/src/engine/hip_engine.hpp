@@ -1,0 +1,502 @@
+// gol-mi355x: the HIP engine class (private to csrc/src/engine).
+//
+// One class, its member functions defined by topic:
+//   engine_hip.hip           construction, the run loop, board I/O, one-tile supersteps
+//   engine_hip_plan.hip      work plans, pass cuts, interior/boundary regions
+//   engine_hip_tune.hip      kernel autotune, schedule choice, pass-cost measurement
+//   engine_hip_subtiles.hip  two sub-tiles per rank on two streams
+//   engine_hip_graph.hip     hipGraph capture and replay of one-tile supersteps
+//   engine_hip_halo.hip      halo exchange (device transport or host staging)
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <functional>
+#include <chrono>
+#include <cstring>
+#include <map>
+#include <thread>
+
+#include "gol/bits.hpp"
+#include "gol/trace.hpp"
+#include "gol/engine.hpp"
+#include "gol/hip_kernels.hpp"
+
+#define HIP_CHECK(x)                                                                                    \
+    do {                                                                                                \
+        hipError_t e_ = (x);                                                                            \
+        if (e_ != hipSuccess)                                                                           \
+            throw ::gol::Error(::gol::strprintf("%s failed: %s (%s:%d)", #x, hipGetErrorString(e_), __FILE__, \
+                                                __LINE__));                                             \
+    } while (0)
+
+namespace gol {
+namespace hipeng {
+
+struct DevPlan {
+    LaneDesc* d = nullptr;
+    i64 waves = 0;
+    i64 rows = 0;  // rows per chunk
+    u32 tflags = 0;  // tile kernel: variant bits (LDS levels per pass, in place)
+    PlanStats st;
+};
+
+struct DevCopies {
+    hipk::CopyDesc* pack = nullptr;
+    hipk::CopyDesc* unpack = nullptr;
+    int npack = 0, nunpack = 0;
+    i64 max_pack = 0, max_unpack = 0;
+};
+
+class HipEngine : public Engine {
+   public:
+    HipEngine(const Geometry& g, const EngineConfig& c, std::shared_ptr<Transport> t);
+
+    // Host -> device copy ordered on the compute stream; returns when the data is in HBM.
+    void upload(void* dst, const void* src, size_t n) {
+        HIP_CHECK(hipMemcpyAsync(dst, src, n, hipMemcpyHostToDevice, s_comp_));
+        HIP_CHECK(hipStreamSynchronize(s_comp_));
+    }
+
+    // Every buffer-writing operation on the compute stream ends with this: the next superstep's
+    // waits (ready / interior / boundary) all see completed work.
+    void mark_ready() {
+        // Nothing waits on these when the compute stream is the only stream (no exchange, no
+        // split schedule): skip them — an event record between two kernels costs ~15 us on the
+        // GPU (a release fence), measured between eager supersteps on one MI355X.
+        if (!events_needed_) return;
+        HIP_CHECK(hipEventRecord(ev_ready_, s_comp_));
+    }
+
+    ~HipEngine() override;
+
+    std::string backend_name() const override { return "hip"; }
+
+    void synchronize() override {
+        if (wd_) {  // poll instead of blocking, so asynchronous transport errors surface
+            HIP_CHECK(hipEventRecord(ev_sync_comm_ ? ev_sync_comm_ : make_sync_events(), s_comm_));
+            HIP_CHECK(hipEventRecord(ev_sync_comp_, s_comp_));
+            wait_watched(ev_sync_comm_);
+            wait_watched(ev_sync_comp_);
+        }
+        HIP_CHECK(hipStreamSynchronize(s_comm_));
+        HIP_CHECK(hipStreamSynchronize(s_comp_));
+    }
+    hipEvent_t make_sync_events() {
+        HIP_CHECK(hipEventCreateWithFlags(&ev_sync_comm_, hipEventDisableTiming));
+        HIP_CHECK(hipEventCreateWithFlags(&ev_sync_comp_, hipEventDisableTiming));
+        return ev_sync_comm_;
+    }
+
+    std::vector<u64> tile_words() override;
+
+    void set_tile_words(const std::vector<u64>& dense) override;
+
+    std::pair<u64, u64> local_reduce() override {
+        sync_canonical();
+        HIP_CHECK(hipMemsetAsync(d_red_, 0, 2 * sizeof(u64), s_comp_));
+        hipk::launch_reduce_board(buf_[cur_], L_, g_.row0, g_.word0(), g_.global_words(), d_red_, s_comp_);
+        HIP_CHECK(hipGetLastError());
+        HIP_CHECK(hipMemcpyAsync(h_red_, d_red_, 2 * sizeof(u64), hipMemcpyDeviceToHost, s_comp_));
+        HIP_CHECK(hipStreamSynchronize(s_comp_));
+        return {h_red_[0], h_red_[1]};
+    }
+
+    bool graph_shape(int& k, int& m);
+
+    // Replay shapes {m supersteps of k, then one superstep of rem < k generations}, largest first:
+    // the run-length hint as ONE graph (its whole superstep count, at most 256, plus its remainder:
+    // the driver's 20-generation bench is a single replay), then M, 4 and 1 supersteps, then the
+    // hint's remainder alone.  Every graph boundary costs ~8.5 us of GPU idle (8192^2 x 1000 through
+    // the CLI: 5 boundaries, 3% of the run).
+    struct Shape {
+        int m, rem;
+    };
+    std::vector<Shape> graph_ladder(int k, int M) const;
+
+    // Buffer parity of the captured (one-tile) mode.
+    int par() const { return cur_; }
+    void set_par(int p) { cur_ = p; }
+
+    void prewarm_graph();
+
+    void run_graphed(u64& generations);
+
+    void replay(hipGraphExec_t exec, int k, int m, int rem);
+    // Buffer-parity flip of a shape (one flip per kernel pass).
+    int graph_flip(int k, int m, int rem) {
+        size_t n = pass_depths(k).size() * (size_t)m;
+        if (rem) n += pass_depths(rem).size();
+        return (int)(n & 1);
+    }
+
+    void run(u64 generations) override;
+
+    // ----- two sub-tiles per rank (1-D) -----
+    // The tile's rows are split into two halves, each with THREE buffers of R ghost rows, each
+    // running a superstep's passes on its own stream with a plan sized for the whole GPU.  The two
+    // kernels of a pass overlap: while one drains, the other's waves fill the freed SIMD slots (two
+    // half-board kernels on two streams: 9.8 vs 11.0 us/gen at 32768^2, docs/PERFORMANCE.md).
+    //   * A superstep's first pass reads the other half's edge rows (and the torus wrap) in place
+    //     (STEP_SEAM): no seam copy, no event between the copy and the first kernel.
+    //   * So that the other half can read them at any time during the superstep, a superstep never
+    //     writes the buffer it started from: its passes alternate between the other two buffers.
+    //   * Each stream waits only for the other half's end of the previous superstep (and, with
+    //     neighbours, the compute stream runs the rank's canonical RCCL messages first and the
+    //     second stream waits for them).
+    // Whether a rank runs one tile or two sub-tiles is decided by measurement at init
+    // (choose_schedule).
+    // Requested (GOL_SUBTILES=2) or auto-wanted: inputs identical on every rank (the mode is a
+    // candidate of the collective schedule timing): mode, layout, average strip height, halo depth,
+    // transport kind.
+    bool dual_wanted() const {
+        const bool want = cfg_.subtiles == 2 ||
+                          (cfg_.subtiles < 0 && g_.dec.H / std::max(1, g_.dec.Py) >= kSubtileMinRows && L_.R >= 64);
+        return want && !two_d() && !cfg_.compat && !cfg_.profile && !cfg_.force_split && !wd_ && L_.aligned() &&
+               (halo_items(L_.R).empty() || device_transport_) && cfg_.kernel != "lds" && cfg_.kernel != "tile";
+    }
+    // Rank-local conditions (agreed over the ranks by the caller): a tile tall enough for two
+    // halves, and memory for one more board pair.  (The halves always run the temporal kernel, at
+    // its own pass depth, whatever the one-tile kernel autotune picked.)
+    bool dual_local_ok() const {
+        if (L_.h < 8 * (i64)L_.R) return false;
+        size_t fr = 0, tot = 0;
+        if (hipMemGetInfo(&fr, &tot) != hipSuccess) return false;
+        return 3 * alloc_bytes_ + ((size_t)1 << 30) < fr;  // 3 buffers of half a tile per half
+    }
+
+    void setup_dual();
+    void teardown_dual();
+    // Plans and copy lists of a k-generation sub-tile superstep (built before any capture).
+    void prepare_dual(int k) {
+        const std::vector<int>& ps = pass_depths(k);
+        for (size_t j = 0; j < ps.size(); ++j)
+            for (int s = 0; s < 2; ++s) sub_plan(s, ps[j], ext_after(ps, j));
+    }
+    void destroy_dual_graphs() {
+        for (auto& kv : dual_graphs_) hipGraphExecDestroy(kv.second);
+        dual_graphs_.clear();
+    }
+
+    const DevPlan& sub_plan(int s, int k, i64 e);
+
+    u32 sub_flags() const { return step_flags() & ~hipk::STEP_WRAP_Y; }  // sub-tiles always have ghost rows
+
+    // rows [r0, r0 + n) of sub-tile s in its buffer `par` (0..2; full pitch, contiguous)
+    u64* sub_rows(int s, int par, i64 r0) { return sub_buf_[s][par] + sub_L_[s].index(r0, -1); }
+    size_t rows_bytes(int s, i64 n) const { return (size_t)(n * sub_L_[s].pitch) * 8; }
+
+    void dual_copy(u64* dst, const u64* src, size_t bytes) {
+        HIP_CHECK(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, s_comp_));
+    }
+
+    // Both halves done -> the canonical buffer (before anything reads it).
+    void sync_canonical() {
+        if (!canon_stale_) return;
+        HIP_CHECK(hipStreamWaitEvent(s_comp_, ev_sub_b_, 0));  // the second half's last superstep
+        for (int s = 0; s < 2; ++s)
+            dual_copy(buf_[cur_] + L_.index(sub_r0_[s], -1), sub_rows(s, sub_cur_, 0), rows_bytes(s, sub_L_[s].h));
+        canon_stale_ = false;
+    }
+
+    // Make `s` wait for `ev` unless it has completed already.  A cross-queue wait costs the waiting
+    // queue ~20 us even on a completed event (kernel trace of the driver's 20-generation bench: the
+    // second half's first kernel started 23 us after the first half's), and at the start of a run()
+    // that follows a synchronisation every event has completed.  (Never inside a graph capture: the
+    // sub-tile supersteps are not captured.)
+    void wait_pending(hipStream_t s, hipEvent_t ev) {
+        const hipError_t q = hipEventQuery(ev);
+        if (q == hipSuccess) return;
+        if (q != hipErrorNotReady) HIP_CHECK(q);
+        HIP_CHECK(hipStreamWaitEvent(s, ev, 0));
+    }
+
+    void dual_superstep(int k);
+
+    void launch_half(int s, int p, int k, hipStream_t st, int only = -1);
+
+    // Graph of launch_half(s, p, k): captured at init only (capture_dual_graphs), nullptr otherwise.
+    // Opt-in (GOL_SUBTILE_GRAPHS=1): replayed per half and superstep, these measured slower than the
+    // eager launches on MI355X / ROCm 7.2 (32768^2, same box, alternating: 20 generations 13.06-13.23
+    // vs 12.75-12.96 us/gen, 2000 generations 10.35 vs 10.24; profiles/subtile_graphs_ab.txt), as did
+    // one graph of both halves with fork/join events (see graph_shape).
+    bool dual_graphs_on() const { return cfg_.graph && !cfg_.profile && graph_ok_ && env_int("GOL_SUBTILE_GRAPHS", 0) != 0; }
+    hipGraphExec_t dual_graph(int s, int p, int k) {
+        if (!dual_graphs_on()) return nullptr;
+        auto it = dual_graphs_.find((s * 3 + p) * 1000 + k);
+        return it == dual_graphs_.end() ? nullptr : it->second;
+    }
+    void capture_dual_graphs(int k);
+
+    const DevPlan& full_plan_stats() {
+        const int R = superstep_depth();
+        return plan(0, pass_depths(R)[0], ext_after(pass_depths(R), 0));
+    }
+
+    // A one-tile rank without neighbours (nothing to exchange) cuts its supersteps at the largest
+    // multiple of the tuned pass depth within R, so none ends with a short pass (8192^2: tile passes
+    // of 24 in 32-generation supersteps ran 24 + 8, and an 8-generation tile pass is 27% slower per
+    // generation).  With neighbours every rank keeps R: the exchanges must match.
+    int superstep_depth() const override {
+        if (dual_ || !tuned_ || cfg_.compat || kdepth_ <= 0 || kdepth_ >= L_.R || !halo_items(L_.R).empty())
+            return L_.R;
+        return (L_.R / kdepth_) * kdepth_;
+    }
+
+   protected:
+    void do_init(const PatternSpec& p) override;
+
+    // Superstep depths prepared at init: the full superstep, and the hinted run's remainder.
+    std::vector<int> init_depths() const {
+        if (cfg_.compat) return {1};
+        const int R = superstep_depth();
+        std::vector<int> ks = {R};
+        for (u64 n : {cfg_.run_hint}) {
+            const int r = (int)(n % (u64)R);
+            if (r > 0 && std::find(ks.begin(), ks.end(), r) == ks.end()) ks.push_back(r);
+        }
+        return ks;
+    }
+
+    void do_superstep(int k) override {
+        if (dual_)
+            dual_superstep(k);
+        else
+            tile_superstep(k);
+    }
+
+    void tile_superstep(int k);
+
+    const std::vector<int>& pass_depths(int k);
+    // Generations still to run after pass j of a superstep (the "extension" of pass j's output:
+    // that many ghost rows when y has neighbours, plus the ghost words when x has neighbours).
+    i64 ext_after(const std::vector<int>& ps, size_t j) const {
+        i64 e = 0;
+        for (size_t i = j + 1; i < ps.size(); ++i) e += ps[i];
+        return e;
+    }
+    static int supported_kernel_depth(int want) {
+        while (want > 1 && !hipk::step_depth_supported(want)) --want;
+        return std::max(1, want);
+    }
+
+    void first_pass(int kx, int kp, i64 e, bool split);
+
+    void spin_up();
+
+    void measure_pass_costs();
+
+    // Pick the superstep schedule by measurement.  Candidates (every rank builds the same list from
+    // rank-invariant inputs, and agrees on the sub-tile mode's rank-local conditions by a reduction,
+    // because the timing is collective):
+    //   local / full  one tile; with neighbours the exchange runs on the compute stream, then one
+    //                 full-region kernel pass (plus the later passes)
+    //   split         one tile; the exchange on the comm stream overlaps the interior kernel, then the
+    //                 boundary bands (needs an interior on every rank)
+    //   subtiles      two half-tiles on two streams (1-D; dual_superstep)
+    // Each candidate runs whole R-generation supersteps on scratch state (one tile: every pass reads
+    // the board and writes the scratch buffer, the exchange writes the ghost rows a real superstep
+    // writes; sub-tiles: their own buffers, loaded from the board at the next run), timed in three
+    // interleaved rounds, best round per candidate, max over ranks.  The smallest time per
+    // generation wins.
+    static constexpr int kSchedReps = 4;
+    void choose_schedule();
+
+    void time_schedule(const std::string& c, int k, int reps);
+
+    void do_set_compat_halos(const std::vector<u64>& above, const std::vector<u64>& below) override;
+
+    std::vector<u64> read_row(i64 r) override {
+        sync_canonical();
+        synchronize();
+        std::vector<u64> row((size_t)L_.pitch);
+        HIP_CHECK(hipMemcpyAsync(row.data(), buf_[cur_] + L_.index(r, -1), (size_t)L_.pitch * 8, hipMemcpyDeviceToHost,
+                                 s_comp_));
+        HIP_CHECK(hipStreamSynchronize(s_comp_));
+        return row;
+    }
+
+    int supported_depth(int want) const override {
+        // Depends on the CONFIGURED kernel only: every rank must cut the same supersteps (the halo
+        // exchange sizes follow k), even when GOL_KERNEL=auto resolves differently per rank.
+        if (cfg_.kernel == "lds") return 1;
+        if (cfg_.kernel == "tile" || multipass_) return std::max(1, want);  // any depth: passes
+        return supported_kernel_depth(want);
+    }
+
+   private:
+    // ----- plans -----
+    u32 step_flags() const {
+        u32 f = 0;
+        if (self_y() && !cfg_.compat) f |= hipk::STEP_WRAP_Y;
+        if (xwrap_by_plan()) f |= hipk::STEP_WRAP_X;
+        return f;
+    }
+    // Tile-kernel variant bits of a plan (tile_plan_flags).  Generations per LDS pass (GOL_TILE_LEVELS
+    // 1, 2 or 4): auto 4 for a double-buffered tile of <= 8 waves, else 2 (kbench, 8 waves: 4 levels
+    // 0.4-2% faster double-buffered, 1-2% slower in place; 16 waves: 3-7% slower;
+    // profiles/tile_levels_ab.txt, profiles/tile_inplace_ab.txt).
+    u32 tile_bits(bool inplace) const {
+        const int lv = tile_lv_ > 0 ? tile_lv_ : (!inplace && cfg_.tile_waves <= 8 ? 4 : 2);
+        return (lv == 2 ? hipk::STEP_TILE_L2 : 0u) | (lv == 4 ? hipk::STEP_TILE_L4 : 0u) |
+               (inplace ? hipk::STEP_TILE_INPLACE : 0u);
+    }
+    // Most rows a tile may hold at depth k (the in-place variant's capacity unless GOL_TILE_INPLACE=0).
+    i64 tile_rows_cap(int k) const {
+        return hipk::tile_max_rows(k, cfg_.tile_waves, step_flags() | tile_bits(tile_inplace_ != 0));
+    }
+
+    bool tile_kernel(int kind) const { return kern_[kind] == "tile"; }
+
+    // Rounds of one-tile-per-CU the LDS tile kernel needs for a plan (cheap estimate, no plan).
+    // Plans are explicit (one descriptor row per tile), so huge boards are left to step_temporal.
+    static constexpr i64 kMaxTileRounds = 16;
+    i64 tile_rounds(int kind, int k, i64 e) const {
+        const i64 rmax = std::max<i64>(1, tile_rows_cap(k));
+        i64 tiles = 0;
+        for (const Region& r : regions(kind, k, e))
+            tiles += ceil_div(r.r1 - r.r0, rmax) * ceil_div(r.c1 - r.c0, (i64)kSegWords);
+        return ceil_div(tiles, (i64)cus_);
+    }
+
+    // Whether supersteps use the interior (kind 1) / boundary (kind 2) split.
+    bool split_used() const {
+        return !cfg_.compat && cfg_.overlap && can_overlap() && (!halo_items(L_.R).empty() || cfg_.force_split);
+    }
+
+    void autotune_kernel();
+
+    bool can_overlap() const {
+        // an interior must exist on EVERY rank (the schedule timing is collective, so the decision
+        // uses the smallest strip, not this rank's), and the LDS kernel reads ghost words for every
+        // row (2-D needs them)
+        if (min_tile_rows() <= 2 * (i64)L_.R) return false;
+        if (kernel_ == "lds" && two_d()) return false;
+        return true;
+    }
+
+    std::vector<Region> regions(int kind, int k, i64 rem = 0) const;
+
+    const DevPlan& plan(int kind, int k, i64 e = 0);
+
+    void launch(int kind, int k, i64 e, const u64* src, u64* dst, hipStream_t s);
+
+    // Ghost words for widths that are not a multiple of 64 when the tile is its own E/W neighbour.
+    void post(u64* buf, hipStream_t s, i64 rem = 0) {
+        const i64 e = self_y() ? 0 : rem;
+        if (self_x() && !L_.aligned()) hipk::launch_fill_ghost_cols(buf, L_, -e, L_.h + e, s);
+    }
+
+    // ----- halo exchange -----
+    const std::vector<HaloItem>& items_for(int k) {
+        auto it = items_.find(k);
+        if (it != items_.end()) return it->second;
+        return items_.emplace(k, halo_items(k)).first->second;
+    }
+
+    void prepare(int k);
+
+    const DevCopies& copies(int k, int parity);
+
+    void build_messages(int k, const std::vector<HaloItem>& items, int parity, std::vector<Message>& sends,
+                        std::vector<Message>& recvs);
+
+    void exchange_device(int k, const std::vector<HaloItem>& items, int parity, hipStream_t s);
+
+    void exchange_staged(int k, const std::vector<HaloItem>& items, int parity, hipStream_t s);
+
+    void account(const std::vector<HaloItem>& items) {
+        stats_.exchanges += 1;
+        for (const HaloItem& it : items) stats_.halo_bytes += (u64)it.send.count() * 8;
+    }
+
+    void record_profile(bool with_exchange);
+
+    // ----- graphs -----
+    // The captured kernels bake in the buffer pointers, so a replay must start at the parity it was
+    // captured at (an odd-pass remainder superstep flips it between run() calls).
+    i64 graph_key(int k, int m, int rem) const { return (((i64)k * 1000 + m) * 1000 + rem) * 2 + par(); }
+    hipGraphExec_t graph_for(int k, int m, int rem);
+
+    // ----- watchdog support -----
+    // Wait for `ev` without blocking in the driver, so a stuck or failed exchange is noticed: the
+    // transport's asynchronous error state is polled while waiting.
+    void wait_watched(hipEvent_t ev) {
+        for (;;) {
+            const hipError_t e = hipEventQuery(ev);
+            if (e == hipSuccess) return;
+            if (e != hipErrorNotReady) HIP_CHECK(e);
+            const std::string ae = t_->async_error();
+            if (!ae.empty()) fatal(ae, 5);
+            std::this_thread::sleep_for(std::chrono::microseconds(50));
+        }
+    }
+    // Bounded lookahead: the host runs at most kFenceDepth units (supersteps or graph launches)
+    // ahead of the GPU, so watchdog kicks track completed GPU work.
+    static constexpr int kFenceDepth = 4;
+    void fence() override {
+        if (!fence_ev_[0])
+            for (auto& e : fence_ev_) HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        HIP_CHECK(hipEventRecord(fence_ev_[fence_i_], s_comp_));
+        fence_used_[fence_i_] = true;
+        fence_i_ = (fence_i_ + 1) % kFenceDepth;
+        if (fence_used_[fence_i_]) wait_watched(fence_ev_[fence_i_]);
+    }
+
+    int dev_ = 0, cus_ = 256;
+    std::string kernel_;  // resolved kernel: temporal | tile | lds (auto resolves at init)
+    std::string kern_[3];  // per plan kind (full / interior / boundary), resolved by autotune
+    int kdepth_ = 8;       // kernel pass depth K (<= halo depth R)
+    int tdepth_ = 8;       // temporal-kernel pass depth (the sub-tile mode's, whatever kernel one tile uses)
+    // temporal-kernel plans: waves per SIMD the one-round plan is sized for (0: the kernel's full
+    // occupancy).  Small tiles pay (K+1)/S of vertical halo with S rows per wave, so fewer, taller
+    // waves can win there; the autotuner tries 2 per SIMD against the full occupancy (3 at K=8).
+    int occ_ = 0;
+    // tile kernel: one LDS buffer updated in place (1), double-buffered (0), or per plan (-1, auto)
+    int tile_inplace_ = (int)env_int("GOL_TILE_INPLACE", -1);
+    int tile_lv_ = (int)env_int("GOL_TILE_LEVELS", 0);  // tile kernel: generations per LDS pass (1, 2, 4; 0 auto)
+    bool multipass_ = false;
+    std::map<int, std::vector<int>> passes_;
+    bool split_ = false;   // superstep schedule: interior/boundary split with overlapped exchange
+    std::map<std::string, double> sched_us_;  // choose_schedule: us per generation per candidate
+    std::map<int, double> pass_us_;           // measure_pass_costs: us per pass by depth (chosen mode)
+    bool tuned_ = false;
+    std::map<std::string, float> tune_ms_;
+    hipEvent_t fence_ev_[kFenceDepth] = {};
+    hipEvent_t ev_sync_comm_ = nullptr, ev_sync_comp_ = nullptr;
+    bool fence_used_[kFenceDepth] = {};
+    int fence_i_ = 0;
+    u64* buf_[2] = {nullptr, nullptr};
+    size_t alloc_bytes_ = 0;
+    int cur_ = 0;
+    hipStream_t s_comp_ = nullptr, s_comm_ = nullptr;
+    hipEvent_t ev_ready_ = nullptr, ev_halo_ = nullptr;
+    hipEvent_t ev_t0_ = nullptr, ev_t1_ = nullptr, ev_t2_ = nullptr, ev_t3_ = nullptr;
+    u64* d_red_ = nullptr;
+    u64* h_red_ = nullptr;
+    bool device_transport_ = false;
+    bool graph_ok_ = true;
+    bool events_needed_ = true;  // another stream waits on ev_ready_
+    std::vector<void*> deferred_free_;
+    std::map<i64, DevPlan> plans_;
+    // GOL_SUBTILES=2 state
+    bool dual_ = false;
+    Layout sub_L_[2];
+    i64 sub_r0_[2] = {0, 0};
+    u64* sub_buf_[2][3] = {{nullptr, nullptr, nullptr}, {nullptr, nullptr, nullptr}};
+    int sub_cur_ = 0;  // buffer (0..2) holding both halves' current generation
+    bool sub_current_ = false;  // the halves hold the current board
+    bool canon_stale_ = false;  // buf_[cur_] lags the halves (sync_canonical before reading it)
+    std::map<int, DevPlan> sub_plans_;
+    std::map<int, hipGraphExec_t> dual_graphs_;  // (half, start buffer, depth) -> launch_half graph
+    hipEvent_t ev_sub_a_ = nullptr, ev_sub_b_ = nullptr;  // half 0 / half 1 done with its last superstep
+    hipEvent_t ev_sub_x_ = nullptr;                        // the rank's exchange (into both halves) done
+    std::map<int, DevCopies> copies_;
+    std::map<int, std::vector<HaloItem>> items_;
+    std::map<i64, hipGraphExec_t> graphs_;
+    std::vector<u64*> dstage_s_, dstage_r_, hstage_s_, hstage_r_;
+};
+
+}  // namespace hipeng
+}  // namespace gol
