@@ -58,6 +58,10 @@ struct EngineConfig {
     u64 run_hint = 0;                 // generations of the runs to come (CLI: iterations); the HIP
                                       // engine captures one graph covering them (<= 256 supersteps)
     bool graph_rccl = false;          // also capture supersteps whose exchange is an RCCL group
+    int subtile_overlap = 0;          // sub-tiles with neighbours: half 0 starts its first pass (all but
+                                      // its band next to the rank's north halo) while the exchange is in
+                                      // flight (GOL_SUBTILE_OVERLAP: 1 on, 0 off (default: measured slower
+                                      // through RCCL self-exchange), -1 = a candidate of the init timing)
     int sub_occ = 2;                  // sub-tile plans: waves per SIMD each half is sized for (GOL_SUB_OCC;
                                       // 0 = the single-tile tuned occupancy)
     bool self_exchange = false;       // GOL_SELF_EXCHANGE: directions whose neighbour is this rank go

@@ -103,6 +103,9 @@ class ThreadTransport : public Transport {
     int rank_;
 };
 std::shared_ptr<ThreadGroup> make_thread_group(int nranks);
+// Exit code of the rank that aborted the group (0 while none has): the other ranks, woken by the
+// abort, exit with the same code, so the process status does not depend on which thread exits first.
+int thread_group_abort_code(ThreadGroup& g);
 
 // RCCL-semantics data plane for thread-mode ranks sharing one GPU (device buffers, stream-ordered
 // rendezvous copies, per-peer FIFO matching): exercises the device-transport engine paths without

@@ -255,6 +255,7 @@ PYBIND11_MODULE(_gol, m) {
         .def_readwrite("tile_waves", &EngineConfig::tile_waves)
         .def_readwrite("tune_tile_waves", &EngineConfig::tune_tile_waves)
         .def_readwrite("sub_occ", &EngineConfig::sub_occ)
+        .def_readwrite("subtile_overlap", &EngineConfig::subtile_overlap)
         .def_readwrite("self_exchange", &EngineConfig::self_exchange)
         .def_readwrite("force_split", &EngineConfig::force_split)
         .def_readwrite("sched", &EngineConfig::sched)

@@ -134,7 +134,7 @@ class ThreadGroup {
         std::unique_lock<std::mutex> lk(mu_);
         auto& q = boxes_[(size_t)dst * n_ + src];
         cv_.wait(lk, [&] { return !q.empty() || aborted_; });
-        if (aborted_ && q.empty()) throw Error("thread group aborted");
+        if (aborted_ && q.empty()) throw Error(strprintf("thread group aborted (exit code %d)", code_));
         std::vector<u8> m = std::move(q.front());
         q.pop_front();
         lk.unlock();
@@ -143,12 +143,17 @@ class ThreadGroup {
                                   m.size(), len));
         if (len) memcpy(buf, m.data(), len);
     }
-    void abort() {
+    void abort(int code) {
         {
             std::lock_guard<std::mutex> lk(mu_);
+            if (!aborted_) code_ = code;
             aborted_ = true;
         }
         cv_.notify_all();
+    }
+    int abort_code() {
+        std::lock_guard<std::mutex> lk(mu_);
+        return aborted_ ? code_ : 0;
     }
 
    private:
@@ -157,7 +162,10 @@ class ThreadGroup {
     std::condition_variable cv_;
     std::vector<std::deque<std::vector<u8>>> boxes_;
     bool aborted_ = false;
+    int code_ = 0;  // exit code of the first rank that aborted the group
 };
+
+int thread_group_abort_code(ThreadGroup& g) { return g.abort_code(); }
 
 std::shared_ptr<ThreadGroup> make_thread_group(int nranks) {
     if (nranks < 1) throw Error("thread group needs >= 1 rank");
@@ -169,7 +177,7 @@ int ThreadTransport::size() const { return g_->size(); }
 void ThreadTransport::send_bytes(int peer, const void* buf, size_t n) { g_->push(rank_, peer, buf, n); }
 void ThreadTransport::recv_bytes(int peer, void* buf, size_t n) { g_->pop(peer, rank_, buf, n); }
 void ThreadTransport::abort(int code) {
-    g_->abort();
+    g_->abort(code);
     Transport::abort(code);
 }
 

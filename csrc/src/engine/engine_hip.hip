@@ -234,7 +234,7 @@ void HipEngine::do_init(const PatternSpec& p) {
     }
     stats_.kernel = split_ ? kern_[1] + "+boundary:" + kern_[2] : kern_[0];
     stats_.schedule = split_ ? "split" : (halo_items(L_.R).empty() ? "local" : "full");
-    if (dual_) stats_.schedule += "+subtiles2";
+    if (dual_) stats_.schedule += sub_overlap_ ? "+subtiles2ov" : "+subtiles2";
     stats_.kernel_depth = kdepth_;
     stats_.tile_waves = cfg_.tile_waves;
     std::string tn;

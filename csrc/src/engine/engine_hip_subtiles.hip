@@ -37,16 +37,20 @@ void HipEngine::teardown_dual() {
             if (b) hipFree(b);
             b = nullptr;
         }
-    dual_ = false;
+    dual_ = sub_overlap_ = false;
     sub_current_ = canon_stale_ = false;
 }
 
-const DevPlan& HipEngine::sub_plan(int s, int k, i64 e) {
-    const int key = (s * 100000 + (int)e * 100 + k);
+const DevPlan& HipEngine::sub_plan(int s, int k, i64 e, int part) {
+    const int key = part * 1000000 + s * 100000 + (int)e * 100 + k;
     auto it = sub_plans_.find(key);
     if (it != sub_plans_.end()) return it->second;
     const Layout& L = sub_L_[s];
+    // output rows -e .. h+e; for half 0, part 1 starts k rows below the tile's top (its inputs never
+    // reach the north ghost rows the exchange writes) and part 2 is the band above that
     std::vector<Region> rg = {{-e, L.h + e, 0, L.nw}};
+    if (part == 1) rg[0].r0 = k;
+    if (part == 2) rg[0].r1 = k;
     i64 bpc = hipk::step_blocks_per_cu(k, sub_flags());
     // waves/SIMD each half's plan is sized for: two concurrent halves fill the SIMDs between
     // them, so 2-wave plans (taller segments, less halo) measured best (kbench: 9.85 vs 10.11
@@ -78,18 +82,36 @@ void HipEngine::dual_superstep(int k) {
     const int a = (p + 1) % 3, b = (p + 2) % 3;  // the passes alternate a, b, a, ... (never p)
     const i64 h1 = sub_L_[1].h;
     wait_pending(s_comp_, ev_sub_b_);  // half 1's previous superstep is done
+    hipGraphExec_t gx[2] = {dual_graph(0, p, k), dual_graph(1, p, k)};
+    const bool graphs = gx[0] && gx[1];
+    // With neighbours, half 0's first pass can start before the exchange: all its output rows but
+    // the k next to the north halo read only rows the halves already hold (its own, and half 1's
+    // edge across the seam); that band runs after the exchange.  The exchange then goes on the
+    // second stream, the one of greatest priority, so the RCCL kernel is dispatched ahead of the
+    // half-tile kernel when both become ready (a kernel that has filled the CUs first would hold
+    // it back).  Chosen by measurement (schedule "subtiles+ov"): it costs a second, small kernel
+    // per superstep.
+    const bool ov = sub_overlap_ && !self_y() && !graphs;
     if (!self_y()) {
+        hipStream_t xs = s_comp_;
+        if (ov) {
+            launch_half(0, p, k, s_comp_, 0, 1);
+            wait_pending(s_comm_, ev_sub_a_);  // the exchange sends half 0's edge and writes its halo
+            xs = s_comm_;
+        }
         // the one-tile engine's canonical messages (Engine::halo_items, 1-D): N then S
         std::vector<Message> sends, recvs;
         sends.push_back({g_.nbr[DIR_N], sub_rows(0, p, 0), rows_bytes(0, k)});
         recvs.push_back({g_.nbr[DIR_S], sub_rows(1, p, h1), rows_bytes(1, k)});
         sends.push_back({g_.nbr[DIR_S], sub_rows(1, p, h1 - k), rows_bytes(1, k)});
         recvs.push_back({g_.nbr[DIR_N], sub_rows(0, p, -k), rows_bytes(0, k)});
-        t_->exchange(sends, recvs, (void*)s_comp_);
+        t_->exchange(sends, recvs, (void*)xs);
         stats_.exchanges += 1;
         stats_.halo_bytes += (u64)(rows_bytes(0, k) + rows_bytes(1, k));
-        HIP_CHECK(hipEventRecord(ev_sub_x_, s_comp_));  // also implies half 0's previous superstep
-        HIP_CHECK(hipStreamWaitEvent(s_comm_, ev_sub_x_, 0));
+        // (full: also implies half 0's previous superstep, which ran on the same stream)
+        HIP_CHECK(hipEventRecord(ev_sub_x_, xs));
+        HIP_CHECK(hipStreamWaitEvent(ov ? s_comp_ : s_comm_, ev_sub_x_, 0));
+        if (ov) launch_half(0, p, k, s_comp_, 0, 2);
     } else {
         wait_pending(s_comm_, ev_sub_a_);  // half 0's previous superstep is done
     }
@@ -99,14 +121,14 @@ void HipEngine::dual_superstep(int k) {
     // half's lone tail; kernel traces of the driver's 20-generation bench), or
     // (GOL_SUBTILE_GRAPHS=1) one replay per half of a graph captured at init per half, start
     // buffer and depth.  The cross-half order stays in the events around them.
-    hipGraphExec_t gx[2] = {dual_graph(0, p, k), dual_graph(1, p, k)};
-    if (gx[0] && gx[1]) {
+    if (graphs) {
         for (int s = 0; s < 2; ++s) HIP_CHECK(hipGraphLaunch(gx[s], s ? s_comm_ : s_comp_));
         stats_.graph_launches += 2;
     } else {
         const int np = (int)pass_depths(k).size();
         for (int j = 0; j < np; ++j)
-            for (int s = 0; s < 2; ++s) launch_half(s, p, k, s ? s_comm_ : s_comp_, j);
+            for (int s = 0; s < 2; ++s)
+                if (!(ov && s == 0 && j == 0)) launch_half(s, p, k, s ? s_comm_ : s_comp_, j);
     }
     HIP_CHECK(hipEventRecord(ev_sub_a_, s_comp_));
     HIP_CHECK(hipEventRecord(ev_sub_b_, s_comm_));
@@ -115,8 +137,8 @@ void HipEngine::dual_superstep(int k) {
 }
 
 // The kernel passes of half s in a superstep of k generations that starts from buffer p (only
-// pass `only` when >= 0).
-void HipEngine::launch_half(int s, int p, int k, hipStream_t st, int only) {
+// pass `only` when >= 0; `part` selects a sub_plan part for the first pass).
+void HipEngine::launch_half(int s, int p, int k, hipStream_t st, int only, int part) {
     const std::vector<int>& ps = pass_depths(k);
     const int a = (p + 1) % 3, b = (p + 2) % 3;  // the passes alternate a, b, a, ... (never p)
     const Layout& Ls = sub_L_[s];
@@ -134,7 +156,7 @@ void HipEngine::launch_half(int s, int p, int k, hipStream_t st, int only) {
     for (size_t j = 0; j < ps.size(); ++j) {
         const int dsti = (j % 2 == 0) ? a : b;
         if (only < 0 || (int)j == only) {
-            const DevPlan& pl = sub_plan(s, ps[j], ext_after(ps, j));
+            const DevPlan& pl = sub_plan(s, ps[j], ext_after(ps, j), j == 0 ? part : 0);
             hipk::launch_step(ps[j], sub_buf_[s][q], sub_buf_[s][dsti], pl.d, pl.waves, j == 0 ? sp0 : sp, st);
         }
         q = dsti;

@@ -103,10 +103,12 @@ void HipEngine::choose_schedule() {
         dual_ok = ok > 0;
     }
     if (dual_ok) {
-        if (cfg_.subtiles == 2)
-            cands = {"subtiles"};
-        else
-            cands.push_back("subtiles");
+        // the overlapped variant needs the exchange (neighbours, or the self-exchange)
+        std::vector<std::string> dc;
+        if (cfg_.subtile_overlap <= 0 || self_y()) dc.push_back("subtiles");
+        if (cfg_.subtile_overlap != 0 && !self_y()) dc.push_back("subtiles+ov");
+        if (cfg_.subtiles == 2) cands.clear();
+        cands.insert(cands.end(), dc.begin(), dc.end());
     }
     std::string pick = cands[0];
     if (cands.size() > 1) {
@@ -134,7 +136,8 @@ void HipEngine::choose_schedule() {
         stats_.halo_bytes = 0;
     }
     split_ = pick == "split";
-    dual_ = pick == "subtiles";
+    dual_ = pick.rfind("subtiles", 0) == 0;
+    sub_overlap_ = pick == "subtiles+ov";
     if (dual_) {
         setup_dual();
         sub_current_ = false;  // the halves hold timing scratch: load the board at the next run
@@ -146,11 +149,12 @@ void HipEngine::choose_schedule() {
 
 // `reps` supersteps of k generations of schedule `c` on scratch state (see choose_schedule).
 void HipEngine::time_schedule(const std::string& c, int k, int reps) {
-    if (c == "subtiles") {
+    if (c.rfind("subtiles", 0) == 0) {
         setup_dual();
         dual_ = true;
+        sub_overlap_ = c == "subtiles+ov";
         for (int i = 0; i < reps; ++i) dual_superstep(k);
-        dual_ = false;
+        dual_ = sub_overlap_ = false;
         return;
     }
     split_ = c == "split";

@@ -173,13 +173,17 @@ class HipEngine : public Engine {
         const std::vector<int>& ps = pass_depths(k);
         for (size_t j = 0; j < ps.size(); ++j)
             for (int s = 0; s < 2; ++s) sub_plan(s, ps[j], ext_after(ps, j));
+        if (sub_overlap_ && !self_y())
+            for (int part : {1, 2}) sub_plan(0, ps[0], ext_after(ps, 0), part);
     }
     void destroy_dual_graphs() {
         for (auto& kv : dual_graphs_) hipGraphExecDestroy(kv.second);
         dual_graphs_.clear();
     }
 
-    const DevPlan& sub_plan(int s, int k, i64 e);
+    // part: 0 the whole pass; a first pass of half 0 split around the exchange (sub_overlap_):
+    // 1 all output rows but the band next to the north halo, 2 that band
+    const DevPlan& sub_plan(int s, int k, i64 e, int part = 0);
 
     u32 sub_flags() const { return step_flags() & ~hipk::STEP_WRAP_Y; }  // sub-tiles always have ghost rows
 
@@ -214,7 +218,7 @@ class HipEngine : public Engine {
 
     void dual_superstep(int k);
 
-    void launch_half(int s, int p, int k, hipStream_t st, int only = -1);
+    void launch_half(int s, int p, int k, hipStream_t st, int only = -1, int part = 0);
 
     // Graph of launch_half(s, p, k): captured at init only (capture_dual_graphs), nullptr otherwise.
     // Opt-in (GOL_SUBTILE_GRAPHS=1): replayed per half and superstep, these measured slower than the
@@ -482,6 +486,7 @@ class HipEngine : public Engine {
     std::map<i64, DevPlan> plans_;
     // GOL_SUBTILES=2 state
     bool dual_ = false;
+    bool sub_overlap_ = false;  // half 0's first pass overlaps the exchange (timed candidate "subtiles+ov")
     Layout sub_L_[2];
     i64 sub_r0_[2] = {0, 0};
     u64* sub_buf_[2][3] = {{nullptr, nullptr, nullptr}, {nullptr, nullptr, nullptr}};

@@ -173,6 +173,7 @@ EngineConfig engine_config(const Options& o, const std::string& backend, int dev
     c.subtiles = env_str("GOL_SUBTILES", "auto") == "auto" ? -1 : (int)env_int("GOL_SUBTILES", 0);
     c.watchdog_s = o.watchdog_s;
     c.sub_occ = (int)env_int("GOL_SUB_OCC", 2);
+    c.subtile_overlap = env_str("GOL_SUBTILE_OVERLAP", "0") == "auto" ? -1 : (int)env_int("GOL_SUBTILE_OVERLAP", 0);
     c.self_exchange = env_int("GOL_SELF_EXCHANGE", 0) != 0;
     c.force_split = env_int("GOL_FORCE_SPLIT", 0) != 0;
     c.graph_rccl = env_int("GOL_GRAPH_RCCL", 0) != 0;
@@ -518,7 +519,8 @@ int run_cli(int argc, char** argv) {
                     } catch (const std::exception& e) {
                         fprintf(stderr, "[gol] rank %d: %s\n", r, e.what());
                         fflush(stderr);
-                        _exit(1);
+                        const int code = thread_group_abort_code(*group);
+                        _exit(code ? code : 1);
                     }
                 });
             }

@@ -96,6 +96,9 @@ class Simulation:
         self_exchange: bool = os.environ.get("GOL_SELF_EXCHANGE", "0") == "1",
         subtiles: int = -1 if os.environ.get("GOL_SUBTILES", "auto") == "auto" else int(os.environ["GOL_SUBTILES"]),
         width: int = 0,
+        subtile_overlap: int = (
+            -1 if os.environ.get("GOL_SUBTILE_OVERLAP", "0") == "auto" else int(os.environ.get("GOL_SUBTILE_OVERLAP", "0"))
+        ),
     ):
         self.transport = transport if transport is not None else _gol.SelfTransport()
         P, rank = self.transport.size(), self.transport.rank()
@@ -119,6 +122,7 @@ class Simulation:
         cfg.tile_waves = int(tile_waves)
         cfg.tune_tile_waves = "GOL_TILE_WAVES" not in os.environ
         cfg.sub_occ = int(sub_occ)
+        cfg.subtile_overlap = int(subtile_overlap)  # 1 / 0 / -1 timed: half 0 overlaps the exchange
         cfg.self_exchange = bool(self_exchange)
         cfg.force_split = bool(force_split)
         cfg.sched = schedule
