@@ -36,9 +36,13 @@ void HipEngine::spin_up() {
 void HipEngine::measure_pass_costs() {
     pass_us_.clear();
     if (cfg_.compat || cfg_.kernel_depth > 0 || kernel_ == "lds" || (!dual_ && tile_kernel(0))) return;
+    // every instantiated depth up to the pass depth, and the deeper ones a superstep could use: a
+    // 20-generation superstep cut 12 + 8 measured cheaper than 8 + 8 + 4 (the K=12 pass runs 2 waves
+    // per SIMD at ~10.6 us/gen as two halves, vs 10.3 at K=8; profiles/pingpong_loop_ab.txt)
     const int K = dual_ ? tdepth_ : kdepth_;
+    const int kmax = std::min(superstep_depth(), hipk::max_step_depth());
     std::vector<int> ds;
-    for (int d = 1; d <= K; ++d)
+    for (int d = 1; d <= std::max(K, kmax); ++d)
         if (hipk::step_depth_supported(d)) ds.push_back(d);
     if (ds.size() < 2) return;
     for (int d : ds) {  // every plan first: plan building idles the GPU and drops its clock

@@ -129,6 +129,17 @@ template <int K>
 constexpr int prefetch_rows() {
     return (GOL_SHALLOW_PF && K <= 4) ? 6 : 3;
 }
+// Deep passes whose one-triple steady loop the compiler schedules with a wait on the fresh prefetch
+// (see WaveRunner::run) use the two-triple loop: K = 6, 7 and 12.  Measured at 32768^2, two halves
+// (profiles/pingpong_loop_ab.txt): K=7 12.2 -> 10.9 us/gen, K=12 12.8 -> 10.6, K=6 12.0 -> 11.8;
+// K=5 and 8 do not gain.  GOL_PINGPONG_MASK (bit K) overrides the set at build time.
+#ifndef GOL_PINGPONG_MASK
+#define GOL_PINGPONG_MASK ((1 << 6) | (1 << 7) | (1 << 12))
+#endif
+template <int K>
+constexpr bool pingpong_loop() {
+    return K < 32 && ((GOL_PINGPONG_MASK >> K) & 1) != 0;
+}
 
 template <int K, int ROWS>
 struct WaveRunner {
@@ -250,6 +261,36 @@ struct WaveRunner {
             if (i + 3 < n) compute_store<0, false>(pf[3].x, pf[3].y, i + 3);
             if (i + 4 < n) compute_store<1, false>(pf[4].x, pf[4].y, i + 4);
         } else {
+            if constexpr (pingpong_loop<K>()) {
+                // Two register triples in turn (rows i..i+2 in pf, i+3..i+5 in q): each is refilled
+                // right after its rows were computed, so no prefetched register is ever copied.  (With
+                // the one-triple loop below the compiler copies the new pf[2] into the register of the
+                // old one at some depths, right after its last use: that copy waits for the load just
+                // issued, s_waitcnt vmcnt(0), and the prefetch is lost.)
+                uint2 q[3];
+                for (; i + 6 <= n; i += 6) {
+                    q[0] = *ld;
+                    next_row();
+                    q[1] = *ld;
+                    next_row();
+                    q[2] = *ld;
+                    next_row();
+                    __builtin_amdgcn_sched_barrier(0);
+                    compute_store<0, false>(pf[0].x, pf[0].y, i);
+                    compute_store<1, false>(pf[1].x, pf[1].y, i + 1);
+                    compute_store<2, false>(pf[2].x, pf[2].y, i + 2);
+                    pf[0] = *ld;
+                    next_row();
+                    pf[1] = *ld;
+                    next_row();
+                    pf[2] = *ld;
+                    next_row();
+                    __builtin_amdgcn_sched_barrier(0);
+                    compute_store<0, false>(q[0].x, q[0].y, i + 3);
+                    compute_store<1, false>(q[1].x, q[1].y, i + 4);
+                    compute_store<2, false>(q[2].x, q[2].y, i + 5);
+                }
+            }
             for (; i + 3 <= n; i += 3) {
                 // hoist the whole next triple's loads above this triple's compute
                 const uint2 x0 = pf[0], x1 = pf[1], x2 = pf[2];

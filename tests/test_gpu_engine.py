@@ -225,6 +225,19 @@ def test_naive_yardstick(gol):
     assert pop == int(numpy_step(random_board(256, 256, 0x5EED), 10).sum())
 
 
+@pytest.mark.parametrize("depth", [6, 7, 12])
+def test_pingpong_loop_depths(gol, depth):
+    """Depths that run the two-triple steady loop (K = 6, 7, 12), with tall segments (300 rows) so the
+    loop runs many six-row iterations plus its leftover triple and tail rows, on the torus and with
+    ghost rows (two passes per superstep)."""
+    N = 2048
+    for R, gens in ((depth, 3 * depth + 1), (2 * depth, 2 * depth + 5)):
+        s = _sim(gol, N, halo_depth=R, kernel_depth=depth, kernel="temporal", rows_per_wave=300, subtiles=0)
+        s.init(5, seed=depth + R)
+        s.step(gens)
+        assert np.array_equal(s.board(), numpy_step(initial_board(5, N, 1, True, depth + R), gens)), (depth, R)
+
+
 @pytest.mark.parametrize("depth", [1, 3, 5, 7, 8, 16])
 def test_kernel_depth_passes(gol, depth):
     """Every instantiated temporal depth as the pass depth, with multi-pass supersteps of 2*depth+1
