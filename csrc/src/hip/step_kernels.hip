@@ -136,9 +136,13 @@ constexpr int prefetch_rows() {
 #ifndef GOL_PINGPONG_MASK
 #define GOL_PINGPONG_MASK ((1 << 6) | (1 << 7) | (1 << 12))
 #endif
-template <int K>
+// ... and, for the ghost-row variant only (the sub-tile passes after the first), K = 5
+#ifndef GOL_PINGPONG_GHOST_MASK
+#define GOL_PINGPONG_GHOST_MASK (1 << 5)
+#endif
+template <int K, int ROWS>
 constexpr bool pingpong_loop() {
-    return K < 32 && ((GOL_PINGPONG_MASK >> K) & 1) != 0;
+    return K < 32 && (((GOL_PINGPONG_MASK >> K) & 1) != 0 || (ROWS == 0 && ((GOL_PINGPONG_GHOST_MASK >> K) & 1) != 0));
 }
 
 template <int K, int ROWS>
@@ -261,7 +265,7 @@ struct WaveRunner {
             if (i + 3 < n) compute_store<0, false>(pf[3].x, pf[3].y, i + 3);
             if (i + 4 < n) compute_store<1, false>(pf[4].x, pf[4].y, i + 4);
         } else {
-            if constexpr (pingpong_loop<K>()) {
+            if constexpr (pingpong_loop<K, ROWS>()) {
                 // Two register triples in turn (rows i..i+2 in pf, i+3..i+5 in q): each is refilled
                 // right after its rows were computed, so no prefetched register is ever copied.  (With
                 // the one-triple loop below the compiler copies the new pf[2] into the register of the
