@@ -396,6 +396,17 @@ struct RowsSplit {
     }
 };
 
+// Two register triples in the band loop for LDS passes of 4 levels (8192^2 tile@24: 1.457-1.494 ->
+// 1.437-1.453 us/gen; no gain at 2 levels, profiles/pingpong_loop_ab.txt).  GOL_TILE_PINGPONG=0/1
+// forces it off / on for every level count.
+template <int LV>
+constexpr bool tile_pingpong() {
+#ifdef GOL_TILE_PINGPONG
+    return GOL_TILE_PINGPONG != 0;
+#else
+    return LV >= 4;
+#endif
+}
 // Stream input rows 0 .. n-1 of `in` (n >= 2*LV+1) through an LV-level register window (LV
 // generations per LDS pass); outputs rows LV .. n-LV-1.
 template <bool LAST, int LV, typename SRC>
@@ -427,6 +438,33 @@ __device__ __forceinline__ void tile_band(const SRC& in, int n, BandSink<LAST>& 
     u32 l0 = in.row(i)[lane], h0 = in.row(i)[64 + lane];
     u32 l1 = in.row(i + 1)[lane], h1 = in.row(i + 1)[64 + lane];
     u32 l2 = in.row(i + 2)[lane], h2 = in.row(i + 2)[64 + lane];
+    if constexpr (tile_pingpong<LV>()) {
+        // Two register triples in turn (as in step_temporal's two-triple loop): each is refilled right
+        // after its rows were computed, so no freshly read register is copied (a copy waits for the read
+        // just issued, and with 2 waves per SIMD nothing else hides that latency).
+        for (; i + 6 <= n; i += 6) {
+            const u32 m0 = in.row(i + 3)[lane], g0 = in.row(i + 3)[64 + lane];
+            const u32 m1 = in.row(i + 4)[lane], g1 = in.row(i + 4)[64 + lane];
+            const u32 m2 = in.row(i + 5)[lane], g2 = in.row(i + 5)[64 + lane];
+            __builtin_amdgcn_sched_barrier(0);
+            lo = l0, hi = h0;
+            if (advance<LV, 0, false>(P, lo, hi, i)) out.put(lo, hi);
+            lo = l1, hi = h1;
+            if (advance<LV, 1, false>(P, lo, hi, i + 1)) out.put(lo, hi);
+            lo = l2, hi = h2;
+            if (advance<LV, 2, false>(P, lo, hi, i + 2)) out.put(lo, hi);
+            l0 = in.row(i + 6)[lane], h0 = in.row(i + 6)[64 + lane];
+            l1 = in.row(i + 7)[lane], h1 = in.row(i + 7)[64 + lane];
+            l2 = in.row(i + 8)[lane], h2 = in.row(i + 8)[64 + lane];
+            __builtin_amdgcn_sched_barrier(0);
+            lo = m0, hi = g0;
+            if (advance<LV, 0, false>(P, lo, hi, i + 3)) out.put(lo, hi);
+            lo = m1, hi = g1;
+            if (advance<LV, 1, false>(P, lo, hi, i + 4)) out.put(lo, hi);
+            lo = m2, hi = g2;
+            if (advance<LV, 2, false>(P, lo, hi, i + 5)) out.put(lo, hi);
+        }
+    }
     for (; i + 3 <= n; i += 3) {
         const u32 a0 = l0, b0 = h0, a1 = l1, b1 = h1, a2 = l2, b2 = h2;
         l0 = in.row(i + 3)[lane], h0 = in.row(i + 3)[64 + lane];
