@@ -38,15 +38,17 @@ Engine::Engine(const Geometry& g, const EngineConfig& c, std::shared_ptr<Transpo
     const bool nbrs = g_.dec.P > 1 || xchg_self_;
     const bool tall_strips = nbrs && !two_d() && strip_rows >= 2048;
     const bool tall_tiles = nbrs && two_d() && strip_rows >= 2048;
-    // ... and 64 when the two-sub-tile mode can run (HIP, GOL_SUBTILES auto or 2, 1-D tiles of >=
+    // ... and 128 when the two-sub-tile mode can run (HIP, GOL_SUBTILES auto or 2, 1-D tiles of >=
     // 24576 rows, aligned width, no measurement / watchdog / compat mode, and a transport whose
-    // exchange it can drive): it synchronises its two streams once per superstep, so longer
-    // supersteps keep more of the overlap.  Rank-invariant inputs only.
+    // exchange it can drive): its halves wait for each other once per superstep (a kernel trace
+    // showed ~47 us of one queue and ~12 us of both idle at every boundary), so longer supersteps
+    // pay that less often: 32768^2, 2048 generations, 10.01-10.05 us/gen at 64, 9.94-9.98 at 96,
+    // 9.70-9.79 at 128 (profiles/subtile_superstep_boundaries.txt).  Rank-invariant inputs only.
     const bool sub_transport = cfg_.transport != "host" && (g_.dec.P == 1 || t_->device_buffers());
     const bool sub_tall = cfg_.backend == "hip" && (cfg_.subtiles == 2 || cfg_.subtiles < 0) && !two_d() && strip_rows >= kSubtileMinRows &&
                           g_.dec.W % 64 == 0 && !cfg_.force_split && !cfg_.profile && cfg_.watchdog_s <= 0 &&
                           !cfg_.compat && cfg_.kernel != "lds" && cfg_.kernel != "tile" && sub_transport;
-    const int want = cfg_.halo_depth > 0 ? cfg_.halo_depth : (tall_strips || sub_tall ? 64 : (tall_tiles ? 56 : 32));
+    const int want = cfg_.halo_depth > 0 ? cfg_.halo_depth : (sub_tall ? 128 : (tall_strips ? 64 : (tall_tiles ? 56 : 32)));
     int R = clamp_halo_depth(g_.dec, want);
     if (two_d()) R = std::min(R, 63);  // the column halo is one 64-cell word
     if (cfg_.compat) {

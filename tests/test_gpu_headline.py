@@ -1,6 +1,6 @@
 """The exact headline configuration (bench.py, BASELINE.json metric) against an independent oracle.
 
-32768^2 board, every setting at its default (auto): halo depth 64, the schedule the init-time
+32768^2 board, every setting at its default (auto): halo depth 128, the schedule the init-time
 measurement picks (two sub-tiles on two streams, or one tile), measured pass cuts, the run-length
 hint of the driver's bench (20 timed generations after 5 warmup ones).  The full board is compared
 with a PyTorch fp32 conv2d torus step on cuda:0 (exact for neighbour counts <= 8) after the driver's
@@ -20,7 +20,7 @@ def test_headline_32768_default_path(gol):
     N, seed = 32768, 0x5EED
     sim = gol.Simulation(N, backend="hip", device=0, run_hint=20).init(5, seed=seed)
     st = sim.stats()
-    assert st["depth"] == 64, st
+    assert st["depth"] == 128, st
     assert st["schedule"] in ("local", "local+subtiles2"), st
     ref = torch.as_tensor(initial_board(5, N, 1, True, seed), device="cuda:0")
     sim.step(5)
