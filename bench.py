@@ -38,7 +38,7 @@ def main() -> int:
     ap.add_argument("--scaling", choices=["weak", "strong"], default="weak")
     ap.add_argument("--decomp", default="1d", help="1d | 2d | auto")
     ap.add_argument("--halo-depth", type=int, default=int(os.environ.get("GOL_HALO_DEPTH", "0")),
-                    help="generations per halo exchange (0 = auto: 32; 64 / 56 for multi-GPU strips / 2-D tiles of >= 2048 rows)")
+                    help="generations per halo exchange (0 = auto: 32; 128 / 56 for multi-GPU strips / 2-D tiles of >= 2048 rows)")
     ap.add_argument("--kernel-depth", type=int, default=int(os.environ.get("GOL_KERNEL_DEPTH", "0")),
                     help="generations per kernel pass (0 = auto)")
     ap.add_argument("--kernel", default=os.environ.get("GOL_KERNEL", "auto"),

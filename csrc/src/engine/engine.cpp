@@ -25,7 +25,7 @@ Engine::Engine(const Geometry& g, const EngineConfig& c, std::shared_ptr<Transpo
         throw Error(strprintf("transport (rank %d of %d) does not match the geometry (rank %d of %d)", t_->rank(),
                               t_->size(), g_.rank, g_.dec.P));
     // auto depth: 32 generations per superstep (the tile-kernel autotune tries passes of up to 32
-    // on one rank); with neighbours (or self-exchange, which stands in for them on one GPU), 64 for
+    // on one rank); with neighbours (or self-exchange, which stands in for them on one GPU), 128 for
     // 1-D strips of >= 2048 rows and 56 for 2-D tiles of >= 2048 rows (the column halo is one word:
     // <= 63): an exchange costs an RCCL kernel plus ~15 us of cross-stream event latency however
     // small it is (kernel traces of the 4096 x 32768 strip of config 3 strong-scaled over 8 GPUs:
@@ -48,7 +48,9 @@ Engine::Engine(const Geometry& g, const EngineConfig& c, std::shared_ptr<Transpo
     const bool sub_tall = cfg_.backend == "hip" && (cfg_.subtiles == 2 || cfg_.subtiles < 0) && !two_d() && strip_rows >= kSubtileMinRows &&
                           g_.dec.W % 64 == 0 && !cfg_.force_split && !cfg_.profile && cfg_.watchdog_s <= 0 &&
                           !cfg_.compat && cfg_.kernel != "lds" && cfg_.kernel != "tile" && sub_transport;
-    const int want = cfg_.halo_depth > 0 ? cfg_.halo_depth : (sub_tall ? 128 : (tall_strips ? 64 : (tall_tiles ? 56 : 32)));
+    // (1-D strips with neighbours: 128 measured 1-3% faster than 64 through RCCL self-exchange,
+    // 4096 x 32768 2.44 -> 2.36, 8192 x 65536 5.93 -> 5.85 us/gen; profiles/per_rank_tiles_self_exchange.txt)
+    const int want = cfg_.halo_depth > 0 ? cfg_.halo_depth : (sub_tall || tall_strips ? 128 : (tall_tiles ? 56 : 32));
     int R = clamp_halo_depth(g_.dec, want);
     if (two_d()) R = std::min(R, 63);  // the column halo is one 64-cell word
     if (cfg_.compat) {

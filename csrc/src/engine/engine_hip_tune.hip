@@ -136,6 +136,15 @@ void HipEngine::choose_schedule() {
             if (best[c] < best[bi]) bi = c;
         }
         pick = cands[bi];
+        // The split schedule must win by 3% over full: its timing (4 supersteps) favoured it by ~1% on
+        // 1-D strips whose runs then went 2-4% slower than full (8192 x 65536 through RCCL: split
+        // timed 6.41 vs 6.48, ran 6.01 vs 5.85 us/gen); the 2-D tiles where it wins do so by 3-5%.
+        if (pick == "split" && sched_us_.count("full") && sched_us_["split"] > 0.97 * sched_us_["full"]) {
+            size_t b2 = cands.size();
+            for (size_t c = 0; c < cands.size(); ++c)
+                if (cands[c] != "split" && (b2 == cands.size() || best[c] < best[b2])) b2 = c;
+            pick = cands[b2];
+        }
         stats_.exchanges = 0;  // the timing exchanges are not part of the run
         stats_.halo_bytes = 0;
     }

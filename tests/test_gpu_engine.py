@@ -358,15 +358,15 @@ def test_python_threads_device_transport(gol, decomp, grid, P):
     assert np.array_equal(board, numpy_step(initial_board(5, N, 1, True, 9), gens))
 
 
-def test_threads_device_transport_deep_halo_64(gol):
-    """Tall 1-D strips (>= 8192 rows) get the auto halo depth 64: 8 kernel passes per exchange, the
-    first seven also computing ghost rows.  2 thread ranks on one GPU (RCCL-semantics transport),
-    16384^2 board vs the PyTorch conv2d oracle."""
+def test_threads_device_transport_deep_halo_128(gol):
+    """Tall 1-D strips (>= 2048 rows) get the auto halo depth 128: 16 kernel passes per exchange,
+    the earlier ones also computing ghost rows.  2 thread ranks on one GPU (RCCL-semantics
+    transport), 16384^2 board vs the PyTorch conv2d oracle."""
     import threading
 
     import torch
 
-    N, P, gens = 16384, 2, 64 * 2 + 13
+    N, P, gens = 16384, 2, 128 + 64 + 13
     ts = gol.parallel.p2p_thread_transports(P)
     out, errs = [None] * P, []
 
@@ -374,7 +374,7 @@ def test_threads_device_transport_deep_halo_64(gol):
         try:
             s = gol.Simulation(N, ts[r], backend="hip", device=0, global_mode=True)
             s.init(5, seed=5)
-            assert s.stats()["depth"] == 64, s.stats()
+            assert s.stats()["depth"] == 128, s.stats()
             s.step(gens)
             out[r] = (s.geometry.row0, s.board())
         except Exception as e:  # pragma: no cover - reported below

@@ -95,9 +95,9 @@ def test_rccl_self_graph_capture(gol, rccl, decomp, monkeypatch):
 @pytest.mark.parametrize("H,W,decomp", [(2304, 1024, "2d"), (2048, 1536, "1d")])
 def test_rccl_self_auto_depth_rectangular(gol, rccl, H, W, decomp):
     """Rectangular per-rank tiles with the auto halo depth of a rank with neighbours (56 in 2-D,
-    64 in 1-D for >= 2048 rows): every superstep's halos through RCCL."""
-    gens = 2 * 64 + 9
+    128 in 1-D for >= 2048 rows): every superstep's halos through RCCL."""
+    gens = 2 * 128 + 9
     got, st = _run(gol, rccl, H, gens, 6, width=W, decomp=decomp)
-    assert st["depth"] == (56 if decomp == "2d" else 64), st
+    assert st["depth"] == (56 if decomp == "2d" else 128), st
     assert st["exchanges"] >= 2, st
     assert np.array_equal(got, numpy_step(random_board(H, W, 6), gens))
