@@ -66,8 +66,7 @@ const DevPlan& HipEngine::sub_plan(int s, int k, i64 e, int part) {
         // waves per SIMD (K=12) gets 1-wave plans, or the second half waits for the first one's
         // waves to retire (20-generation runs cut 12 + 8 took 14.5-14.8 instead of 11.8 us/gen in a
         // quarter of the runs, profiles/pingpong_loop_ab.txt)
-        const i64 kocc = hipk::step_blocks_per_cu(k, sub_flags());
-        bpc = std::min<i64>(bpc, std::max<i64>(1, kocc - 1));
+        if (hipk::step_blocks_per_cu(k, sub_flags()) <= 2) bpc = 1;
     }
     const i64 rows = balanced_rows_per_chunk(rg, L.nw, L.h, k, bpc * kWavesPerBlock * cus_, 2 * (i64)k, true);
     DevPlan p;
