@@ -97,6 +97,31 @@ def test_rectangular_boards(gol, P, kw):
     assert len(set(fps)) == 1
 
 
+@pytest.mark.parametrize("P,kw,depth", [
+    (1, {"width": 128}, 32),                                                   # one rank: 32
+    (2, {"width": 128, "global_mode": True}, 128),                             # 1-D strips of 2048 rows with neighbours
+    (4, {"width": 256, "decomp": "2d", "grid": "2x2", "global_mode": True}, 56),  # 2-D tiles of 2048 rows: <= 63
+    (2, {"width": 128, "global_mode": True, "halo_depth": 20}, 20),            # explicit depth wins
+])
+def test_auto_halo_depth(gol, P, kw, depth):
+    """The auto halo depth (generations per exchange) is decided from rank-invariant inputs: 32 on one
+    rank, 128 for 1-D strips of >= 2048 rows with neighbours, 56 for 2-D tiles of >= 2048 rows."""
+    N = 4096
+    ts = gol.parallel.thread_transports(P)
+    got = [None] * P
+
+    def worker(r):
+        s = gol.Simulation(N, ts[r], backend="cpu", **kw).init(5, seed=1)
+        got[r] = s.stats()["depth"]
+
+    th = [threading.Thread(target=worker, args=(r,)) for r in range(P)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    assert got == [depth] * P, got
+
+
 def test_fingerprint_decomposition_invariant(gol):
     N, gens = 256, 30
     one = gol.Simulation(N, backend="cpu", global_mode=True).init(5, 99).step(gens).fingerprint()
