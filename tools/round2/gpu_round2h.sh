@@ -1,0 +1,18 @@
+#!/bin/bash
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
+mkdir -p gpurun_out/r2h
+export TMPDIR=/tmp
+run() {
+  local name=$1 t=$2; shift 2
+  echo "=== $name ($(date +%T))"
+  timeout -k 10 "$t" "$@" > "gpurun_out/r2h/$name.log" 2>&1
+  local rc=$?
+  echo "=== $name rc=$rc"; tail -n 2 "gpurun_out/r2h/$name.log" | cut -c1-300
+  return $rc
+}
+run pytest_sub 300 python -u -m pytest tests/test_gpu_engine.py -k "subtiles or hint" -x -q -m gpu --timeout 120 --timeout-method thread || exit $?
+run pytest_engine 600 python -u -m pytest tests/test_gpu_engine.py tests/test_gpu_rccl.py tests/test_gpu_headline.py -x -q -m gpu --timeout 200 --timeout-method thread || exit $?
+for i in 1 2 3; do run bench_$i 120 python bench.py --gpus 1 --steps 20 --warmup 5 || exit $?; done
+run bench_long 200 python bench.py --gpus 1 --steps 2000 --warmup 200 || exit $?
+run bench_self 200 python bench.py --gpus 1 --steps 20 --warmup 5 --self-exchange || exit $?
+run short 300 python tools/short_run_probe.py --variants sub2,sub0 || exit $?

@@ -1,0 +1,8 @@
+#!/bin/bash
+# shallow passes: rotating 6-row prefetch (pf2) vs queue-shift prefetch (pf1, previous build), 32768^2
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
+mkdir -p gpurun_out/r2u
+for K in 1 2 3 4 8; do for s2 in 0 1; do for v in pf1 pf2; do
+  r=$(KB_SPLIT2=$s2 timeout -k 5 60 ./build/kbench_$v 32768 $K $((K*40)) 2>&1 | tail -1) || exit 1
+  echo "$v K=$K split2=$s2 $r" | tee -a gpurun_out/r2u/ab.txt | sed 's/"skew.*"rows"/rows/' | cut -c1-140
+done; done; done
