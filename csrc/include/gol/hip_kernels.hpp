@@ -31,6 +31,7 @@ enum : u32 {
     STEP_TILE_L2 = 1u << 4, // tile kernel: two generations per LDS pass (half the barriers)
     STEP_TILE_L4 = 1u << 6, // tile kernel: four generations per LDS pass
     STEP_TILE_INPLACE = 1u << 7,  // tile kernel: one tile buffer updated in place (twice the rows)
+    STEP_TILE_FOLD = 1u << 8,     // tile kernel: 32-lane tiles folded in half (fold plans, plan.hpp)
     STEP_SEAM = 1u << 5,    // temporal kernel: rows < 0 are read from StepParams::above, rows >= h
                             // from StepParams::below (sub-tile first pass: the other half's edges)
 };
@@ -69,6 +70,8 @@ void launch_step(int k, const u64* src, u64* dst, const LaneDesc* plan, i64 n_wa
 // LDS-resident temporal kernel (step_tile): one workgroup of `nw_per_wg` (4, 8, 16) waves per plan
 // wave; `rows` = the plan's rows per chunk (<= tile_max_rows(k), the 160 KiB LDS limit).
 constexpr size_t kMaxLdsBytes = 160 * 1024;
+// Least chunk height of a folded-tile plan (STEP_TILE_FOLD): its segments are >= 14 rows tall.
+constexpr int kFoldMinRows = 28;
 i64 tile_max_rows(int k, int nw_per_wg, u32 flags);
 int tile_blocks_per_cu(int nw_per_wg, i64 rows, int k, u32 flags);
 void launch_step_tile(int nw_per_wg, int k, const u64* src, u64* dst, const LaneDesc* plan, i64 n_tiles, i64 rows,

@@ -60,9 +60,12 @@ struct PlanStats {
 // lanes right of word nw-1 stream word 0, so no ghost words are needed.
 // Waves are ordered for L2 locality: column-major, and whole workgroups of `wg_waves` waves
 // permuted so each of the `xcds` XCDs (workgroup b runs on XCD b % xcds) gets a contiguous stretch.
+// With `fold` (the tile kernel's STEP_TILE_FOLD) segments are packed into 32-lane tiles of <= 30
+// output words, and each tile's 64 lanes are its 32 lanes twice: the kernel folds the tile's rows so
+// lanes 0-31 stream the top half and lanes 32-63 (bottom up) the bottom half.
 std::vector<LaneDesc> build_plan(const std::vector<Region>& regions, i64 nw, i64 h, i64 rows_per_chunk, int k,
                                  bool xwrap, PlanStats* stats = nullptr, int wg_waves = kWavesPerBlock,
-                                 int xcds = 8);
+                                 int xcds = 8, bool fold = false);
 
 // Bounds check of a plan before it is uploaded (a bad plan would fault the GPU): every lane's word
 // column lies in [-1, nw]; without y-wrap its input rows [row0-k, row0+nrows+k) lie in the
@@ -72,7 +75,7 @@ std::vector<LaneDesc> build_plan(const std::vector<Region>& regions, i64 nw, i64
 std::string validate_plan(const std::vector<LaneDesc>& lanes, i64 nw, i64 h, int R, int k, bool wrap_y);
 
 // Number of waves (padded to whole workgroups) of the plan, without materialising lanes.
-i64 plan_waves(const std::vector<Region>& regions, i64 nw, i64 h, i64 rows_per_chunk);
+i64 plan_waves(const std::vector<Region>& regions, i64 nw, i64 h, i64 rows_per_chunk, bool fold = false);
 
 // Pick a segment height so that the sweep has enough waves to fill the GPU (about `target_waves`)
 // while keeping the 2k-row vertical halo overhead small.
@@ -82,6 +85,6 @@ i64 choose_rows_per_chunk(const std::vector<Region>& regions, int k, i64 target_
 // `resident_waves` (every wave resident from the start, equal work, no straggler workgroups).
 // Time ~ rounds x (S + k), so one full round with the shortest segments is optimal.
 i64 balanced_rows_per_chunk(const std::vector<Region>& regions, i64 nw, i64 h, int k, i64 resident_waves,
-                            i64 min_rows, bool xwrap);
+                            i64 min_rows, bool xwrap, bool fold = false);
 
 }  // namespace gol

@@ -170,11 +170,12 @@ PYBIND11_MODULE(_gol, m) {
     // ---- planner --------------------------------------------------------------------------
     m.def(
         "build_plan",
-        [](const std::vector<std::tuple<i64, i64, i64, i64>>& regions, i64 nw, i64 h, i64 rows, int k, bool xwrap) {
+        [](const std::vector<std::tuple<i64, i64, i64, i64>>& regions, i64 nw, i64 h, i64 rows, int k, bool xwrap,
+           bool fold) {
             std::vector<Region> rg;
             for (auto& t : regions) rg.push_back({std::get<0>(t), std::get<1>(t), std::get<2>(t), std::get<3>(t)});
             PlanStats st;
-            std::vector<LaneDesc> lanes = build_plan(rg, nw, h, rows, k, xwrap, &st);
+            std::vector<LaneDesc> lanes = build_plan(rg, nw, h, rows, k, xwrap, &st, kWavesPerBlock, 8, fold);
             py::array_t<i32> a({(py::ssize_t)lanes.size(), (py::ssize_t)4});
             std::memcpy(a.mutable_data(), lanes.data(), lanes.size() * sizeof(LaneDesc));
             py::dict d;
@@ -185,7 +186,7 @@ PYBIND11_MODULE(_gol, m) {
             return py::make_tuple(a, d);
         },
         py::arg("regions"), py::arg("nw"), py::arg("h"), py::arg("rows_per_chunk"), py::arg("k"),
-        py::arg("xwrap") = false);
+        py::arg("xwrap") = false, py::arg("fold") = false);
     m.def("choose_rows_per_chunk", [](const std::vector<std::tuple<i64, i64, i64, i64>>& regions, int k, i64 target,
                                       i64 min_rows) {
         std::vector<Region> rg;

@@ -15,6 +15,10 @@ struct Item {
     int lanes() const { return (int)nwords + 2; }
 };
 
+// Lanes of one packed tile: a 64-lane wave, or (fold) the 32-lane half that both halves of a
+// folded tile share (plan.hpp)
+int pack_lanes(bool fold) { return fold ? kWaveLanes / 2 : kWaveLanes; }
+
 }  // namespace
 
 i64 choose_rows_per_chunk(const std::vector<Region>& regions, int k, i64 target_waves, i64 min_rows) {
@@ -34,12 +38,12 @@ i64 choose_rows_per_chunk(const std::vector<Region>& regions, int k, i64 target_
 }
 
 i64 balanced_rows_per_chunk(const std::vector<Region>& regions, i64 nw, i64 h, int k, i64 resident_waves,
-                            i64 min_rows, bool xwrap) {
+                            i64 min_rows, bool xwrap, bool fold) {
     i64 max_rows = 1;
     for (const Region& r : regions) max_rows = std::max(max_rows, r.r1 - r.r0);
     (void)k;
     (void)xwrap;
-    auto waves = [&](i64 S) { return plan_waves(regions, nw, h, S); };
+    auto waves = [&](i64 S) { return plan_waves(regions, nw, h, S, fold); };
     i64 lo = std::max<i64>(1, std::min(min_rows, max_rows)), hi = max_rows;
     if (waves(lo) <= resident_waves) return lo;
     if (waves(hi) > resident_waves) return hi;  // cannot fit one round: fewest, tallest segments
@@ -57,8 +61,10 @@ namespace {
 
 // Cut the regions into segments of <= rows_per_chunk rows x <= 62 words and pack them into waves:
 // full-width segments get a wave each; narrow ones (same height) are packed first-fit-decreasing.
-std::vector<std::vector<Item>> pack_waves(const std::vector<Region>& regions, i64 nw, i64 h, i64 rows_per_chunk) {
+std::vector<std::vector<Item>> pack_waves(const std::vector<Region>& regions, i64 nw, i64 h, i64 rows_per_chunk,
+                                          bool fold) {
     if (rows_per_chunk < 1) rows_per_chunk = 1;
+    const int lw = pack_lanes(fold), sw = lw - 2;
     std::map<i64, std::vector<Item>> by_rows;
     for (const Region& rg : regions) {
         i64 rows = rg.r1 - rg.r0, words = rg.c1 - rg.c0;
@@ -71,8 +77,7 @@ std::vector<std::vector<Item>> pack_waves(const std::vector<Region>& regions, i6
         i64 r = rg.r0;
         for (i64 ch = 0; ch < nch; ++ch) {
             i64 nr = base + (ch < extra ? 1 : 0);
-            for (i64 c = rg.c0; c < rg.c1; c += kSegWords)
-                by_rows[nr].push_back({r, nr, c, std::min<i64>(kSegWords, rg.c1 - c)});
+            for (i64 c = rg.c0; c < rg.c1; c += sw) by_rows[nr].push_back({r, nr, c, std::min<i64>(sw, rg.c1 - c)});
             r += nr;
         }
     }
@@ -80,7 +85,7 @@ std::vector<std::vector<Item>> pack_waves(const std::vector<Region>& regions, i6
     for (auto& kv : by_rows) {
         std::vector<Item> narrow;
         for (const Item& it : kv.second) {
-            if (it.lanes() == kWaveLanes)
+            if (it.lanes() == lw)
                 waves.push_back({it});
             else
                 narrow.push_back(it);
@@ -93,7 +98,7 @@ std::vector<std::vector<Item>> pack_waves(const std::vector<Region>& regions, i6
             bool placed = false;
             for (size_t j = first_open; j < open.size(); ++j) {
                 auto& w = open[j];
-                if (w.first + it.lanes() <= kWaveLanes) {
+                if (w.first + it.lanes() <= lw) {
                     w.first += it.lanes();
                     w.second.push_back(it);
                     placed = true;
@@ -101,7 +106,7 @@ std::vector<std::vector<Item>> pack_waves(const std::vector<Region>& regions, i6
                 }
             }
             if (!placed) open.push_back({it.lanes(), {it}});
-            while (first_open < open.size() && open[first_open].first > kWaveLanes - 3) ++first_open;
+            while (first_open < open.size() && open[first_open].first > lw - 3) ++first_open;
         }
         for (auto& w : open) waves.push_back(std::move(w.second));
     }
@@ -110,13 +115,14 @@ std::vector<std::vector<Item>> pack_waves(const std::vector<Region>& regions, i6
 
 }  // namespace
 
-i64 plan_waves(const std::vector<Region>& regions, i64 nw, i64 h, i64 rows_per_chunk) {
-    return round_up(std::max<i64>(1, (i64)pack_waves(regions, nw, h, rows_per_chunk).size()), kWavesPerBlock);
+i64 plan_waves(const std::vector<Region>& regions, i64 nw, i64 h, i64 rows_per_chunk, bool fold) {
+    return round_up(std::max<i64>(1, (i64)pack_waves(regions, nw, h, rows_per_chunk, fold).size()), kWavesPerBlock);
 }
 
 std::vector<LaneDesc> build_plan(const std::vector<Region>& regions, i64 nw, i64 h, i64 rows_per_chunk, int k,
-                                 bool xwrap, PlanStats* stats, int wg_waves, int xcds) {
-    std::vector<std::vector<Item>> packed = pack_waves(regions, nw, h, rows_per_chunk);
+                                 bool xwrap, PlanStats* stats, int wg_waves, int xcds, bool fold) {
+    std::vector<std::vector<Item>> packed = pack_waves(regions, nw, h, rows_per_chunk, fold);
+    const int lw = pack_lanes(fold);
     i64 nwaves = round_up(std::max<i64>(1, (i64)packed.size()), kWavesPerBlock);
     // XCD-aware order.  The full-width segments are sorted (narrow, packed waves stay last), then
     // whole workgroups are permuted so that XCD x — workgroup b is dispatched to XCD b % xcds — runs
@@ -128,8 +134,8 @@ std::vector<LaneDesc> build_plan(const std::vector<Region>& regions, i64 nw, i64
     // 32768^2 K=1 passes 71 -> 61 us, K=4 17.5 -> 16.1 us/gen, K=8 11.49 -> 11.20 (two halves on two
     // streams), 16384^2 K=8 4.20 -> 4.11 (profiles/plan_order_ab.txt).
     const bool row_major = !(getenv("GOL_PLAN_ORDER") && std::string(getenv("GOL_PLAN_ORDER")) == "col");
-    std::stable_sort(packed.begin(), packed.end(), [row_major](const std::vector<Item>& a, const std::vector<Item>& b) {
-        const bool fa = a.size() == 1 && a[0].lanes() == kWaveLanes, fb = b.size() == 1 && b[0].lanes() == kWaveLanes;
+    std::stable_sort(packed.begin(), packed.end(), [row_major, lw](const std::vector<Item>& a, const std::vector<Item>& b) {
+        const bool fa = a.size() == 1 && a[0].lanes() == lw, fb = b.size() == 1 && b[0].lanes() == lw;
         if (fa != fb) return fa;
         if (!fa) return false;
         if (row_major) return a[0].r0 != b[0].r0 ? a[0].r0 < b[0].r0 : a[0].c0 < b[0].c0;
@@ -182,8 +188,10 @@ std::vector<LaneDesc> build_plan(const std::vector<Region>& regions, i64 nw, i64
             }
         }
         // idle lanes: stream a valid in-bounds column (the first item's first column), never store
-        for (; l < kWaveLanes; ++l) L[l] = {(i32)w[0].r0, (i32)w[0].c0, 0u, (i32)nrows};
-        st.lane_rows += (i64)kWaveLanes * (nrows + 2 * (i64)k);
+        for (; l < lw; ++l) L[l] = {(i32)w[0].r0, (i32)w[0].c0, 0u, (i32)nrows};
+        // folded tile: lanes 32-63 repeat lanes 0-31 (they stream the other half of the same rows)
+        for (; l < kWaveLanes; ++l) L[l] = L[l - lw];
+        st.lane_rows += (i64)lw * (nrows + 2 * (i64)k);
     }
     if (stats) *stats = st;
     return lanes;

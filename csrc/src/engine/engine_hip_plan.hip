@@ -105,15 +105,36 @@ const DevPlan& HipEngine::plan(int kind, int k, i64 e) {
         const i64 r1 = balanced_rows_per_chunk(rg, L_.nw, L_.h, k, cus_, 1, xwrap_by_plan());
         bool ip = tile_inplace_ > 0 || (tile_inplace_ < 0 && r1 > rdb && rip > rdb);
         if (tile_inplace_ < 0 && rows > 0) ip = rows > rdb;
+        // Folded tiles (32 lanes wide, twice as tall, step_kernels.hip step_tile_fold) when one round of
+        // them fits the double buffer: 8192^2 K=24 1.43-1.45 -> 1.39-1.40 us/gen, K=32 1.46 -> 1.38
+        // (profiles/tile_fold_ab.txt).  GOL_TILE_FOLD=0/1 forces.
+        const u32 ff = step_flags() | tile_bits(false) | hipk::STEP_TILE_FOLD;
+        const i64 rfm = hipk::tile_max_rows(k, cfg_.tile_waves, ff);
+        const i64 r1f = balanced_rows_per_chunk(rg, L_.nw, L_.h, k, cus_, hipk::kFoldMinRows, xwrap_by_plan(), true);
+        // A folded tile needs >= kFoldMinRows / 2 rows (segments of a chunk height S are >= S / 2 rows):
+        // regions thinner than that (boundary bands) and tiny boards keep plain tiles.
+        i64 thinnest = 1 << 30;
+        for (const Region& r : rg)
+            if (r.r1 > r.r0 && r.c1 > r.c0) thinnest = std::min(thinnest, r.r1 - r.r0);
+        const bool fold = r1f >= hipk::kFoldMinRows && thinnest >= hipk::kFoldMinRows / 2 &&
+                          (tile_fold_ > 0 || (tile_fold_ < 0 && rows <= 0 && !ip && r1f <= rfm));
+        if (fold) {
+            if (rows <= 0) rows = std::min(r1f, rfm);
+            if (rows < hipk::kFoldMinRows || rows > rfm)
+                throw Error(strprintf("GOL_TILE_FOLD: %lld rows per folded tile outside %d..%lld at depth %d",
+                                      (long long)rows, hipk::kFoldMinRows, (long long)rfm, k));
+            p.tflags = tile_bits(false) | hipk::STEP_TILE_FOLD;
+            p.fold = true;
+        }
         const i64 rmax = ip ? rip : rdb;
-        p.tflags = tile_bits(ip);
+        if (!fold) p.tflags = tile_bits(ip);
         if (rmax < 1) throw Error(strprintf("GOL_KERNEL=tile: depth %d leaves no LDS rows", k));
-        if (rows > rmax) rows = rmax;
+        if (!fold && rows > rmax) rows = rmax;
         if (tile_rounds(kind, k, e) > kMaxTileRounds)
             throw Error(strprintf("GOL_KERNEL=tile: this tile needs %lld rounds of LDS tiles; use the temporal "
                                   "kernel for boards this large",
                                   (long long)tile_rounds(kind, k, e)));
-        if (rows <= 0) {
+        if (rows <= 0) {  // (a folded plan has its rows already)
             const i64 rounds = ceil_div(r1, rmax);
             rows = rounds <= 1 ? r1
                                : std::min(rmax, balanced_rows_per_chunk(rg, L_.nw, L_.h, k, rounds * cus_, 1,
@@ -133,7 +154,7 @@ const DevPlan& HipEngine::plan(int kind, int k, i64 e) {
         }
     }
     std::vector<LaneDesc> lanes = build_plan(rg, L_.nw, L_.h, rows, k, xwrap_by_plan(), &p.st,
-                                             tile_kernel(kind) ? 1 : kWavesPerBlock, cfg_.plan_xcds);
+                                             tile_kernel(kind) ? 1 : kWavesPerBlock, cfg_.plan_xcds, p.fold);
     const std::string bad = validate_plan(lanes, L_.nw, L_.h, L_.R, k, (step_flags() & hipk::STEP_WRAP_Y) != 0);
     if (!bad.empty()) throw Error(strprintf("refusing to launch an unsafe plan (kind %d, k %d, e %lld): %s", kind, k,
                                             (long long)e, bad.c_str()));

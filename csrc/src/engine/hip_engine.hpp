@@ -38,7 +38,8 @@ struct DevPlan {
     LaneDesc* d = nullptr;
     i64 waves = 0;
     i64 rows = 0;  // rows per chunk
-    u32 tflags = 0;  // tile kernel: variant bits (LDS levels per pass, in place)
+    u32 tflags = 0;  // tile kernel: variant bits (LDS levels per pass, in place, folded)
+    bool fold = false;  // tile kernel: folded 32-lane tiles (plan.hpp build_plan(..., fold))
     PlanStats st;
 };
 
@@ -459,6 +460,7 @@ class HipEngine : public Engine {
     int occ_ = 0;
     // tile kernel: one LDS buffer updated in place (1), double-buffered (0), or per plan (-1, auto)
     int tile_inplace_ = (int)env_int("GOL_TILE_INPLACE", -1);
+    int tile_fold_ = (int)env_int("GOL_TILE_FOLD", -1);
     int tile_lv_ = (int)env_int("GOL_TILE_LEVELS", 0);  // tile kernel: generations per LDS pass (1, 2, 4; 0 auto)
     bool multipass_ = false;
     std::map<int, std::vector<int>> passes_;

@@ -385,6 +385,8 @@ struct BandSink {
 struct RowsLinear {
     const u32* base;
     __device__ __forceinline__ const u32* row(int i) const { return base + i * kTileRowU32; }
+    __device__ __forceinline__ u32 lo(int i, int lane) const { return row(i)[lane]; }
+    __device__ __forceinline__ u32 hi(int i, int lane) const { return row(i)[64 + lane]; }
 };
 struct RowsSplit {
     const u32* above;  // LV rows, then the rows below (and over-read slack)
@@ -394,6 +396,8 @@ struct RowsSplit {
         return i < lv ? above + i * kTileRowU32
                       : (i < lv + m ? mid + (i - lv) * kTileRowU32 : above + (i - m) * kTileRowU32);
     }
+    __device__ __forceinline__ u32 lo(int i, int lane) const { return row(i)[lane]; }
+    __device__ __forceinline__ u32 hi(int i, int lane) const { return row(i)[64 + lane]; }
 };
 
 // Two register triples in the band loop for LDS passes of 4 levels (8192^2 tile@24: 1.457-1.494 ->
@@ -409,13 +413,13 @@ constexpr bool tile_pingpong() {
 }
 // Stream input rows 0 .. n-1 of `in` (n >= 2*LV+1) through an LV-level register window (LV
 // generations per LDS pass); outputs rows LV .. n-LV-1.
-template <bool LAST, int LV, typename SRC>
-__device__ __forceinline__ void tile_band(const SRC& in, int n, BandSink<LAST>& out, int lane) {
+template <int LV, typename SRC, typename SINK>
+__device__ __forceinline__ void tile_band(const SRC& in, int n, SINK& out, int lane) {
     Pipe<LV> P;
     u32 lo, hi;
 #define GOL_TILE_ROW(PH, GUARD, IDX)                                   \
-    lo = in.row(IDX)[lane];                                            \
-    hi = in.row(IDX)[64 + lane];                                       \
+    lo = in.lo((IDX), lane);                                           \
+    hi = in.hi((IDX), lane);                                           \
     if (advance<LV, PH, GUARD>(P, lo, hi, (IDX))) out.put(lo, hi);
     constexpr int i0 = ((2 * LV + 2) / 3) * 3;  // first multiple of 3 with the window full
     int i = 0;
@@ -435,17 +439,17 @@ __device__ __forceinline__ void tile_band(const SRC& in, int n, BandSink<LAST>& 
     // too few to hide it by switching waves: 35% of wave time was s_waitcnt, PMC at 8192^2).  The
     // last prefetch reads up to 3 rows past the band: still inside the tile buffers or the LDS slack
     // rows (tile_lds_bytes), and never used.
-    u32 l0 = in.row(i)[lane], h0 = in.row(i)[64 + lane];
-    u32 l1 = in.row(i + 1)[lane], h1 = in.row(i + 1)[64 + lane];
-    u32 l2 = in.row(i + 2)[lane], h2 = in.row(i + 2)[64 + lane];
+    u32 l0 = in.lo(i, lane), h0 = in.hi(i, lane);
+    u32 l1 = in.lo(i + 1, lane), h1 = in.hi(i + 1, lane);
+    u32 l2 = in.lo(i + 2, lane), h2 = in.hi(i + 2, lane);
     if constexpr (tile_pingpong<LV>()) {
         // Two register triples in turn (as in step_temporal's two-triple loop): each is refilled right
         // after its rows were computed, so no freshly read register is copied (a copy waits for the read
         // just issued, and with 2 waves per SIMD nothing else hides that latency).
         for (; i + 6 <= n; i += 6) {
-            const u32 m0 = in.row(i + 3)[lane], g0 = in.row(i + 3)[64 + lane];
-            const u32 m1 = in.row(i + 4)[lane], g1 = in.row(i + 4)[64 + lane];
-            const u32 m2 = in.row(i + 5)[lane], g2 = in.row(i + 5)[64 + lane];
+            const u32 m0 = in.lo(i + 3, lane), g0 = in.hi(i + 3, lane);
+            const u32 m1 = in.lo(i + 4, lane), g1 = in.hi(i + 4, lane);
+            const u32 m2 = in.lo(i + 5, lane), g2 = in.hi(i + 5, lane);
             __builtin_amdgcn_sched_barrier(0);
             lo = l0, hi = h0;
             if (advance<LV, 0, false>(P, lo, hi, i)) out.put(lo, hi);
@@ -453,9 +457,9 @@ __device__ __forceinline__ void tile_band(const SRC& in, int n, BandSink<LAST>& 
             if (advance<LV, 1, false>(P, lo, hi, i + 1)) out.put(lo, hi);
             lo = l2, hi = h2;
             if (advance<LV, 2, false>(P, lo, hi, i + 2)) out.put(lo, hi);
-            l0 = in.row(i + 6)[lane], h0 = in.row(i + 6)[64 + lane];
-            l1 = in.row(i + 7)[lane], h1 = in.row(i + 7)[64 + lane];
-            l2 = in.row(i + 8)[lane], h2 = in.row(i + 8)[64 + lane];
+            l0 = in.lo(i + 6, lane), h0 = in.hi(i + 6, lane);
+            l1 = in.lo(i + 7, lane), h1 = in.hi(i + 7, lane);
+            l2 = in.lo(i + 8, lane), h2 = in.hi(i + 8, lane);
             __builtin_amdgcn_sched_barrier(0);
             lo = m0, hi = g0;
             if (advance<LV, 0, false>(P, lo, hi, i + 3)) out.put(lo, hi);
@@ -467,9 +471,9 @@ __device__ __forceinline__ void tile_band(const SRC& in, int n, BandSink<LAST>& 
     }
     for (; i + 3 <= n; i += 3) {
         const u32 a0 = l0, b0 = h0, a1 = l1, b1 = h1, a2 = l2, b2 = h2;
-        l0 = in.row(i + 3)[lane], h0 = in.row(i + 3)[64 + lane];
-        l1 = in.row(i + 4)[lane], h1 = in.row(i + 4)[64 + lane];
-        l2 = in.row(i + 5)[lane], h2 = in.row(i + 5)[64 + lane];
+        l0 = in.lo(i + 3, lane), h0 = in.hi(i + 3, lane);
+        l1 = in.lo(i + 4, lane), h1 = in.hi(i + 4, lane);
+        l2 = in.lo(i + 5, lane), h2 = in.hi(i + 5, lane);
         __builtin_amdgcn_sched_barrier(0);
         lo = a0, hi = b0;
         if (advance<LV, 0, false>(P, lo, hi, i)) out.put(lo, hi);
@@ -524,10 +528,10 @@ __device__ __forceinline__ void tile_pass(u32* A, u32* B, u32* side, u64* dst, c
     auto stream = [&](auto& sink) {
         if constexpr (IP) {
             const RowsSplit in{sw, A + r0 * kTileRowU32, LV, r1 - r0};
-            tile_band<std::remove_reference_t<decltype(sink)>::kLast, LV>(in, n, sink, lane);
+            tile_band<LV>(in, n, sink, lane);
         } else {
             const RowsLinear in{A + (r0 - LV) * kTileRowU32};
-            tile_band<std::remove_reference_t<decltype(sink)>::kLast, LV>(in, n, sink, lane);
+            tile_band<LV>(in, n, sink, lane);
         }
     };
     if (g + LV < K) {
@@ -621,11 +625,132 @@ __global__ __launch_bounds__(64 * NW) void step_tile(const u64* __restrict__ src
     GOL_STAMP(kStampSlotsLast);
 }
 
+// ------------------------------------------------------------------------------------------
+// step_tile_fold (STEP_TILE_FOLD): the tile kernel with the tile folded in half.  A tile is 32 lanes
+// wide (<= 30 output words + 2 halo lanes, plan.hpp fold plans) and twice as tall: lanes 0-31 stream
+// its top half downwards, lanes 32-63 its bottom half upwards (B3/S23 is symmetric, so the level
+// pipeline runs unchanged in either direction).  Virtual row j is tile row j for half 0 and tile row
+// T-1-j for half 1 (T = nrows + 2K staged rows, Th = ceil(T/2)); generation g computes virtual rows
+// [g+1, Th) in both halves, so the trapezoid shrinks at the tile's two outer edges only and its
+// vertical halo (2K rows) is paid over twice the output rows: at 8192^2, K=24 the computed rows per
+// output row drop from ~1.35 (68-row tiles) to ~1.17 (139-row tiles) at ~4% more halo lanes.
+//
+// LDS row j holds virtual row j of both halves in the tile kernel's layout ([lo of lanes 0-63][hi of
+// lanes 0-63]), so the band stream and its sinks are step_tile's, with no per-lane row arithmetic.
+// Where the halves meet, a band reads LV virtual rows past Th: row Th+x of half 0 is tile row Th+x,
+// i.e. half 1's virtual row T-1-Th-x, and vice versa.  Those rows are kept as mirrors: staged with
+// the same formula, and every pass that writes virtual row v in [T-Th-4, T-1-Th] also writes it to
+// row T-1-v in the other half's lanes (lane ^ 32), so no lane ever reads another half's slot.
+// ------------------------------------------------------------------------------------------
+constexpr int kFoldMirror = 4;  // mirrored rows past the middle (the deepest LDS pass, LV <= 4)
+
+struct FoldSink {
+    static constexpr bool kLast = false;
+    u32* lds;
+    int row;     // virtual row of the next output
+    int lane;
+    int m_lo;    // rows m_lo .. tm1 - Th are mirrored to row tm1 - row
+    int m_hi;
+    int tm1;     // T - 1
+    __device__ __forceinline__ void put(u32 lo, u32 hi) {
+        lds[row * kTileRowU32 + lane] = lo;
+        lds[row * kTileRowU32 + 64 + lane] = hi;
+        if (row >= m_lo && row <= m_hi) {  // wave-uniform
+            const int m = tm1 - row;
+            lds[m * kTileRowU32 + (lane ^ 32)] = lo;
+            lds[m * kTileRowU32 + 64 + (lane ^ 32)] = hi;
+        }
+        ++row;
+    }
+};
+
+// LDS rows of one buffer of a folded tile: Th rows, the mirrors, and the band stream's over-read
+__host__ __device__ constexpr int fold_buffer_rows(int T) { return (T + 1) / 2 + kFoldMirror + 4; }
+
+template <int NW, int LV>
+__device__ __forceinline__ void fold_pass(const u32* A, u32* B, u64* dst, const LaneDesc& d, const StepParams& p,
+                                          int K, int g, int T, int wv, int lane) {
+    const int Th = (T + 1) / 2;
+    const int lo_r = g + LV, cnt = Th - g - LV;
+    const int b = (cnt + NW - 1) / NW;
+    const int r0 = lo_r + wv * b;
+    const int r1 = min(r0 + b, lo_r + cnt);
+    if (r1 <= r0) return;
+    const int n = r1 - r0 + 2 * LV;
+    const RowsLinear in{A + (r0 - LV) * kTileRowU32};
+    if (g + LV < K) {
+        FoldSink sk{B, r0, lane, T - Th - kFoldMirror, T - 1 - Th, T - 1};
+        tile_band<LV>(in, n, sk, lane);
+    } else {
+        // virtual row r0 is tile row t0, output row row0 + t0 - K; half 1 stores upwards
+        const int half = lane >> 5;
+        const int t0 = half ? T - 1 - r0 : r0;
+        const bool out_lane = d.flags & LANE_STORE;
+        uint2* st = out_lane ? reinterpret_cast<uint2*>(dst + (i64)(d.row0 + t0 - K + p.R) * p.pitch + (d.col + 1))
+                             : reinterpret_cast<uint2*>(p.trash + ((i64)((blockIdx.x * NW + wv) & (kTrashWaves - 1)) * 64 + lane));
+        BandSink<true> sk{nullptr, st, out_lane ? (half ? -p.pitch : p.pitch) : 0, 0, lane};
+        tile_band<LV>(in, n, sk, lane);
+    }
+}
+
+template <int NW, bool WRAPY, int LV>
+__global__ __launch_bounds__(64 * NW) void step_tile_fold(const u64* __restrict__ src, u64* __restrict__ dst,
+                                                          const LaneDesc* __restrict__ plan, StepParams p, int K) {
+    extern __shared__ __attribute__((aligned(16))) u32 tile_lds[];
+    const int lane = threadIdx.x & 63;
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const LaneDesc d = plan[(i64)blockIdx.x * kWaveLanes + lane];  // lanes 32-63 repeat lanes 0-31
+    const int nrows = __builtin_amdgcn_readfirstlane(d.nrows);
+    if (nrows <= 0) return;  // padding tile (uniform over the workgroup)
+    const int T = nrows + 2 * K;
+    const int nb = fold_buffer_rows(T);
+    u32* A = tile_lds;
+    u32* B = tile_lds + nb * kTileRowU32;
+
+    // 1. stage LDS rows 0 .. Th+kFoldMirror+3: row j = tile row j (half 0) / T-1-j (half 1), tile row t
+    //    being board row row0-K+t; two 4-byte DMAs per row (lo plane, hi plane)
+    const int half = lane >> 5;
+    for (int i = wv; i < nb; i += NW) {
+        const int t = half ? T - 1 - i : i;
+        int r = d.row0 - K + t;
+        if (WRAPY) r = r < 0 ? r + p.h : (r >= p.h ? r - p.h : r);
+        const u32* g = reinterpret_cast<const u32*>(src + (i64)(r + p.R) * p.pitch + (d.col + 1));
+        u32* l = A + i * kTileRowU32;
+        __builtin_amdgcn_global_load_lds((glb_void_t*)g, (lds_void_t*)l, 4, 0, 0);
+        __builtin_amdgcn_global_load_lds((glb_void_t*)(g + 1), (lds_void_t*)(l + 64), 4, 0, 0);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+
+    // 2. K generations in LDS passes of up to LV levels, as step_tile (double-buffered)
+    for (int g = 0; g < K;) {
+        const int left = K - g;
+        int lv = 1;
+        if (LV >= 4 && left >= 4) {
+            lv = 4;
+            fold_pass<NW, (LV >= 4 ? 4 : 1)>(A, B, dst, d, p, K, g, T, wv, lane);
+        } else if (LV >= 2 && left >= 2) {
+            lv = 2;
+            fold_pass<NW, (LV >= 2 ? 2 : 1)>(A, B, dst, d, p, K, g, T, wv, lane);
+        } else {
+            fold_pass<NW, 1>(A, B, dst, d, p, K, g, T, wv, lane);
+        }
+        g += lv;
+        if (g < K) {
+            __syncthreads();
+            u32* t = A;
+            A = B;
+            B = t;
+        }
+    }
+}
+
 int tile_levels(u32 flags) { return (flags & STEP_TILE_L4) ? 4 : ((flags & STEP_TILE_L2) ? 2 : 1); }
 
 // LDS rows of a tile with `rows` output rows at depth k: double-buffered, two copies of the tile
 // (+4 rows of over-read slack); in place, one copy plus NW private side rows per wave.
 i64 tile_lds_rows(i64 rows, int k, int nw, u32 flags) {
+    if (flags & STEP_TILE_FOLD) return 2 * (i64)fold_buffer_rows((int)(rows + 2 * (i64)k));
     if (flags & STEP_TILE_INPLACE) return rows + 2 * (i64)k + (i64)nw * tile_side_rows(tile_levels(flags));
     return 2 * (rows + 2 * (i64)k) + 4;
 }
@@ -642,7 +767,16 @@ const void* tile_kernel_ip(u32 flags) {
     return (flags & STEP_WRAP_Y) ? (const void*)step_tile<NW, true, 1, IP> : (const void*)step_tile<NW, false, 1, IP>;
 }
 template <int NW>
+const void* tile_kernel_fold(u32 flags) {
+    if (flags & STEP_TILE_L4)
+        return (flags & STEP_WRAP_Y) ? (const void*)step_tile_fold<NW, true, 4> : (const void*)step_tile_fold<NW, false, 4>;
+    if (flags & STEP_TILE_L2)
+        return (flags & STEP_WRAP_Y) ? (const void*)step_tile_fold<NW, true, 2> : (const void*)step_tile_fold<NW, false, 2>;
+    return (flags & STEP_WRAP_Y) ? (const void*)step_tile_fold<NW, true, 1> : (const void*)step_tile_fold<NW, false, 1>;
+}
+template <int NW>
 const void* tile_kernel(u32 flags) {
+    if (flags & STEP_TILE_FOLD) return tile_kernel_fold<NW>(flags);
     return (flags & STEP_TILE_INPLACE) ? tile_kernel_ip<NW, true>(flags) : tile_kernel_ip<NW, false>(flags);
 }
 
@@ -765,6 +899,7 @@ void launch_step(int k, const u64* src, u64* dst, const LaneDesc* plan, i64 n_wa
 
 i64 tile_max_rows(int k, int nw_per_wg, u32 flags) {
     const i64 lds_rows = kMaxLdsBytes / (kTileRowU32 * 4);  // 320 rows of 512 B
+    if (flags & STEP_TILE_FOLD) return 2 * (lds_rows / 2 - kFoldMirror - 4) - 1 - 2 * (i64)k;
     if (flags & STEP_TILE_INPLACE) return lds_rows - (i64)nw_per_wg * tile_side_rows(tile_levels(flags)) - 2 * (i64)k;
     return (lds_rows - 4) / 2 - 2 * (i64)k;
 }
@@ -772,10 +907,10 @@ i64 tile_max_rows(int k, int nw_per_wg, u32 flags) {
 static const void* tile_kernel_checked(int nw_per_wg, u32 flags) {
     const void* f = tile_kernel_for(nw_per_wg, flags);
     if (!f) throw Error(strprintf("step_tile: unsupported waves per workgroup %d (4, 8 or 16)", nw_per_wg));
-    static bool attr_set[256] = {};
+    static bool attr_set[512] = {};
     const int lvk = (flags & STEP_TILE_L4) ? 2 : ((flags & STEP_TILE_L2) ? 1 : 0);
     const int key = (((nw_per_wg & 15) * 2 + ((flags & STEP_WRAP_Y) ? 1 : 0)) * 3 + lvk) * 2 +
-                    ((flags & STEP_TILE_INPLACE) ? 1 : 0);
+                    ((flags & STEP_TILE_INPLACE) ? 1 : 0) + ((flags & STEP_TILE_FOLD) ? 256 : 0);
     if (!attr_set[key]) {  // allow the full 160 KiB of dynamic LDS
         hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kMaxLdsBytes);
         if (e != hipSuccess) throw Error(strprintf("step_tile: hipFuncSetAttribute: %s", hipGetErrorString(e)));
@@ -801,6 +936,12 @@ void launch_step_tile(int nw_per_wg, int k, const u64* src, u64* dst, const Lane
     if (rows < 1 || rows > rmax)
         throw Error(strprintf("step_tile: %lld rows per tile exceed the LDS capacity (max %lld at depth %d)",
                               (long long)rows, (long long)rmax, k));
+    // folded tiles: the staged mirror and over-read rows past the middle are tile rows < T
+    // (K + nrows/2 >= 8) and every pass but the last recomputes the mirrored rows (nrows >= 6): the
+    // plan's segments are >= rows/2 >= 14 rows (engine and kbench: regions of >= kFoldMinRows/2 rows)
+    if ((p.flags & STEP_TILE_FOLD) && rows < kFoldMinRows)
+        throw Error(strprintf("step_tile: a folded tile plan needs at least %d rows (got %lld)", kFoldMinRows,
+                              (long long)rows));
     const void* f = tile_kernel_checked(nw_per_wg, p.flags);
     StepParams pp = p;
     if (!pp.trash) pp.trash = trash_of_current_device();

@@ -15,6 +15,8 @@ def naive_byte_run(N: int, generations: int, threads: int = 256, sync_each: bool
     return _native.naive_byte_run(N, generations, threads, sync_each, seed)
 
 
-def build_plan(regions, nw, h, rows_per_chunk, k, xwrap=False):
-    """Lane descriptors of the temporal kernel's work plan: (array[n_lanes, 4], stats)."""
-    return _native.build_plan(regions, nw, h, rows_per_chunk, k, xwrap)
+def build_plan(regions, nw, h, rows_per_chunk, k, xwrap=False, fold=False):
+    """Lane descriptors of the temporal kernel's work plan: (array[n_lanes, 4], stats).
+
+    fold=True: the folded tile kernel's plan (32-lane tiles, lanes 32-63 repeat lanes 0-31)."""
+    return _native.build_plan(regions, nw, h, rows_per_chunk, k, xwrap, fold)

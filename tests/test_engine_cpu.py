@@ -152,6 +152,27 @@ def test_plan_coverage(gol):
     assert st["out_words"] == 100 * 300
 
 
+@pytest.mark.parametrize("nw,h,rows", [(128, 300, 139), (300, 100, 13), (7, 50, 12)])
+def test_fold_plan(gol, nw, h, rows):
+    # folded tiles (step_tile_fold): segments of <= 30 words packed into 32 lanes, lanes 32-63 of each
+    # tile repeat lanes 0-31, and every output word is stored by exactly one lane of the first halves
+    lanes, st = gol.ops.build_plan([(0, h, 0, nw)], nw, h, rows, 24, True, fold=True)
+    tiles = lanes.reshape(-1, 64, 4)
+    assert (tiles[:, :32] == tiles[:, 32:]).all()
+    cover = np.zeros((h, nw), int)
+    for row0, col, flags, nrows in tiles[:, :32].reshape(-1, 4):
+        if flags & 1:
+            cover[row0 : row0 + nrows, col] += 1
+    assert (cover == 1).all()
+    assert st["out_words"] == h * nw
+    for t in tiles[:, :32]:  # each segment: a halo lane, <= 30 output words, a halo lane
+        run = 0
+        for f in t[:, 2] & 1:
+            run = run + 1 if f else 0
+            assert run <= 30
+        assert not (t[0, 2] & 1) and not (t[31, 2] & 1)
+
+
 def test_dump_format_helpers(gol):
     from gol_amd.utils import format_dump, read_dump
 

@@ -275,6 +275,28 @@ def test_tile_kernel_sizes(gol, N):
     assert np.array_equal(s.board(), numpy_step(initial_board(5, N, 1, True, N + 1), gens))
 
 
+@pytest.mark.parametrize("fold", ["0", "1"])
+@pytest.mark.parametrize("N,depth,tile_waves", [(2048, 24, 8), (700, 13, 16), (1000, 5, 4), (640, 32, 8)])
+def test_tile_fold(gol, monkeypatch, fold, N, depth, tile_waves):
+    """Folded tiles (GOL_TILE_FOLD=1: 32-lane tiles twice as tall, lanes 32-63 streaming the bottom
+    half upwards, mirrored middle rows) and plain tiles (0) vs numpy, odd and even tile heights."""
+    monkeypatch.setenv("GOL_TILE_FOLD", fold)
+    gens = 2 * depth + 3
+    s = _sim(gol, N, halo_depth=depth, kernel_depth=depth, kernel="tile", tile_waves=tile_waves).init(5, seed=N + depth)
+    s.step(gens)
+    assert np.array_equal(s.board(), numpy_step(initial_board(5, N, 1, True, N + depth), gens))
+
+
+@pytest.mark.parametrize("fold", ["0", "1"])
+def test_tile_fold_split_ghost_rows(gol, monkeypatch, fold):
+    """Folded tiles in the split schedule (interior and boundary regions, ghost rows, no y-wrap)."""
+    monkeypatch.setenv("GOL_TILE_FOLD", fold)
+    N, gens = 1024, 8 * 6 + 5
+    s = _sim(gol, N, halo_depth=8, kernel="tile", force_split=True).init(5, seed=41)
+    s.step(gens)
+    assert np.array_equal(s.board(), numpy_step(initial_board(5, N, 1, True, 41), gens))
+
+
 @pytest.mark.parametrize("rows", [1, 5, 64])
 def test_tile_kernel_plan_rows(gol, rows):
     N, gens = 640, 21

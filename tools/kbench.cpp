@@ -10,6 +10,7 @@
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
+#include <string>
 #include <vector>
 
 #include "gol/hip_kernels.hpp"
@@ -55,18 +56,20 @@ int main(int argc, char** argv) {
     hipDeviceProp_t prop;
     CK(hipGetDeviceProperties(&prop, 0));
     const int tile_lv = argc > 8 ? atoi(argv[8]) : 1;  // tile kernel: generations per LDS pass
+    const bool fold = tile_nw > 0 && getenv("KB_FOLD") && atoi(getenv("KB_FOLD"));  // folded 32-lane tiles
     (void)pf;
     (void)skew;  // the LDS-ring prefetch and skewed pipeline variants were removed (measured slower)
     const u32 flags = hipk::STEP_WRAP_Y |
                       (tile_lv == 2 ? hipk::STEP_TILE_L2 : 0u) | (tile_lv == 4 ? hipk::STEP_TILE_L4 : 0u) |
-                      (getenv("KB_INPLACE") && atoi(getenv("KB_INPLACE")) ? hipk::STEP_TILE_INPLACE : 0u);
+                      (getenv("KB_INPLACE") && atoi(getenv("KB_INPLACE")) ? hipk::STEP_TILE_INPLACE : 0u) |
+                      (fold ? hipk::STEP_TILE_FOLD : 0u);
     std::vector<Region> rg = {{0, N, 0, L.nw}};
     i64 rows = rows_arg;
     if (tile_nw > 0) {
         const i64 rmax = hipk::tile_max_rows(K, tile_nw, flags);
         if (rows > rmax) rows = rmax;
         for (i64 rounds = 1; rows <= 0; ++rounds) {
-            const i64 r = balanced_rows_per_chunk(rg, L.nw, N, K, rounds * prop.multiProcessorCount, 1, true);
+            const i64 r = balanced_rows_per_chunk(rg, L.nw, N, K, rounds * prop.multiProcessorCount, fold ? hipk::kFoldMinRows : 1, true, fold);
             if (r <= rmax) rows = r;
         }
     } else if (rows <= 0) {
@@ -77,7 +80,14 @@ int main(int argc, char** argv) {
     }
     PlanStats st;
     const int xcds = getenv("KB_XCDS") ? atoi(getenv("KB_XCDS")) : 8;  // 1: plain row-major order
-    std::vector<LaneDesc> lanes = build_plan(rg, L.nw, N, rows, K, true, &st, tile_nw > 0 ? 1 : kWavesPerBlock, xcds);
+    std::vector<LaneDesc> lanes = build_plan(rg, L.nw, N, rows, K, true, &st, tile_nw > 0 ? 1 : kWavesPerBlock, xcds, fold);
+    {
+        const std::string bad = validate_plan(lanes, L.nw, N, L.R, K, true);
+        if (!bad.empty()) {
+            fprintf(stderr, "unsafe plan: %s\n", bad.c_str());
+            return 1;
+        }
+    }
     LaneDesc* dplan;
     CK(hipMalloc(&dplan, lanes.size() * sizeof(LaneDesc)));
     CK(hipMemcpy(dplan, lanes.data(), lanes.size() * sizeof(LaneDesc), hipMemcpyHostToDevice));
@@ -168,6 +178,36 @@ int main(int argc, char** argv) {
         printf("\n");
     }
 #endif
+    if (getenv("KB_CHECK") && atoi(getenv("KB_CHECK")) && tile_nw > 0) {
+        // K generations from the same random board: this tile kernel vs K single-generation passes of
+        // the temporal kernel (its own one-round plan); every word of the board must match
+        hipk::launch_init_fill(a, L, ip, 0);
+        launch(a, b);
+        std::vector<u64> got((size_t)(L.words())), ref((size_t)(L.words()));
+        CK(hipMemcpy(got.data(), b, got.size() * 8, hipMemcpyDeviceToHost));
+        const i64 r1 = balanced_rows_per_chunk(rg, L.nw, N, 1, 4 * kWavesPerBlock * prop.multiProcessorCount, 2, true);
+        PlanStats s1;
+        std::vector<LaneDesc> l1 = build_plan(rg, L.nw, N, r1, 1, true, &s1, kWavesPerBlock, xcds);
+        LaneDesc* dp1;
+        CK(hipMalloc(&dp1, l1.size() * sizeof(LaneDesc)));
+        CK(hipMemcpy(dp1, l1.data(), l1.size() * sizeof(LaneDesc), hipMemcpyHostToDevice));
+        hipk::StepParams s1p{L.pitch, (i32)L.h, (i32)L.nw, L.R, hipk::STEP_WRAP_Y};
+        hipk::launch_init_fill(a, L, ip, 0);
+        for (int g = 0; g < K; ++g) {
+            hipk::launch_step(1, a, b, dp1, s1.waves, s1p, 0);
+            std::swap(a, b);
+        }
+        CK(hipDeviceSynchronize());
+        CK(hipMemcpy(ref.data(), a, ref.size() * 8, hipMemcpyDeviceToHost));
+        i64 bad = 0;
+        for (i64 r = 0; r < N; ++r)
+            for (i64 c = 0; c < L.nw; ++c) {
+                const size_t o = (size_t)((r + L.R) * L.pitch + c + 1);
+                if (got[o] != ref[o]) ++bad;
+            }
+        printf("check: %lld of %lld words differ\n", (long long)bad, (long long)(N * L.nw));
+        if (bad) return 2;
+    }
     const double per_gen_us = best * 1e3 / (steps * K);
     const int bpc = tile_nw > 0 ? hipk::tile_blocks_per_cu(tile_nw, rows, K, flags) : hipk::step_blocks_per_cu(K, flags);
     printf("{\"N\": %lld, \"K\": %d, \"skew\": %d, \"pf\": %d, \"tile_nw\": %d, \"rows\": %lld, \"waves\": %lld, "
