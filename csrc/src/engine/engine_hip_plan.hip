@@ -106,8 +106,8 @@ const DevPlan& HipEngine::plan(int kind, int k, i64 e) {
         bool ip = tile_inplace_ > 0 || (tile_inplace_ < 0 && r1 > rdb && rip > rdb);
         if (tile_inplace_ < 0 && rows > 0) ip = rows > rdb;
         // Folded tiles (32 lanes wide, twice as tall, step_kernels.hip step_tile_fold) when one round of
-        // them fits the double buffer: 8192^2 K=24 1.43-1.45 -> 1.39-1.40 us/gen, K=32 1.46 -> 1.38
-        // (profiles/tile_fold_ab.txt).  GOL_TILE_FOLD=0/1 forces.
+        // them fits: 8192^2 K=24 1.43-1.45 -> 1.39-1.40 us/gen, K=32 1.46 -> 1.38 (double-buffered,
+        // profiles/tile_fold_ab.txt).  GOL_TILE_FOLD=0/1 forces.
         const u32 ff = step_flags() | tile_bits(false) | hipk::STEP_TILE_FOLD;
         const i64 rfm = hipk::tile_max_rows(k, cfg_.tile_waves, ff);
         const i64 r1f = balanced_rows_per_chunk(rg, L_.nw, L_.h, k, cus_, hipk::kFoldMinRows, xwrap_by_plan(), true);
@@ -116,14 +116,20 @@ const DevPlan& HipEngine::plan(int kind, int k, i64 e) {
         i64 thinnest = 1 << 30;
         for (const Region& r : rg)
             if (r.r1 > r.r0 && r.c1 > r.c0) thinnest = std::min(thinnest, r.r1 - r.r0);
+        // Folded in place (one buffer + side rows, twice the rows) only when forced (GOL_TILE_FOLD=1 with a
+        // plan that needs it): on the 4096 x 32768 strip it ties the in-place tile kernel (K=32, 4 levels
+        // 2.40-2.44 vs 2.42-2.44 us/gen; 240 of 256 CUs busy) and loses with 2 levels per LDS pass.
+        const i64 rfmi = hipk::tile_max_rows(k, cfg_.tile_waves, step_flags() | tile_bits(true) | hipk::STEP_TILE_FOLD);
+        const bool fold_ip = tile_inplace_ > 0 || (tile_inplace_ < 0 && r1f > rfm);
+        const i64 fcap = fold_ip ? rfmi : rfm;
         const bool fold = r1f >= hipk::kFoldMinRows && thinnest >= hipk::kFoldMinRows / 2 &&
-                          (tile_fold_ > 0 || (tile_fold_ < 0 && rows <= 0 && !ip && r1f <= rfm));
+                          (tile_fold_ > 0 || (tile_fold_ < 0 && rows <= 0 && !fold_ip && r1f <= fcap));
         if (fold) {
-            if (rows <= 0) rows = std::min(r1f, rfm);
-            if (rows < hipk::kFoldMinRows || rows > rfm)
+            if (rows <= 0) rows = std::min(r1f, fcap);
+            if (rows < hipk::kFoldMinRows || rows > fcap)
                 throw Error(strprintf("GOL_TILE_FOLD: %lld rows per folded tile outside %d..%lld at depth %d",
-                                      (long long)rows, hipk::kFoldMinRows, (long long)rfm, k));
-            p.tflags = tile_bits(false) | hipk::STEP_TILE_FOLD;
+                                      (long long)rows, hipk::kFoldMinRows, (long long)fcap, k));
+            p.tflags = tile_bits(fold_ip) | hipk::STEP_TILE_FOLD;
             p.fold = true;
         }
         const i64 rmax = ip ? rip : rdb;

@@ -667,20 +667,45 @@ struct FoldSink {
 // LDS rows of one buffer of a folded tile: Th rows, the mirrors, and the band stream's over-read
 __host__ __device__ constexpr int fold_buffer_rows(int T) { return (T + 1) / 2 + kFoldMirror + 4; }
 
-template <int NW, int LV>
-__device__ __forceinline__ void fold_pass(const u32* A, u32* B, u64* dst, const LaneDesc& d, const StepParams& p,
+// One LDS pass of a folded tile: double-buffered (IP false: reads A, writes B) or in place (IP true:
+// as step_tile's in-place pass, each wave first copies its band's LV rows above and below into its
+// side rows; the mirrors past the middle are such rows for the middle band, so they too are read from
+// the copy while the pass rewrites them).
+template <int NW, int LV, bool IP>
+__device__ __forceinline__ void fold_pass(u32* A, u32* B, u32* side, u64* dst, const LaneDesc& d, const StepParams& p,
                                           int K, int g, int T, int wv, int lane) {
     const int Th = (T + 1) / 2;
     const int lo_r = g + LV, cnt = Th - g - LV;
     const int b = (cnt + NW - 1) / NW;
     const int r0 = lo_r + wv * b;
     const int r1 = min(r0 + b, lo_r + cnt);
-    if (r1 <= r0) return;
     const int n = r1 - r0 + 2 * LV;
-    const RowsLinear in{A + (r0 - LV) * kTileRowU32};
+    u32* sw = side + wv * tile_side_rows(LV) * kTileRowU32;
+    if constexpr (IP) {
+        if (r1 > r0) {
+#pragma unroll
+            for (int j = 0; j < LV; ++j) {
+                sw[j * kTileRowU32 + lane] = A[(r0 - LV + j) * kTileRowU32 + lane];
+                sw[j * kTileRowU32 + 64 + lane] = A[(r0 - LV + j) * kTileRowU32 + 64 + lane];
+                sw[(LV + j) * kTileRowU32 + lane] = A[(r1 + j) * kTileRowU32 + lane];
+                sw[(LV + j) * kTileRowU32 + 64 + lane] = A[(r1 + j) * kTileRowU32 + 64 + lane];
+            }
+        }
+        __syncthreads();  // every wave's copy is taken before any band is overwritten
+    }
+    if (r1 <= r0) return;
+    auto stream = [&](auto& sink) {
+        if constexpr (IP) {
+            const RowsSplit in{sw, A + r0 * kTileRowU32, LV, r1 - r0};
+            tile_band<LV>(in, n, sink, lane);
+        } else {
+            const RowsLinear in{A + (r0 - LV) * kTileRowU32};
+            tile_band<LV>(in, n, sink, lane);
+        }
+    };
     if (g + LV < K) {
-        FoldSink sk{B, r0, lane, T - Th - kFoldMirror, T - 1 - Th, T - 1};
-        tile_band<LV>(in, n, sk, lane);
+        FoldSink sk{IP ? A : B, r0, lane, T - Th - kFoldMirror, T - 1 - Th, T - 1};
+        stream(sk);
     } else {
         // virtual row r0 is tile row t0, output row row0 + t0 - K; half 1 stores upwards
         const int half = lane >> 5;
@@ -689,11 +714,11 @@ __device__ __forceinline__ void fold_pass(const u32* A, u32* B, u64* dst, const 
         uint2* st = out_lane ? reinterpret_cast<uint2*>(dst + (i64)(d.row0 + t0 - K + p.R) * p.pitch + (d.col + 1))
                              : reinterpret_cast<uint2*>(p.trash + ((i64)((blockIdx.x * NW + wv) & (kTrashWaves - 1)) * 64 + lane));
         BandSink<true> sk{nullptr, st, out_lane ? (half ? -p.pitch : p.pitch) : 0, 0, lane};
-        tile_band<LV>(in, n, sk, lane);
+        stream(sk);
     }
 }
 
-template <int NW, bool WRAPY, int LV>
+template <int NW, bool WRAPY, int LV, bool IP>
 __global__ __launch_bounds__(64 * NW) void step_tile_fold(const u64* __restrict__ src, u64* __restrict__ dst,
                                                           const LaneDesc* __restrict__ plan, StepParams p, int K) {
     extern __shared__ __attribute__((aligned(16))) u32 tile_lds[];
@@ -705,7 +730,8 @@ __global__ __launch_bounds__(64 * NW) void step_tile_fold(const u64* __restrict_
     const int T = nrows + 2 * K;
     const int nb = fold_buffer_rows(T);
     u32* A = tile_lds;
-    u32* B = tile_lds + nb * kTileRowU32;
+    u32* B = tile_lds + nb * kTileRowU32;     // double-buffered: the second buffer
+    u32* side = tile_lds + nb * kTileRowU32;  // in place: NW x tile_side_rows(LV) private rows
 
     // 1. stage LDS rows 0 .. Th+kFoldMirror+3: row j = tile row j (half 0) / T-1-j (half 1), tile row t
     //    being board row row0-K+t; two 4-byte DMAs per row (lo plane, hi plane)
@@ -722,25 +748,27 @@ __global__ __launch_bounds__(64 * NW) void step_tile_fold(const u64* __restrict_
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
 
-    // 2. K generations in LDS passes of up to LV levels, as step_tile (double-buffered)
+    // 2. K generations in LDS passes of up to LV levels, as step_tile
     for (int g = 0; g < K;) {
         const int left = K - g;
         int lv = 1;
         if (LV >= 4 && left >= 4) {
             lv = 4;
-            fold_pass<NW, (LV >= 4 ? 4 : 1)>(A, B, dst, d, p, K, g, T, wv, lane);
+            fold_pass<NW, (LV >= 4 ? 4 : 1), IP>(A, B, side, dst, d, p, K, g, T, wv, lane);
         } else if (LV >= 2 && left >= 2) {
             lv = 2;
-            fold_pass<NW, (LV >= 2 ? 2 : 1)>(A, B, dst, d, p, K, g, T, wv, lane);
+            fold_pass<NW, (LV >= 2 ? 2 : 1), IP>(A, B, side, dst, d, p, K, g, T, wv, lane);
         } else {
-            fold_pass<NW, 1>(A, B, dst, d, p, K, g, T, wv, lane);
+            fold_pass<NW, 1, IP>(A, B, side, dst, d, p, K, g, T, wv, lane);
         }
         g += lv;
         if (g < K) {
             __syncthreads();
-            u32* t = A;
-            A = B;
-            B = t;
+            if constexpr (!IP) {
+                u32* t = A;
+                A = B;
+                B = t;
+            }
         }
     }
 }
@@ -750,7 +778,10 @@ int tile_levels(u32 flags) { return (flags & STEP_TILE_L4) ? 4 : ((flags & STEP_
 // LDS rows of a tile with `rows` output rows at depth k: double-buffered, two copies of the tile
 // (+4 rows of over-read slack); in place, one copy plus NW private side rows per wave.
 i64 tile_lds_rows(i64 rows, int k, int nw, u32 flags) {
-    if (flags & STEP_TILE_FOLD) return 2 * (i64)fold_buffer_rows((int)(rows + 2 * (i64)k));
+    if (flags & STEP_TILE_FOLD)
+        return (flags & STEP_TILE_INPLACE)
+                   ? (i64)fold_buffer_rows((int)(rows + 2 * (i64)k)) + (i64)nw * tile_side_rows(tile_levels(flags))
+                   : 2 * (i64)fold_buffer_rows((int)(rows + 2 * (i64)k));
     if (flags & STEP_TILE_INPLACE) return rows + 2 * (i64)k + (i64)nw * tile_side_rows(tile_levels(flags));
     return 2 * (rows + 2 * (i64)k) + 4;
 }
@@ -766,13 +797,17 @@ const void* tile_kernel_ip(u32 flags) {
         return (flags & STEP_WRAP_Y) ? (const void*)step_tile<NW, true, 2, IP> : (const void*)step_tile<NW, false, 2, IP>;
     return (flags & STEP_WRAP_Y) ? (const void*)step_tile<NW, true, 1, IP> : (const void*)step_tile<NW, false, 1, IP>;
 }
+template <int NW, bool IP>
+const void* tile_kernel_fold_ip(u32 flags) {
+    if (flags & STEP_TILE_L4)
+        return (flags & STEP_WRAP_Y) ? (const void*)step_tile_fold<NW, true, 4, IP> : (const void*)step_tile_fold<NW, false, 4, IP>;
+    if (flags & STEP_TILE_L2)
+        return (flags & STEP_WRAP_Y) ? (const void*)step_tile_fold<NW, true, 2, IP> : (const void*)step_tile_fold<NW, false, 2, IP>;
+    return (flags & STEP_WRAP_Y) ? (const void*)step_tile_fold<NW, true, 1, IP> : (const void*)step_tile_fold<NW, false, 1, IP>;
+}
 template <int NW>
 const void* tile_kernel_fold(u32 flags) {
-    if (flags & STEP_TILE_L4)
-        return (flags & STEP_WRAP_Y) ? (const void*)step_tile_fold<NW, true, 4> : (const void*)step_tile_fold<NW, false, 4>;
-    if (flags & STEP_TILE_L2)
-        return (flags & STEP_WRAP_Y) ? (const void*)step_tile_fold<NW, true, 2> : (const void*)step_tile_fold<NW, false, 2>;
-    return (flags & STEP_WRAP_Y) ? (const void*)step_tile_fold<NW, true, 1> : (const void*)step_tile_fold<NW, false, 1>;
+    return (flags & STEP_TILE_INPLACE) ? tile_kernel_fold_ip<NW, true>(flags) : tile_kernel_fold_ip<NW, false>(flags);
 }
 template <int NW>
 const void* tile_kernel(u32 flags) {
@@ -899,7 +934,10 @@ void launch_step(int k, const u64* src, u64* dst, const LaneDesc* plan, i64 n_wa
 
 i64 tile_max_rows(int k, int nw_per_wg, u32 flags) {
     const i64 lds_rows = kMaxLdsBytes / (kTileRowU32 * 4);  // 320 rows of 512 B
-    if (flags & STEP_TILE_FOLD) return 2 * (lds_rows / 2 - kFoldMirror - 4) - 1 - 2 * (i64)k;
+    if (flags & STEP_TILE_FOLD)  // rows + 2k = T with ceil(T/2) + 8 rows per buffer
+        return (flags & STEP_TILE_INPLACE)
+                   ? 2 * (lds_rows - (i64)nw_per_wg * tile_side_rows(tile_levels(flags)) - kFoldMirror - 4) - 1 - 2 * (i64)k
+                   : 2 * (lds_rows / 2 - kFoldMirror - 4) - 1 - 2 * (i64)k;
     if (flags & STEP_TILE_INPLACE) return lds_rows - (i64)nw_per_wg * tile_side_rows(tile_levels(flags)) - 2 * (i64)k;
     return (lds_rows - 4) / 2 - 2 * (i64)k;
 }

@@ -287,6 +287,18 @@ def test_tile_fold(gol, monkeypatch, fold, N, depth, tile_waves):
     assert np.array_equal(s.board(), numpy_step(initial_board(5, N, 1, True, N + depth), gens))
 
 
+@pytest.mark.parametrize("N,depth,tile_waves", [(2048, 24, 8), (1100, 9, 16)])
+def test_tile_fold_inplace(gol, monkeypatch, N, depth, tile_waves):
+    """Folded tiles updated in place (GOL_TILE_FOLD=1, GOL_TILE_INPLACE=1: side-row copies, mirrored
+    middle rows read from the copy) vs numpy."""
+    monkeypatch.setenv("GOL_TILE_FOLD", "1")
+    monkeypatch.setenv("GOL_TILE_INPLACE", "1")
+    gens = 2 * depth + 5
+    s = _sim(gol, N, halo_depth=depth, kernel_depth=depth, kernel="tile", tile_waves=tile_waves).init(5, seed=N)
+    s.step(gens)
+    assert np.array_equal(s.board(), numpy_step(initial_board(5, N, 1, True, N), gens))
+
+
 @pytest.mark.parametrize("fold", ["0", "1"])
 def test_tile_fold_split_ghost_rows(gol, monkeypatch, fold):
     """Folded tiles in the split schedule (interior and boundary regions, ghost rows, no y-wrap)."""
