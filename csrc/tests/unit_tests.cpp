@@ -140,6 +140,35 @@ static void test_plan() {
             CHECK(!validate_plan(lanes, nw, h, R - 1, k, false).empty());  // one row too deep
         }
     }
+    // folded-tile plans: 32-lane tiles (<= 30 output words + 2 halo lanes), lanes 32-63 repeat lanes
+    // 0-31, every output word stored by exactly one lane of the first halves
+    for (i64 nw : {1, 29, 30, 31, 128, 130}) {
+        for (bool xwrap : {false, true}) {
+            const i64 h = 300;
+            PlanStats st;
+            auto lanes = build_plan({{0, h, 0, nw}}, nw, h, 139, 24, xwrap, &st, 1, 8, true);
+            CHECK(validate_plan(lanes, nw, h, 24, 24, false).empty());
+            std::vector<int> cover((size_t)(h * nw), 0);
+            bool dup = true;
+            for (size_t w = 0; w < lanes.size() / 64; ++w) {
+                int run = 0;
+                for (int l = 0; l < 32; ++l) {
+                    const LaneDesc& d = lanes[w * 64 + l];
+                    const LaneDesc& e = lanes[w * 64 + 32 + l];
+                    dup &= d.row0 == e.row0 && d.col == e.col && d.flags == e.flags && d.nrows == e.nrows;
+                    run = (d.flags & LANE_STORE) ? run + 1 : 0;
+                    CHECK(run <= 30);
+                    if (d.flags & LANE_STORE)
+                        for (int r = 0; r < d.nrows; ++r) cover[(size_t)((d.row0 + r) * nw + d.col)]++;
+                }
+            }
+            CHECK(dup);
+            bool all1 = true;
+            for (int c : cover) all1 &= c == 1;
+            CHECK(all1);
+            CHECK(st.out_words == h * nw);
+        }
+    }
     // a corrupted lane is reported
     auto lanes = build_plan({{0, 10, 0, 5}}, 5, 10, 10, 1, false);
     lanes[3].col = 9;
