@@ -185,9 +185,10 @@ def test_threads_per_block_selects_tile_workgroup(gol_bin, tmp_path, threads, wa
 def test_perf_smoke_8192(gol_bin, tmp_path):
     """SURVEY §4.3 perf smoke: 8192^2 x 1000 generations through the CLI, cell-updates/s above a floor.
 
-    Measured 4.3-4.6e13/s on one MI355X (profiles/baseline_configs_1gpu.txt); the floor (3e13) catches
-    a fallback to a slow path (the yardstick byte kernel runs at ≈4e11) and a regression of a third in
-    the tile kernel or its autotune."""
+    Measured 4.8-4.9e13/s on one MI355X with folded tiles (profiles/tile_fold_ab.txt; 4.3-4.7e13 with
+    plain tiles across boxes); the floor (4e13) catches a fallback to a slow path (the yardstick byte
+    kernel runs at ≈4e11), the loss of the folded tiles' autotune choice beyond box noise, and any
+    larger regression of the tile kernel."""
     import re
 
     r = _run(gol_bin, [5, 8192, 1000, 512, 0], tmp_path, 1)
@@ -196,4 +197,4 @@ def test_perf_smoke_8192(gol_bin, tmp_path):
     assert m, r.stdout
     secs, updates = float(m.group(1)), int(m.group(2))
     assert updates == 8192 * 8192 * 1000
-    assert updates / secs > 3e13, f"{updates / secs:.3e} cell-updates/s"
+    assert updates / secs > 4e13, f"{updates / secs:.3e} cell-updates/s"
