@@ -242,6 +242,13 @@ void HipEngine::do_init(const PatternSpec& p) {
     for (const auto& kv : sched_us_)
         tn += strprintf("%ssched:%s=%.3fus/gen", tn.empty() ? "" : " ", kv.first.c_str(), kv.second);
     for (const auto& kv : pass_us_) tn += strprintf("%spass%d=%.1fus", tn.empty() ? "" : " ", kv.first, kv.second);
+    if (!split_ && !dual_ && tile_kernel(0) && kernel_ != "lds") {  // the tile variant the full superstep runs
+        const DevPlan& p0 = plan(0, kdepth_, 0);
+        tn += strprintf("%stile_plan=%s,%lldrows,%lldtiles", tn.empty() ? "" : " ",
+                        p0.fold ? ((p0.tflags & hipk::STEP_TILE_INPLACE) ? "fold-inplace" : "fold")
+                                : ((p0.tflags & hipk::STEP_TILE_INPLACE) ? "inplace" : "double"),
+                        (long long)p0.rows, (long long)p0.waves);
+    }
     stats_.tuning = tn;
     // Build the plans of the supersteps the runs will use now (the full superstep and the
     // remainder of the hinted run length), so neither graph capture nor a hinted timed loop

@@ -283,6 +283,7 @@ def test_tile_fold(gol, monkeypatch, fold, N, depth, tile_waves):
     monkeypatch.setenv("GOL_TILE_FOLD", fold)
     gens = 2 * depth + 3
     s = _sim(gol, N, halo_depth=depth, kernel_depth=depth, kernel="tile", tile_waves=tile_waves).init(5, seed=N + depth)
+    assert ("tile_plan=fold," in s.stats()["tuning"]) == (fold == "1"), s.stats()["tuning"]
     s.step(gens)
     assert np.array_equal(s.board(), numpy_step(initial_board(5, N, 1, True, N + depth), gens))
 
