@@ -9,16 +9,22 @@ A *step* is one Game of Life generation (B3/S23) over the whole board.  Each ran
 32768 x 32768 tile (weak scaling, the reference's per-rank semantics: gol-main.c:76) — the global
 board is (N*32768) x 32768, a torus, with RCCL halo exchange over xGMI between ranks.  ``--scaling
 strong`` instead splits one 32768^2 board over the N GPUs.  The board is random (pattern 5,
-synthetic), the timed region runs every generation in full: W untimed warmup generations, barrier +
-device sync, K timed generations, device sync + barrier; the max over ranks is reported.  Metric =
-global cells x K / elapsed.  Without a GPU it falls back to the CPU backend on BASELINE config 1
-(256^2).
+synthetic).  The timed region runs every generation in full: W untimed warmup generations, then the
+ranks are aligned (host barrier + a 1-element RCCL all-reduce on the engine's stream, waited for on
+every GPU), K timed generations, device sync; the max over ranks of the per-rank elapsed time is
+reported, with the residual start skew (``start_skew_us``).  Metric = global cells x K / elapsed.
+``--gpus N`` without a launcher (no WORLD_SIZE) starts ``torch.distributed.run`` with N ranks as a
+child process and relays its output (it never measures one GPU in place of N).  A progress watchdog
+(``--watchdog`` seconds) makes every rank exit non-zero if a peer hangs or RCCL fails.  Without a
+GPU it falls back to the CPU backend on BASELINE config 1 (256^2).
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -27,7 +33,7 @@ sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 METRIC = "cell-updates/sec (whole node) on 32768^2 board; 1/2/4/8-GPU weak+strong scaling"
 
 
-def main() -> int:
+def parse_args(argv=None):
     ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=4000, help="timed generations")
@@ -38,7 +44,8 @@ def main() -> int:
     ap.add_argument("--scaling", choices=["weak", "strong"], default="weak")
     ap.add_argument("--decomp", default="1d", help="1d | 2d | auto")
     ap.add_argument("--halo-depth", type=int, default=int(os.environ.get("GOL_HALO_DEPTH", "0")),
-                    help="generations per halo exchange (0 = auto: 32; 128 / 56 for multi-GPU strips / 2-D tiles of >= 2048 rows)")
+                    help="generations per halo exchange (0 = auto: 32 without neighbours; 128 for 1-D strips "
+                         "of >= 2048 rows with neighbours and for sub-tile ranks; 56 for 2-D tiles of >= 2048 rows)")
     ap.add_argument("--kernel-depth", type=int, default=int(os.environ.get("GOL_KERNEL_DEPTH", "0")),
                     help="generations per kernel pass (0 = auto)")
     ap.add_argument("--kernel", default=os.environ.get("GOL_KERNEL", "auto"),
@@ -50,17 +57,50 @@ def main() -> int:
                     help="route the halos of directions whose neighbour is the rank itself through the transport "
                          "(one GPU: a 1-rank RCCL communicator, ncclSend/ncclRecv to itself)")
     ap.add_argument("--allow-host-staging", action="store_true",
-                    help="if RCCL cannot initialise, stage halos through host memory instead of failing")
+                    help="if RCCL cannot initialise (e.g. ranks sharing one GPU in a rehearsal), stage halos "
+                         "through host memory instead of failing")
+    ap.add_argument("--watchdog", type=float, default=float(os.environ.get("GOL_WATCHDOG", "120")),
+                    help="seconds without progress (or an RCCL error) before every rank aborts non-zero (0 = off)")
+    ap.add_argument("--no-phases", action="store_true", help="skip the untimed per-phase probe after the run")
     ap.add_argument("--seed", type=int, default=0x5EED)
-    args = ap.parse_args()
+    return ap.parse_args(argv)
+
+
+def _free_port() -> int:
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_children(args) -> int:
+    """``--gpus N`` (N > 1) without a launcher: run this script under torch.distributed.run, N ranks,
+    as a child process (never exec: the parent touches no GPU, but a child keeps the contract simple),
+    and relay its exit code.  The ranks print the JSON line themselves (rank 0)."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__)] + sys.argv[1:]
+    print(f"[bench] --gpus {args.gpus} without a launcher: running {' '.join(cmd[1:6])} ... as a child",
+          file=sys.stderr, flush=True)
+    env = dict(os.environ)
+    env.setdefault("MASTER_ADDR", "127.0.0.1")
+    return subprocess.run(cmd, env=env).returncode
+
+
+def main() -> int:
+    args = parse_args()
+    # Decided before anything touches the GPU (importing the package does not; hip_device_count does).
+    world_env = os.environ.get("WORLD_SIZE")
+    if world_env is None and args.gpus > 1:
+        return launch_children(args)
+    world = int(world_env or "1")
+    if world != args.gpus:
+        print(f"[bench] error: --gpus {args.gpus} but the launcher started WORLD_SIZE={world} ranks",
+              file=sys.stderr, flush=True)
+        return 2
 
     import gol_amd
     from gol_amd.parallel import init_distributed, rccl_transport, torch_transport
 
     native = gol_amd.native
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    if world != args.gpus and world > 1:
-        print(f"[bench] warning: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
     have_gpu = native.hip_device_count() > 0
     backend = "hip" if have_gpu else "cpu"
     size, steps, warmup = args.size, args.steps, args.warmup
@@ -87,8 +127,9 @@ def main() -> int:
             elif not args.allow_host_staging:
                 # a multi-GPU number measured over host-staged halos is not the RCCL/xGMI design
                 if rank == 0:
-                    print("[bench] RCCL unavailable on some rank: refusing to measure host-staged halos "
-                          "(pass --allow-host-staging to do so)", file=sys.stderr, flush=True)
+                    print(json.dumps({"metric": METRIC, "value": None, "unit": "cell-updates/s", "n_gpus": P,
+                                      "error": "RCCL unavailable on some rank; refusing to measure host-staged "
+                                               "halos (pass --allow-host-staging to do so)"}), flush=True)
                 return 3
             elif rank == 0:
                 print("[bench] using host-staged halos on every rank", file=sys.stderr, flush=True)
@@ -99,6 +140,7 @@ def main() -> int:
     else:
         transport = native.SelfTransport()
 
+    t_init = time.perf_counter()
     sim = gol_amd.Simulation(
         size,
         transport,
@@ -114,8 +156,17 @@ def main() -> int:
         run_hint=steps,  # the timed run replays one captured graph (graph boundaries idle the GPU)
         self_exchange=args.self_exchange,
         width=args.width if have_gpu else 0,
+        watchdog=args.watchdog,
     )
     sim.init(pattern=5, seed=args.seed)
+    my_init = time.perf_counter() - t_init
+    init_s = transport.allreduce_max(my_init)
+    init_per_rank = [round(my_init, 3)]
+    if P > 1:
+        import torch.distributed as dist
+
+        init_per_rank = [None] * P
+        dist.all_gather_object(init_per_rank, round(my_init, 3), group=cpu_group)
     dec = sim.decomposition
     cells = dec.H * dec.W
 
@@ -124,7 +175,7 @@ def main() -> int:
     use_torch_sync = backend == "hip" and torch.cuda.is_available()
 
     def device_sync():
-        sim.synchronize()  # the engine's own HIP streams
+        sim.synchronize()  # the engine's own HIP streams (watchdog-armed)
         if use_torch_sync:
             torch.cuda.synchronize()
 
@@ -133,16 +184,29 @@ def main() -> int:
     device_sync()
     sim.step(warmup)
     device_sync()
-    transport.barrier()
+    sim.engine.device_barrier()  # host barrier + RCCL all-reduce completed on every GPU
     t0 = time.perf_counter()
     sim.step(steps)
     device_sync()
     t1 = time.perf_counter()
-    transport.barrier()
     elapsed = transport.allreduce_max(t1 - t0)
+    # perf_counter is CLOCK_MONOTONIC: comparable across the processes of one node
+    start_skew = transport.allreduce_max(t0) - transport.allreduce_min(t0)
+    span = transport.allreduce_max(t1) - transport.allreduce_min(t0)
+    transport.barrier()
     pop = sim.population()
     st = sim.stats()
     halo_bytes = transport.allreduce_sum(int(st["halo_bytes"]))  # all ranks, init + warmup + timed
+    k_timed = st["depth"] if steps >= st["depth"] else steps
+    phases = None
+    if backend == "hip" and not args.no_phases:
+        ph = sim.engine.phase_probe(min(steps, st["depth"]))
+        phases = {"superstep_gens": int(ph.get("superstep_gens", k_timed)),
+                  "timed_supersteps": -(-steps // max(1, int(ph.get("superstep_gens", k_timed))))}
+        for key in ("exchange_us", "superstep_us"):
+            if key in ph:
+                phases[key + "_max"] = round(transport.allreduce_max(ph[key]), 2)
+                phases[key + "_min"] = round(transport.allreduce_min(ph[key]), 2)
 
     yard = None
     if args.yardstick and rank == 0 and have_gpu:
@@ -189,7 +253,17 @@ def main() -> int:
                 "self_exchange": bool(args.self_exchange),
                 "halo_exchanges_rank0": st["exchanges"],
                 "halo_bytes_all_ranks": halo_bytes,
+                "watchdog_s": args.watchdog,
             },
+            "timing": {
+                "per_rank_elapsed_max_us": round(elapsed * 1e6, 2),
+                "start_skew_us": round(start_skew * 1e6, 2),
+                "span_us": round(span * 1e6, 2),
+                "init_s": round(init_s, 3),
+                "init_s_per_rank": init_per_rank,
+            },
+            "start_skew_us": round(start_skew * 1e6, 2),
+            "phases": phases,
             "baseline_note": "reference publishes no numbers (BASELINE.md); vs_baseline is null",
         }
         if yard:

@@ -17,6 +17,7 @@
 #pragma once
 
 #include <algorithm>
+#include <map>
 #include <memory>
 #include <string>
 #include <utility>
@@ -57,11 +58,15 @@ struct EngineConfig {
                                       // 2 on, 0 off, -1 auto = on for tiles of >= kSubtileMinRows rows)
     u64 run_hint = 0;                 // generations of the runs to come (CLI: iterations); the HIP
                                       // engine captures one graph covering them (<= 256 supersteps)
-    bool graph_rccl = false;          // also capture supersteps whose exchange is an RCCL group
-    int subtile_overlap = 0;          // sub-tiles with neighbours: half 0 starts its first pass (all but
+    int graph_rccl = -1;              // one-tile supersteps whose exchange is an RCCL group, captured in
+                                      // hipGraphs (GOL_GRAPH_RCCL: 1 on, 0 off, -1 = a candidate of the
+                                      // init-time schedule timing, "full+graph")
+    int subtile_graphs = -1;          // sub-tile passes replayed from per-half hipGraphs (GOL_SUBTILE_GRAPHS:
+                                      // 1 on, 0 off, -1 = a timed candidate, "subtiles+graph")
+    int subtile_overlap = -1;         // sub-tiles with neighbours: half 0 starts its first pass (all but
                                       // its band next to the rank's north halo) while the exchange is in
-                                      // flight (GOL_SUBTILE_OVERLAP: 1 on, 0 off (default: measured slower
-                                      // through RCCL self-exchange), -1 = a candidate of the init timing)
+                                      // flight (GOL_SUBTILE_OVERLAP: 1 on, 0 off, -1 = a candidate of the
+                                      // init-time schedule timing, "subtiles+ov")
     int sub_occ = 2;                  // sub-tile plans: waves per SIMD each half is sized for (GOL_SUB_OCC;
                                       // 0 = the single-tile tuned occupancy)
     bool self_exchange = false;       // GOL_SELF_EXCHANGE: directions whose neighbour is this rank go
@@ -108,6 +113,18 @@ class Engine {
     // Global values (collective over the transport).
     u64 population();
     u64 fingerprint();
+    // Collective: align the ranks right before a timed region.  Host barrier; with a device
+    // transport also a 1-element all-reduce on the compute stream, waited for, so every rank leaves
+    // when the collective has completed on the GPUs, not when a host barrier happened to release it.
+    virtual void device_barrier() { t_->barrier(); }
+    // Collective, untimed: per-phase GPU costs of a k-generation superstep of the schedule in use, in
+    // us: "exchange_us" (the halo exchange alone, when there is one) and "superstep_us" (a whole
+    // superstep, exchange included), each the best of a few rounds.  Runs on scratch state: the
+    // board and the generation count are unchanged.  Empty on backends without a GPU clock.
+    virtual std::map<std::string, double> phase_probe(int k) {
+        (void)k;
+        return {};
+    }
 
     const Geometry& geometry() const { return g_; }
     const Layout& layout() const { return L_; }
@@ -162,12 +179,19 @@ class Engine {
     virtual int superstep_depth() const { return L_.R; }
     void setup_compat();
     void maybe_inject_fault();
-    // Watchdog mode: wait until earlier work has completed (bounded lookahead), polling the
-    // transport's asynchronous error state; then kick the watchdog.  No-op without a watchdog.
+    // Watchdog mode: a superstep (or graph replay) has been issued: record its progress marker
+    // (backend hook) and kick the watchdog.  No-op without a watchdog.
     void progress(const char* next_phase);
-    virtual void fence() {}
+    virtual void note_progress() {}
+    // Watchdog probe, run on the watchdog thread (watchdog.hpp): GPU progress markers retired so far,
+    // outstanding GPU work, and the data plane's asynchronous error state.
+    virtual Watchdog::Probe probe() {
+        Watchdog::Probe p;
+        p.error = t_->async_error();
+        return p;
+    }
     [[noreturn]] void fatal(const std::string& what, int code);
-    struct Armed {  // arms the watchdog (if any) for the lifetime of a run() call
+    struct Armed {  // arms the watchdog (if any) for the lifetime of a run() / init() / synchronize() call
         explicit Armed(Watchdog* w) : w_(w) {
             if (w_) w_->arm(true);
         }

@@ -70,6 +70,13 @@ class Transport {
     // Ranks of the device data plane's communicator as the library reports them (RCCL:
     // ncclCommCount); -1 for host transports.
     virtual int data_plane_ranks() { return -1; }
+    // Device transports: enqueue a collective on `stream` (a hipStream_t) that completes on every
+    // rank's GPU only once every rank has reached it (RCCL: a 1-element all-reduce).  Used to align
+    // the ranks' timed regions on the GPUs themselves; host transports need nothing beyond barrier().
+    virtual void device_barrier(void* stream) { (void)stream; }
+    // Whether exchange() may be captured into a hipGraph (RCCL: its kernels become graph nodes; the
+    // thread-rank emulation rendezvous across streams of several threads and cannot be captured).
+    virtual bool graph_capturable() const { return false; }
 };
 
 // P = 1.

@@ -203,6 +203,7 @@ PYBIND11_MODULE(_gol, m) {
         .def("data_plane_ranks", &Transport::data_plane_ranks)
         .def("barrier", &Transport::barrier, py::call_guard<py::gil_scoped_release>())
         .def("allreduce_max", &Transport::allreduce_max, py::call_guard<py::gil_scoped_release>())
+        .def("allreduce_min", &Transport::allreduce_min, py::call_guard<py::gil_scoped_release>())
         .def("allreduce_sum", &Transport::allreduce_sum, py::call_guard<py::gil_scoped_release>());
     py::class_<SelfTransport, Transport, std::shared_ptr<SelfTransport>>(m, "SelfTransport").def(py::init<>());
     py::class_<ThreadTransport, Transport, std::shared_ptr<ThreadTransport>>(m, "ThreadTransport");
@@ -262,6 +263,7 @@ PYBIND11_MODULE(_gol, m) {
         .def_readwrite("sched", &EngineConfig::sched)
         .def_readwrite("kernel_depth", &EngineConfig::kernel_depth)
         .def_readwrite("graph_rccl", &EngineConfig::graph_rccl)
+        .def_readwrite("subtile_graphs", &EngineConfig::subtile_graphs)
         .def_readwrite("plan_xcds", &EngineConfig::plan_xcds);
 
     py::class_<Engine>(m, "Engine")
@@ -293,6 +295,8 @@ PYBIND11_MODULE(_gol, m) {
         .def("local_reduce", &Engine::local_reduce, py::call_guard<py::gil_scoped_release>())
         .def("population", &Engine::population, py::call_guard<py::gil_scoped_release>())
         .def("fingerprint", &Engine::fingerprint, py::call_guard<py::gil_scoped_release>())
+        .def("device_barrier", &Engine::device_barrier, py::call_guard<py::gil_scoped_release>())
+        .def("phase_probe", &Engine::phase_probe, py::arg("k"), py::call_guard<py::gil_scoped_release>())
         .def_property_readonly("geometry", &Engine::geometry)
         .def_property_readonly("layout", &Engine::layout)
         .def_property_readonly("generation", &Engine::generation)

@@ -28,6 +28,7 @@ class RcclTransport : public Transport {
     }
     ~RcclTransport() override {
         if (comm_) ncclCommDestroy(comm_);
+        if (dbuf_) (void)hipFree(dbuf_);
     }
     int rank() const override { return ctl_->rank(); }
     int size() const override { return ctl_->size(); }
@@ -35,6 +36,7 @@ class RcclTransport : public Transport {
     void send_bytes(int peer, const void* buf, size_t n) override { ctl_->send_bytes(peer, buf, n); }
     void recv_bytes(int peer, void* buf, size_t n) override { ctl_->recv_bytes(peer, buf, n); }
     bool device_buffers() const override { return true; }
+    bool graph_capturable() const override { return true; }
 
     void exchange(const std::vector<Message>& sends, const std::vector<Message>& recvs, void* stream) override {
         // Canonical order: sends[i] and recvs[i] belong to the same direction; RCCL matches
@@ -71,6 +73,13 @@ class RcclTransport : public Transport {
         if (comm_ && ncclCommCount(comm_, &n) != ncclSuccess) return -1;
         return n;
     }
+    void device_barrier(void* stream) override {
+        if (!dbuf_) {
+            const hipError_t e = hipMalloc(&dbuf_, sizeof(float) * 2);  // on the current (engine's) device
+            if (e != hipSuccess) throw Error(strprintf("device_barrier: hipMalloc: %s", hipGetErrorString(e)));
+        }
+        nccl_check(ncclAllReduce(dbuf_, dbuf_, 1, ncclFloat32, ncclSum, comm_, (hipStream_t)stream), "ncclAllReduce");
+    }
     std::string async_error() override {
         if (!comm_) return "";
         ncclResult_t st = ncclSuccess;
@@ -88,6 +97,7 @@ class RcclTransport : public Transport {
    private:
     std::shared_ptr<Transport> ctl_;
     ncclComm_t comm_ = nullptr;
+    void* dbuf_ = nullptr;  // device_barrier's all-reduce operand
 };
 
 }  // namespace

@@ -39,15 +39,15 @@ Engine::Engine(const Geometry& g, const EngineConfig& c, std::shared_ptr<Transpo
     const bool tall_strips = nbrs && !two_d() && strip_rows >= 2048;
     const bool tall_tiles = nbrs && two_d() && strip_rows >= 2048;
     // ... and 128 when the two-sub-tile mode can run (HIP, GOL_SUBTILES auto or 2, 1-D tiles of >=
-    // 24576 rows, aligned width, no measurement / watchdog / compat mode, and a transport whose
-    // exchange it can drive): its halves wait for each other once per superstep (a kernel trace
+    // 24576 rows, aligned width, no measurement / compat mode; any transport: device transports
+    // run the halves' exchange stream ordered, host transports stage it): its halves wait for each
+    // other once per superstep (a kernel trace
     // showed ~47 us of one queue and ~12 us of both idle at every boundary), so longer supersteps
     // pay that less often: 32768^2, 2048 generations, 10.01-10.05 us/gen at 64, 9.94-9.98 at 96,
     // 9.70-9.79 at 128 (profiles/subtile_superstep_boundaries.txt).  Rank-invariant inputs only.
-    const bool sub_transport = cfg_.transport != "host" && (g_.dec.P == 1 || t_->device_buffers());
     const bool sub_tall = cfg_.backend == "hip" && (cfg_.subtiles == 2 || cfg_.subtiles < 0) && !two_d() && strip_rows >= kSubtileMinRows &&
-                          g_.dec.W % 64 == 0 && !cfg_.force_split && !cfg_.profile && cfg_.watchdog_s <= 0 &&
-                          !cfg_.compat && cfg_.kernel != "lds" && cfg_.kernel != "tile" && sub_transport;
+                          g_.dec.W % 64 == 0 && !cfg_.force_split && !cfg_.profile && !cfg_.compat &&
+                          cfg_.kernel != "lds" && cfg_.kernel != "tile";
     // (1-D strips with neighbours: 128 measured 1-3% faster than 64 through RCCL self-exchange,
     // 4096 x 32768 2.44 -> 2.36, 8192 x 65536 5.93 -> 5.85 us/gen; profiles/per_rank_tiles_self_exchange.txt)
     const int want = cfg_.halo_depth > 0 ? cfg_.halo_depth : (sub_tall || tall_strips ? 128 : (tall_tiles ? 56 : 32));
@@ -73,22 +73,33 @@ Engine::Engine(const Geometry& g, const EngineConfig& c, std::shared_ptr<Transpo
         }
     }
     if (cfg_.watchdog_s > 0) {
-        wd_ = std::make_unique<Watchdog>(cfg_.watchdog_s, [this](const std::string& what) {
-            fatal("watchdog: " + what, 4);
-        });
+        // (the probe is a virtual call on the watchdog thread: it is enabled at the end of init(),
+        // once the backend is fully constructed, and backends stop the watchdog first on destruction)
+        wd_ = std::make_unique<Watchdog>(
+            cfg_.watchdog_s, [this](const std::string& what) { fatal("watchdog: " + what, 4); },
+            [this] { return probe(); });
     }
 }
 
 void Engine::fatal(const std::string& what, int code) {
     fprintf(stderr, "[gol] rank %d, generation %llu: %s; aborting the job\n", g_.rank, (unsigned long long)gen_,
             what.c_str());
+    fflush(stderr);
+    // The transport's abort (ncclCommAbort, MPI_Abort, socket teardown) must not be able to hang
+    // the exit: a last-resort timer ends the process regardless.
+    std::thread([code] {
+        std::this_thread::sleep_for(std::chrono::seconds(15));
+        fprintf(stderr, "[gol] transport abort did not return within 15 s; exiting\n");
+        fflush(stderr);
+        _exit(code);
+    }).detach();
     t_->abort(code);
     _exit(code);  // not reached: Transport::abort does not return
 }
 
 void Engine::progress(const char* next_phase) {
     if (!wd_) return;
-    fence();
+    note_progress();
     wd_->kick(next_phase);
 }
 
@@ -138,6 +149,7 @@ std::vector<Engine::HaloItem> Engine::halo_items(int k) const {
 
 void Engine::init(const PatternSpec& p) {
     trace::Range range("gol.init");
+    Armed armed(wd_.get());
     gen_ = 0;
     stats_ = EngineStats{};
     stats_.depth = L_.R;
@@ -146,6 +158,7 @@ void Engine::init(const PatternSpec& p) {
     stats_.kernel_depth = L_.R;
     do_init(p);
     if (cfg_.compat) setup_compat();
+    if (wd_) wd_->enable_probe();
 }
 
 void Engine::setup_compat() {

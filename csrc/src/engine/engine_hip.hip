@@ -98,9 +98,66 @@ HipEngine::HipEngine(const Geometry& g, const EngineConfig& c, std::shared_ptr<T
     }
     HIP_CHECK(hipMalloc(&d_red_, 2 * sizeof(u64)));
     HIP_CHECK(hipHostMalloc(&h_red_, 2 * sizeof(u64), hipHostMallocDefault));
+    if (wd_)
+        for (auto& m : mk_)
+            for (auto& e : m.ev) HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+}
+
+HipEngine::Marker& HipEngine::marker_slot() {
+    for (;;) {
+        {
+            std::lock_guard<std::mutex> lk(mk_mu_);
+            std::string err;
+            if (!retire_markers_locked(&err)) throw Error("progress marker: " + err);
+            if (mk_count_ < kMarkers) return mk_[(mk_head_ + mk_count_) % kMarkers];
+        }
+        // every marker in flight: the host is kMarkers supersteps ahead of the GPU
+        std::this_thread::sleep_for(std::chrono::microseconds(50));
+    }
+}
+
+bool HipEngine::retire_markers_locked(std::string* err) {
+    while (mk_count_ > 0) {
+        const Marker& m = mk_[mk_head_];
+        for (int i = 0; i < m.n; ++i) {
+            const hipError_t q = hipEventQuery(m.ev[i]);
+            if (q == hipErrorNotReady) return true;
+            if (q != hipSuccess) {
+                *err = strprintf("hipEventQuery: %s", hipGetErrorString(q));
+                return false;
+            }
+        }
+        mk_head_ = (mk_head_ + 1) % kMarkers;
+        --mk_count_;
+        ++mk_done_;
+    }
+    return true;
+}
+
+void HipEngine::note_progress() {
+    if (mk_published_) {  // the sub-tile superstep published its own end-of-superstep events
+        mk_published_ = false;
+        return;
+    }
+    Marker& m = marker_slot();
+    HIP_CHECK(hipEventRecord(m.ev[0], s_comp_));
+    m.n = 1;
+    publish_marker();
+}
+
+Watchdog::Probe HipEngine::probe() {
+    Watchdog::Probe p;
+    p.error = t_->async_error();
+    std::lock_guard<std::mutex> lk(mk_mu_);
+    std::string err;
+    if (!retire_markers_locked(&err) && p.error.empty()) p.error = err;
+    p.completed = mk_done_;
+    p.pending = mk_count_ > 0;
+    return p;
 }
 
 HipEngine::~HipEngine() {
+    wd_.reset();  // its thread calls probe(), which reads the members destroyed below
     hipStreamSynchronize(s_comp_);
     hipStreamSynchronize(s_comm_);
     destroy_dual_graphs();
@@ -108,8 +165,8 @@ HipEngine::~HipEngine() {
     for (auto& sb : sub_buf_)
         for (u64* b : sb)
             if (b) hipFree(b);
-    if (ev_sub_a_) hipEventDestroy(ev_sub_a_);
-    if (ev_sub_b_) hipEventDestroy(ev_sub_b_);
+    for (auto e : ev_sub_own_)
+        if (e) hipEventDestroy(e);
     if (ev_sub_x_) hipEventDestroy(ev_sub_x_);
     for (auto& kv : graphs_) hipGraphExecDestroy(kv.second);
     for (auto& kv : plans_) hipFree(kv.second.d);
@@ -119,7 +176,7 @@ HipEngine::~HipEngine() {
     }
     for (auto& v : {&dstage_s_, &dstage_r_})
         for (u64* p : *v) hipFree(p);
-    for (auto& v : {&hstage_s_, &hstage_r_})
+    for (auto& v : {&hstage_s_, &hstage_r_, &xhs_, &xhr_})
         for (u64* p : *v) hipHostFree(p);
     for (int i = 0; i < 2; ++i) hipFree(buf_[i]);
     for (void* p : deferred_free_) hipFree(p);
@@ -127,10 +184,9 @@ HipEngine::~HipEngine() {
     hipHostFree(h_red_);
     hipEventDestroy(ev_ready_);
     hipEventDestroy(ev_halo_);
-    for (auto e : fence_ev_)
-        if (e) hipEventDestroy(e);
-    for (auto e : {ev_sync_comm_, ev_sync_comp_})
-        if (e) hipEventDestroy(e);
+    for (auto& m : mk_)
+        for (auto e : m.ev)
+            if (e) hipEventDestroy(e);
     if (cfg_.profile)
         for (auto e : {ev_t0_, ev_t1_, ev_t2_, ev_t3_}) hipEventDestroy(e);
     hipStreamDestroy(s_comp_);
@@ -219,9 +275,16 @@ void HipEngine::do_init(const PatternSpec& p) {
     synchronize();
     if (dcells) deferred_free_.push_back(dcells);  // hipFree may synchronise the whole device
     if (!tuned_) {
+        auto kick = [this](const char* phase) {
+            if (wd_) wd_->kick(phase);
+        };
+        kick("init: kernel autotune");
         if (cfg_.kernel == "auto") autotune_kernel();
+        kick("init: schedule timing");
         choose_schedule();  // collective when ranks have neighbours
+        kick("init: pass costs");
         measure_pass_costs();
+        kick("init: plans and graphs");
         tuned_ = true;
         passes_.clear();  // the pass cuts may depend on the tuned kernel (pass_depths)
         // The comm stream waits on the compute stream's ready event only in the split

@@ -18,9 +18,10 @@ bool HipEngine::graph_shape(int& k, int& m) {
     m += m & 1;  // even: the graph returns to the same buffer parity
     bool local = cfg_.compat || halo_items(k).empty();
     if (!local && !device_transport_) return false;  // host-staged exchange cannot be captured
-    // RCCL inside captured graphs is opt-in: with R-deep supersteps (hundreds of us each) the
-    // eager launch cost is negligible, and an eager exchange keeps RCCL's own error handling.
-    if (!local && !cfg_.graph_rccl) return false;
+    // RCCL inside captured graphs: a candidate of the schedule timing ("full+graph", choose_schedule)
+    // or forced with GOL_GRAPH_RCCL=1; eager otherwise (an eager exchange keeps RCCL's own error
+    // handling, and with R-deep supersteps the eager launch cost is small).
+    if (!local && !graph_rccl_on_) return false;
     return true;
 }
 

@@ -18,10 +18,11 @@ void HipEngine::setup_dual() {
             HIP_CHECK(hipMemsetAsync(sub_buf_[s][i], 0, bytes, s_comp_));
         }
     }
-    if (!ev_sub_a_) {
-        HIP_CHECK(hipEventCreateWithFlags(&ev_sub_a_, hipEventDisableTiming));
-        HIP_CHECK(hipEventCreateWithFlags(&ev_sub_b_, hipEventDisableTiming));
+    if (!ev_sub_own_[0]) {
+        for (auto& e : ev_sub_own_) HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
         HIP_CHECK(hipEventCreateWithFlags(&ev_sub_x_, hipEventDisableTiming));
+        ev_sub_a_ = ev_sub_own_[0];
+        ev_sub_b_ = ev_sub_own_[1];
     }
     HIP_CHECK(hipStreamSynchronize(s_comp_));
 }
@@ -85,7 +86,6 @@ void HipEngine::dual_superstep(int k) {
     prepare_dual(k);
     const int p = sub_cur_;
     const int a = (p + 1) % 3, b = (p + 2) % 3;  // the passes alternate a, b, a, ... (never p)
-    const i64 h1 = sub_L_[1].h;
     wait_pending(s_comp_, ev_sub_b_);  // half 1's previous superstep is done
     hipGraphExec_t gx[2] = {dual_graph(0, p, k), dual_graph(1, p, k)};
     const bool graphs = gx[0] && gx[1];
@@ -104,13 +104,9 @@ void HipEngine::dual_superstep(int k) {
             wait_pending(s_comm_, ev_sub_a_);  // the exchange sends half 0's edge and writes its halo
             xs = s_comm_;
         }
-        // the one-tile engine's canonical messages (Engine::halo_items, 1-D): N then S
         std::vector<Message> sends, recvs;
-        sends.push_back({g_.nbr[DIR_N], sub_rows(0, p, 0), rows_bytes(0, k)});
-        recvs.push_back({g_.nbr[DIR_S], sub_rows(1, p, h1), rows_bytes(1, k)});
-        sends.push_back({g_.nbr[DIR_S], sub_rows(1, p, h1 - k), rows_bytes(1, k)});
-        recvs.push_back({g_.nbr[DIR_N], sub_rows(0, p, -k), rows_bytes(0, k)});
-        t_->exchange(sends, recvs, (void*)xs);
+        dual_messages(p, k, sends, recvs);
+        exchange_rows(sends, recvs, xs);
         stats_.exchanges += 1;
         stats_.halo_bytes += (u64)(rows_bytes(0, k) + rows_bytes(1, k));
         // (full: also implies half 0's previous superstep, which ran on the same stream)
@@ -135,10 +131,74 @@ void HipEngine::dual_superstep(int k) {
             for (int s = 0; s < 2; ++s)
                 if (!(ov && s == 0 && j == 0)) launch_half(s, p, k, s ? s_comm_ : s_comp_, j);
     }
+    if (wd_) {
+        // with a watchdog the end-of-superstep events are the superstep's progress marker (a fresh
+        // pair from the marker ring; ev_sub_a_ / ev_sub_b_ always name the latest pair)
+        Marker& m = marker_slot();
+        ev_sub_a_ = m.ev[0];
+        ev_sub_b_ = m.ev[1];
+        m.n = 2;
+    }
     HIP_CHECK(hipEventRecord(ev_sub_a_, s_comp_));
     HIP_CHECK(hipEventRecord(ev_sub_b_, s_comm_));
+    if (wd_) {
+        publish_marker();
+        mk_published_ = true;
+    }
     HIP_CHECK(hipGetLastError());
     sub_cur_ = (pass_depths(k).size() % 2) ? a : b;
+}
+
+// The one-tile engine's canonical messages (Engine::halo_items, 1-D): N then S, from / into the
+// halves' buffer p.
+void HipEngine::dual_messages(int p, int k, std::vector<Message>& sends, std::vector<Message>& recvs) {
+    const i64 h1 = sub_L_[1].h;
+    sends.push_back({g_.nbr[DIR_N], sub_rows(0, p, 0), rows_bytes(0, k)});
+    recvs.push_back({g_.nbr[DIR_S], sub_rows(1, p, h1), rows_bytes(1, k)});
+    sends.push_back({g_.nbr[DIR_S], sub_rows(1, p, h1 - k), rows_bytes(1, k)});
+    recvs.push_back({g_.nbr[DIR_N], sub_rows(0, p, -k), rows_bytes(0, k)});
+}
+
+// Device transports (RCCL) are stream ordered on `s`.  Host transports are staged through pinned
+// host memory and block: the rows to send are complete once `s` has drained (the caller orders both
+// halves' previous superstep before `s`), the receives land on `s`.
+void HipEngine::exchange_rows(const std::vector<Message>& sends, const std::vector<Message>& recvs, hipStream_t s) {
+    if (device_transport_) {
+        t_->exchange(sends, recvs, (void*)s);
+        return;
+    }
+    trace::Range r("gol.exchange_staged");
+    size_t need = 0;
+    for (const auto* v : {&sends, &recvs})
+        for (const Message& m : *v) need = std::max(need, m.bytes);
+    if (xhs_.size() < sends.size() || xhr_.size() < recvs.size() || need > xh_bytes_) {
+        HIP_CHECK(hipStreamSynchronize(s));
+        for (auto* v : {&xhs_, &xhr_}) {
+            for (u64* q : *v) HIP_CHECK(hipHostFree(q));
+            v->clear();
+        }
+        xh_bytes_ = std::max(need, (size_t)rows_bytes(0, L_.R));
+        for (size_t i = 0; i < sends.size(); ++i) {
+            u64* q = nullptr;
+            HIP_CHECK(hipHostMalloc(&q, xh_bytes_, hipHostMallocDefault));
+            xhs_.push_back(q);
+        }
+        for (size_t i = 0; i < recvs.size(); ++i) {
+            u64* q = nullptr;
+            HIP_CHECK(hipHostMalloc(&q, xh_bytes_, hipHostMallocDefault));
+            xhr_.push_back(q);
+        }
+    }
+    std::vector<Message> hs, hr;
+    for (size_t i = 0; i < sends.size(); ++i) {
+        HIP_CHECK(hipMemcpyAsync(xhs_[i], sends[i].buf, sends[i].bytes, hipMemcpyDeviceToHost, s));
+        hs.push_back({sends[i].peer, xhs_[i], sends[i].bytes});
+    }
+    for (size_t i = 0; i < recvs.size(); ++i) hr.push_back({recvs[i].peer, xhr_[i], recvs[i].bytes});
+    HIP_CHECK(hipStreamSynchronize(s));
+    t_->exchange_host(hs, hr);
+    for (size_t i = 0; i < recvs.size(); ++i)
+        HIP_CHECK(hipMemcpyAsync(recvs[i].buf, xhr_[i], recvs[i].bytes, hipMemcpyHostToDevice, s));
 }
 
 // The kernel passes of half s in a superstep of k generations that starts from buffer p (only

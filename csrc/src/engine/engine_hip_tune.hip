@@ -99,7 +99,13 @@ void HipEngine::choose_schedule() {
     } else {
         cands.push_back(nbrs ? "full" : "local");
         if (cfg_.sched == "auto" && split_used()) cands.push_back("split");
+        // the one-tile superstep with its RCCL group captured in a graph (one replay per run)
+        if (nbrs && device_transport_ && t_->graph_capturable() && cfg_.graph && !cfg_.profile && !cfg_.compat &&
+            cfg_.graph_rccl < 0)
+            cands.push_back("full+graph");
     }
+    graph_rccl_on_ = cfg_.graph_rccl == 1;
+    sub_graphs_on_ = cfg_.subtile_graphs == 1;
     bool dual_ok = cfg_.subtiles != 0 && cands[0] != "split" && dual_wanted();
     if (dual_ok) {
         double ok = dual_local_ok() ? 1.0 : 0.0;
@@ -111,27 +117,38 @@ void HipEngine::choose_schedule() {
         std::vector<std::string> dc;
         if (cfg_.subtile_overlap <= 0 || self_y()) dc.push_back("subtiles");
         if (cfg_.subtile_overlap != 0 && !self_y()) dc.push_back("subtiles+ov");
+        if (cfg_.subtile_graphs < 0 && cfg_.graph && !cfg_.profile) dc.push_back("subtiles+graph");
         if (cfg_.subtiles == 2) cands.clear();
         cands.insert(cands.end(), dc.begin(), dc.end());
     }
     std::string pick = cands[0];
     if (cands.size() > 1) {
-        const int k = L_.R;
+        // Supersteps of the length the runs will use: kSchedReps back-to-back R-generation supersteps,
+        // or, when the hinted run is shorter than R (the driver's 20-generation bench is a single
+        // 20-generation superstep), that one superstep started from an idle GPU, as the run will
+        // be: its launch latency, exchange and drain weigh more there, and the candidates are
+        // within a few % of each other, so it gets more rounds.
+        const bool short_run = cfg_.run_hint > 0 && cfg_.run_hint < (u64)L_.R;
+        const int k = short_run ? supported_depth((int)cfg_.run_hint) : L_.R;
+        const int reps = short_run ? 1 : kSchedReps;
+        const int rounds = short_run ? 9 : 3;
         std::vector<double> best(cands.size(), 1e30);
         spin_up();
-        for (int round = 0; round < 3; ++round)
+        for (int round = 0; round < rounds; ++round)
             for (size_t c = 0; c < cands.size(); ++c) {
-                if (round == 0) time_schedule(cands[c], k, 1);  // warm-up: connections, plans
+                if (round == 0) time_schedule(cands[c], k, reps);  // warm-up: connections, plans, graphs
                 synchronize();
                 t_->barrier();
                 const auto t0 = std::chrono::steady_clock::now();
-                time_schedule(cands[c], k, kSchedReps);
+                time_schedule(cands[c], k, reps);
                 synchronize();
                 const double dt = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
-                best[c] = std::min(best[c], t_->allreduce_max(dt) * 1e6 / (kSchedReps * k));
+                best[c] = std::min(best[c], t_->allreduce_max(dt) * 1e6 / (reps * k));
             }
+        const bool graph_failed = t_->allreduce_max(sched_graph_failed_ ? 1.0 : 0.0) > 0;
         size_t bi = 0;
         for (size_t c = 0; c < cands.size(); ++c) {
+            if (graph_failed && cands[c] == "full+graph") best[c] = 1e30;
             sched_us_[cands[c]] = best[c];
             if (best[c] < best[bi]) bi = c;
         }
@@ -145,12 +162,21 @@ void HipEngine::choose_schedule() {
                 if (cands[c] != "split" && (b2 == cands.size() || best[c] < best[b2])) b2 = c;
             pick = cands[b2];
         }
-        stats_.exchanges = 0;  // the timing exchanges are not part of the run
+        stats_.exchanges = 0;  // the timing exchanges and replays are not part of the run
         stats_.halo_bytes = 0;
+        stats_.graph_launches = 0;
+    }
+    if (sched_graph_) {  // (it captured the communicator: destroy it before the comm can go)
+        HIP_CHECK(hipStreamSynchronize(s_comp_));
+        HIP_CHECK(hipGraphExecDestroy(sched_graph_));
+        sched_graph_ = nullptr;
     }
     split_ = pick == "split";
     dual_ = pick.rfind("subtiles", 0) == 0;
     sub_overlap_ = pick == "subtiles+ov";
+    graph_rccl_on_ = cfg_.graph_rccl == 1 || pick == "full+graph";
+    sub_graphs_on_ = cfg_.subtile_graphs == 1 || pick == "subtiles+graph";
+    if (!sub_graphs_on_) destroy_dual_graphs();
     if (dual_) {
         setup_dual();
         sub_current_ = false;  // the halves hold timing scratch: load the board at the next run
@@ -161,13 +187,61 @@ void HipEngine::choose_schedule() {
 }
 
 // `reps` supersteps of k generations of schedule `c` on scratch state (see choose_schedule).
-void HipEngine::time_schedule(const std::string& c, int k, int reps) {
+void HipEngine::time_schedule(const std::string& c, int k, int reps, bool eager) {
     if (c.rfind("subtiles", 0) == 0) {
         setup_dual();
         dual_ = true;
         sub_overlap_ = c == "subtiles+ov";
+        const bool sg = sub_graphs_on_;
+        sub_graphs_on_ = c == "subtiles+graph" || cfg_.subtile_graphs == 1;
+        if (sub_graphs_on_) {
+            prepare_dual(k);
+            capture_dual_graphs(k);  // once per (half, start buffer, depth)
+        }
         for (int i = 0; i < reps; ++i) dual_superstep(k);
         dual_ = sub_overlap_ = false;
+        sub_graphs_on_ = sg;
+        return;
+    }
+    // One-tile supersteps as the runs replay them (graphs: "local" always, "full+graph" candidate):
+    // `reps` supersteps captured once (round 0's warm-up call, after one eager superstep that loads
+    // every kernel variant), one replay per call.
+    const bool graphed =
+        !eager && (c == "full+graph" || (c == "local" && cfg_.graph && !cfg_.profile && !cfg_.compat && graph_ok_));
+    if (graphed) {
+        const std::string base = c == "local" ? "local" : "full";
+        if (sched_graph_ && sched_graph_reps_ != reps) {
+            HIP_CHECK(hipStreamSynchronize(s_comp_));
+            HIP_CHECK(hipGraphExecDestroy(sched_graph_));
+            sched_graph_ = nullptr;
+        }
+        if (!sched_graph_ && !sched_graph_failed_) {
+            prepare(k);
+            time_schedule(base, k, 1, true);
+            HIP_CHECK(hipStreamSynchronize(s_comp_));
+            hipGraph_t graph = nullptr;
+            try {
+                HIP_CHECK(hipStreamBeginCapture(s_comp_, hipStreamCaptureModeRelaxed));
+                time_schedule(base, k, reps, true);
+                HIP_CHECK(hipStreamEndCapture(s_comp_, &graph));
+                HIP_CHECK(hipGraphInstantiate(&sched_graph_, graph, nullptr, nullptr, 0));
+                HIP_CHECK(hipGraphDestroy(graph));
+                HIP_CHECK(hipGraphUpload(sched_graph_, s_comp_));
+            } catch (const Error& e) {
+                hipGraph_t g2 = nullptr;
+                hipStreamEndCapture(s_comp_, &g2);
+                if (g2) hipGraphDestroy(g2);
+                hipGetLastError();
+                sched_graph_ = nullptr;
+                sched_graph_failed_ = true;  // the candidate is dropped (agreed over the ranks)
+                fprintf(stderr, "[gol] rank %d: schedule graph capture failed: %s\n", g_.rank, e.what());
+            }
+            sched_graph_reps_ = reps;
+        }
+        if (sched_graph_)
+            HIP_CHECK(hipGraphLaunch(sched_graph_, s_comp_));
+        else
+            time_schedule(base, k, reps, true);  // the same exchanges as the peers' replays
         return;
     }
     split_ = c == "split";
@@ -304,6 +378,92 @@ void HipEngine::autotune_kernel() {
     HIP_CHECK(hipEventDestroy(e0));
     HIP_CHECK(hipEventDestroy(e1));
     kernel_ = kern_[0];
+}
+
+void HipEngine::device_barrier() {
+    synchronize();
+    t_->barrier();
+    if (device_transport_) {
+        t_->device_barrier((void*)s_comp_);
+        Armed armed(wd_.get());
+        HIP_CHECK(hipStreamSynchronize(s_comp_));
+    }
+}
+
+// Per-phase costs for the scaling model (docs/PERFORMANCE.md): the exchange of a k-deep halo alone,
+// and whole k-generation supersteps of the chosen schedule, timed with events on scratch state
+// (time_schedule) after the board has been synchronised back to the canonical buffer.  Collective:
+// every rank runs the same exchanges; rounds start from a host barrier.
+std::map<std::string, double> HipEngine::phase_probe(int k) {
+    Armed armed(wd_.get());
+    std::map<std::string, double> out;
+    k = supported_depth(std::max(1, std::min(k, superstep_depth())));
+    sync_canonical();
+    synchronize();
+    const EngineStats saved = stats_;
+    const bool was_dual = dual_, was_ov = sub_overlap_, was_split = split_;
+    hipEvent_t e0, e1;
+    HIP_CHECK(hipEventCreate(&e0));
+    HIP_CHECK(hipEventCreate(&e1));
+    auto elapsed_us = [&] {
+        HIP_CHECK(hipEventSynchronize(e1));
+        float ms = 0;
+        HIP_CHECK(hipEventElapsedTime(&ms, e0, e1));
+        return (double)ms * 1e3;
+    };
+    const bool xchg = dual_ ? !self_y() : !items_for(k).empty();
+    if (xchg) {
+        if (!dual_) prepare(k);
+        double best = 1e30;
+        for (int round = 0; round < 4; ++round) {
+            t_->barrier();
+            HIP_CHECK(hipEventRecord(e0, s_comp_));
+            if (dual_) {
+                std::vector<Message> sends, recvs;
+                dual_messages(sub_cur_, k, sends, recvs);
+                exchange_rows(sends, recvs, s_comp_);
+            } else if (device_transport_) {
+                exchange_device(k, items_for(k), cur_, s_comp_);
+            } else {
+                exchange_staged(k, items_for(k), cur_, s_comp_);
+            }
+            HIP_CHECK(hipEventRecord(e1, s_comp_));
+            const double us = elapsed_us();
+            if (round > 0) best = std::min(best, us);  // round 0 warms the connections up
+        }
+        out["exchange_us"] = best;
+    }
+    const std::string sched = dual_ ? (sub_overlap_ ? "subtiles+ov" : "subtiles")
+                                    : (split_ ? "split" : (halo_items(L_.R).empty() ? "local" : "full"));
+    const int reps = 2;
+    double best = 1e30;
+    for (int round = 0; round < 3; ++round) {
+        t_->barrier();
+        HIP_CHECK(hipEventRecord(e0, s_comp_));
+        if (was_dual) HIP_CHECK(hipStreamWaitEvent(s_comm_, e0, 0));
+        time_schedule(sched, k, reps);
+        if (was_dual) HIP_CHECK(hipStreamWaitEvent(s_comp_, ev_sub_b_, 0));
+        HIP_CHECK(hipEventRecord(e1, s_comp_));
+        best = std::min(best, elapsed_us() / reps);
+    }
+    out["superstep_us"] = best;
+    out["superstep_gens"] = k;
+    synchronize();
+    if (sched_graph_) {
+        HIP_CHECK(hipGraphExecDestroy(sched_graph_));
+        sched_graph_ = nullptr;
+    }
+    HIP_CHECK(hipEventDestroy(e0));
+    HIP_CHECK(hipEventDestroy(e1));
+    dual_ = was_dual;
+    sub_overlap_ = was_ov;
+    split_ = was_split;
+    if (dual_) {
+        sub_current_ = false;  // the halves hold probe scratch: reload the board at the next run
+        canon_stale_ = false;
+    }
+    stats_ = saved;  // the probe's exchanges and supersteps are not part of any run
+    return out;
 }
 
 }  // namespace hipeng

@@ -16,6 +16,7 @@
 #include <chrono>
 #include <cstring>
 #include <map>
+#include <mutex>
 #include <thread>
 
 #include "gol/bits.hpp"
@@ -75,19 +76,11 @@ class HipEngine : public Engine {
     std::string backend_name() const override { return "hip"; }
 
     void synchronize() override {
-        if (wd_) {  // poll instead of blocking, so asynchronous transport errors surface
-            HIP_CHECK(hipEventRecord(ev_sync_comm_ ? ev_sync_comm_ : make_sync_events(), s_comm_));
-            HIP_CHECK(hipEventRecord(ev_sync_comp_, s_comp_));
-            wait_watched(ev_sync_comm_);
-            wait_watched(ev_sync_comp_);
-        }
+        // (blocking: with a watchdog, its thread polls the GPU progress markers and the transport's
+        // asynchronous error state meanwhile, and aborts the job if either stalls or fails)
+        Armed armed(wd_.get());
         HIP_CHECK(hipStreamSynchronize(s_comm_));
         HIP_CHECK(hipStreamSynchronize(s_comp_));
-    }
-    hipEvent_t make_sync_events() {
-        HIP_CHECK(hipEventCreateWithFlags(&ev_sync_comm_, hipEventDisableTiming));
-        HIP_CHECK(hipEventCreateWithFlags(&ev_sync_comp_, hipEventDisableTiming));
-        return ev_sync_comm_;
     }
 
     std::vector<u64> tile_words() override;
@@ -134,6 +127,9 @@ class HipEngine : public Engine {
 
     void run(u64 generations) override;
 
+    void device_barrier() override;
+    std::map<std::string, double> phase_probe(int k) override;
+
     // ----- two sub-tiles per rank (1-D) -----
     // The tile's rows are split into two halves, each with THREE buffers of R ghost rows, each
     // running a superstep's passes on its own stream with a plan sized for the whole GPU.  The two
@@ -154,8 +150,8 @@ class HipEngine : public Engine {
     bool dual_wanted() const {
         const bool want = cfg_.subtiles == 2 ||
                           (cfg_.subtiles < 0 && g_.dec.H / std::max(1, g_.dec.Py) >= kSubtileMinRows && L_.R >= 64);
-        return want && !two_d() && !cfg_.compat && !cfg_.profile && !cfg_.force_split && !wd_ && L_.aligned() &&
-               (halo_items(L_.R).empty() || device_transport_) && cfg_.kernel != "lds" && cfg_.kernel != "tile";
+        return want && !two_d() && !cfg_.compat && !cfg_.profile && !cfg_.force_split && L_.aligned() &&
+               cfg_.kernel != "lds" && cfg_.kernel != "tile";
     }
     // Rank-local conditions (agreed over the ranks by the caller): a tile tall enough for two
     // halves, and memory for one more board pair.  (The halves always run the temporal kernel, at
@@ -218,15 +214,18 @@ class HipEngine : public Engine {
     }
 
     void dual_superstep(int k);
+    void dual_messages(int p, int k, std::vector<Message>& sends, std::vector<Message>& recvs);
+    void exchange_rows(const std::vector<Message>& sends, const std::vector<Message>& recvs, hipStream_t s);
 
     void launch_half(int s, int p, int k, hipStream_t st, int only = -1, int part = 0);
 
     // Graph of launch_half(s, p, k): captured at init only (capture_dual_graphs), nullptr otherwise.
-    // Opt-in (GOL_SUBTILE_GRAPHS=1): replayed per half and superstep, these measured slower than the
-    // eager launches on MI355X / ROCm 7.2 (32768^2, same box, alternating: 20 generations 13.06-13.23
-    // vs 12.75-12.96 us/gen, 2000 generations 10.35 vs 10.24; profiles/subtile_graphs_ab.txt), as did
-    // one graph of both halves with fork/join events (see graph_shape).
-    bool dual_graphs_on() const { return cfg_.graph && !cfg_.profile && graph_ok_ && env_int("GOL_SUBTILE_GRAPHS", 0) != 0; }
+    // A candidate of the schedule timing ("subtiles+graph"; GOL_SUBTILE_GRAPHS=1 forces it): replayed
+    // per half and superstep, these measured slower than the eager launches in round 2 on MI355X /
+    // ROCm 7.2 (32768^2, same box, alternating: 20 generations 13.06-13.23 vs 12.75-12.96 us/gen, 2000
+    // generations 10.35 vs 10.24; profiles/subtile_graphs_ab.txt), as did one graph of both halves
+    // with fork/join events (see graph_shape), so the node they run on decides.
+    bool dual_graphs_on() const { return cfg_.graph && !cfg_.profile && graph_ok_ && sub_graphs_on_; }
     hipGraphExec_t dual_graph(int s, int p, int k) {
         if (!dual_graphs_on()) return nullptr;
         auto it = dual_graphs_.find((s * 3 + p) * 1000 + k);
@@ -308,7 +307,8 @@ class HipEngine : public Engine {
     static constexpr int kSchedReps = 4;
     void choose_schedule();
 
-    void time_schedule(const std::string& c, int k, int reps);
+    // (eager: the one-tile candidates without their graph replay; used to capture those graphs)
+    void time_schedule(const std::string& c, int k, int reps, bool eager = false);
 
     void do_set_compat_halos(const std::vector<u64>& above, const std::vector<u64>& below) override;
 
@@ -424,30 +424,27 @@ class HipEngine : public Engine {
     i64 graph_key(int k, int m, int rem) const { return (((i64)k * 1000 + m) * 1000 + rem) * 2 + par(); }
     hipGraphExec_t graph_for(int k, int m, int rem);
 
-    // ----- watchdog support -----
-    // Wait for `ev` without blocking in the driver, so a stuck or failed exchange is noticed: the
-    // transport's asynchronous error state is polled while waiting.
-    void wait_watched(hipEvent_t ev) {
-        for (;;) {
-            const hipError_t e = hipEventQuery(ev);
-            if (e == hipSuccess) return;
-            if (e != hipErrorNotReady) HIP_CHECK(e);
-            const std::string ae = t_->async_error();
-            if (!ae.empty()) fatal(ae, 5);
-            std::this_thread::sleep_for(std::chrono::microseconds(50));
-        }
+    // ----- watchdog support: progress markers -----
+    // With a watchdog, every superstep (or graph replay) publishes a marker: HIP events recorded at
+    // its end on the streams it used.  The watchdog thread retires completed markers (probe), so GPU
+    // progress is observed without the host ever waiting on the GPU; the host waits only when all
+    // kMarkers markers are in flight (bounded lookahead).  The sub-tile path publishes its
+    // end-of-superstep events (ev_sub_a_/ev_sub_b_, recorded anyway) as the marker: no extra event
+    // records on the hot path.
+    static constexpr int kMarkers = 64;
+    struct Marker {
+        hipEvent_t ev[2] = {nullptr, nullptr};
+        int n = 0;  // events recorded for this marker
+    };
+    Marker& marker_slot();  // the next free slot (waits for the oldest marker when all are in flight)
+    void publish_marker() {
+        std::lock_guard<std::mutex> lk(mk_mu_);
+        ++mk_count_;
     }
-    // Bounded lookahead: the host runs at most kFenceDepth units (supersteps or graph launches)
-    // ahead of the GPU, so watchdog kicks track completed GPU work.
-    static constexpr int kFenceDepth = 4;
-    void fence() override {
-        if (!fence_ev_[0])
-            for (auto& e : fence_ev_) HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-        HIP_CHECK(hipEventRecord(fence_ev_[fence_i_], s_comp_));
-        fence_used_[fence_i_] = true;
-        fence_i_ = (fence_i_ + 1) % kFenceDepth;
-        if (fence_used_[fence_i_]) wait_watched(fence_ev_[fence_i_]);
-    }
+    // retire the completed markers at the head of the ring (mk_mu_ held); false on a HIP error
+    bool retire_markers_locked(std::string* err);
+    void note_progress() override;
+    Watchdog::Probe probe() override;
 
     int dev_ = 0, cus_ = 256;
     std::string kernel_;  // resolved kernel: temporal | tile | lds (auto resolves at init)
@@ -469,10 +466,11 @@ class HipEngine : public Engine {
     std::map<int, double> pass_us_;           // measure_pass_costs: us per pass by depth (chosen mode)
     bool tuned_ = false;
     std::map<std::string, float> tune_ms_;
-    hipEvent_t fence_ev_[kFenceDepth] = {};
-    hipEvent_t ev_sync_comm_ = nullptr, ev_sync_comp_ = nullptr;
-    bool fence_used_[kFenceDepth] = {};
-    int fence_i_ = 0;
+    Marker mk_[kMarkers];
+    int mk_head_ = 0, mk_count_ = 0;  // published, unretired markers: mk_[mk_head_ ..] (under mk_mu_)
+    unsigned long long mk_done_ = 0;  // markers retired so far
+    std::mutex mk_mu_;
+    bool mk_published_ = false;  // this superstep's marker is already published (sub-tile path)
     u64* buf_[2] = {nullptr, nullptr};
     size_t alloc_bytes_ = 0;
     int cur_ = 0;
@@ -483,6 +481,11 @@ class HipEngine : public Engine {
     u64* h_red_ = nullptr;
     bool device_transport_ = false;
     bool graph_ok_ = true;
+    bool graph_rccl_on_ = false;  // one-tile supersteps with an RCCL exchange are captured (choose_schedule)
+    bool sub_graphs_on_ = false;  // sub-tile passes replay per-half graphs (choose_schedule)
+    hipGraphExec_t sched_graph_ = nullptr;  // the "full+graph" candidate's timing graph (choose_schedule)
+    bool sched_graph_failed_ = false;
+    int sched_graph_reps_ = 0;
     bool events_needed_ = true;  // another stream waits on ev_ready_
     std::vector<void*> deferred_free_;
     std::map<i64, DevPlan> plans_;
@@ -498,11 +501,15 @@ class HipEngine : public Engine {
     std::map<int, DevPlan> sub_plans_;
     std::map<int, hipGraphExec_t> dual_graphs_;  // (half, start buffer, depth) -> launch_half graph
     hipEvent_t ev_sub_a_ = nullptr, ev_sub_b_ = nullptr;  // half 0 / half 1 done with its last superstep
+                                                           // (ev_sub_own_, or a progress marker's pair)
+    hipEvent_t ev_sub_own_[2] = {nullptr, nullptr};
     hipEvent_t ev_sub_x_ = nullptr;                        // the rank's exchange (into both halves) done
     std::map<int, DevCopies> copies_;
     std::map<int, std::vector<HaloItem>> items_;
     std::map<i64, hipGraphExec_t> graphs_;
     std::vector<u64*> dstage_s_, dstage_r_, hstage_s_, hstage_r_;
+    std::vector<u64*> xhs_, xhr_;  // sub-tile host staging (exchange_rows), xh_bytes_ each
+    size_t xh_bytes_ = 0;
 };
 
 }  // namespace hipeng

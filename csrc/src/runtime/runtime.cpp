@@ -173,10 +173,14 @@ EngineConfig engine_config(const Options& o, const std::string& backend, int dev
     c.subtiles = env_str("GOL_SUBTILES", "auto") == "auto" ? -1 : (int)env_int("GOL_SUBTILES", 0);
     c.watchdog_s = o.watchdog_s;
     c.sub_occ = (int)env_int("GOL_SUB_OCC", 2);
-    c.subtile_overlap = env_str("GOL_SUBTILE_OVERLAP", "0") == "auto" ? -1 : (int)env_int("GOL_SUBTILE_OVERLAP", 0);
+    auto tri = [](const char* name) {  // 0 off, 1 on, auto (default) -1: a timed candidate
+        return env_str(name, "auto") == "auto" ? -1 : (int)(env_int(name, 0) != 0);
+    };
+    c.subtile_overlap = tri("GOL_SUBTILE_OVERLAP");
+    c.subtile_graphs = tri("GOL_SUBTILE_GRAPHS");
     c.self_exchange = env_int("GOL_SELF_EXCHANGE", 0) != 0;
     c.force_split = env_int("GOL_FORCE_SPLIT", 0) != 0;
-    c.graph_rccl = env_int("GOL_GRAPH_RCCL", 0) != 0;
+    c.graph_rccl = tri("GOL_GRAPH_RCCL");
     c.plan_xcds = (int)env_int("GOL_PLAN_XCDS", 8);
     c.sched = env_str("GOL_SCHEDULE", "auto");
     if (c.sched != "auto" && c.sched != "split" && c.sched != "full")

@@ -12,8 +12,8 @@ long long now_ns() {
 }
 }  // namespace
 
-Watchdog::Watchdog(double timeout_s, Fire fire)
-    : timeout_s_(timeout_s), fire_(std::move(fire)), last_ns_(now_ns()), phase_("start") {
+Watchdog::Watchdog(double timeout_s, Fire fire, ProbeFn probe)
+    : timeout_s_(timeout_s), fire_(std::move(fire)), probe_(std::move(probe)), last_ns_(now_ns()), phase_("start") {
     if (!(timeout_s_ > 0)) throw Error("watchdog timeout must be positive");
     th_ = std::thread([this] { loop(); });
 }
@@ -39,16 +39,34 @@ void Watchdog::loop() {
     long long tick_ns = limit / 4;
     if (tick_ns < 1000000) tick_ns = 1000000;
     if (tick_ns > 250000000) tick_ns = 250000000;
+    unsigned long long seen = 0;
     std::unique_lock<std::mutex> lk(mu_);
     while (!stop_) {
         cv_.wait_for(lk, std::chrono::nanoseconds(tick_ns));
         if (stop_) break;
-        if (!armed_.load()) continue;
-        const long long idle = now_ns() - last_ns_.load(std::memory_order_relaxed);
-        if (idle > limit) {
-            const char* ph = phase_.load(std::memory_order_relaxed);
-            std::string what = strprintf("no progress for %.1f s (limit %.1f s) in phase '%s'", idle * 1e-9,
-                                         timeout_s_, ph ? ph : "?");
+        Probe pr;
+        if (probe_ && probe_on_.load()) {
+            lk.unlock();
+            pr = probe_();
+            lk.lock();
+            if (stop_) break;
+            if (pr.completed != seen) {  // a GPU marker completed since the last tick
+                seen = pr.completed;
+                last_ns_.store(now_ns(), std::memory_order_relaxed);
+            }
+        }
+        std::string what;
+        if (!pr.error.empty()) {
+            what = pr.error;
+        } else if (armed_.load() > 0 || pr.pending) {
+            const long long idle = now_ns() - last_ns_.load(std::memory_order_relaxed);
+            if (idle > limit) {
+                const char* ph = phase_.load(std::memory_order_relaxed);
+                what = strprintf("no progress for %.1f s (limit %.1f s) in phase '%s'%s", idle * 1e-9, timeout_s_,
+                                 ph ? ph : "?", pr.pending ? ", GPU work outstanding" : "");
+            }
+        }
+        if (!what.empty()) {
             lk.unlock();
             fire_(what);  // normally does not return (aborts the job)
             lk.lock();

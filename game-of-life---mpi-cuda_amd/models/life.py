@@ -41,6 +41,12 @@ class LifeRule:
 CONWAY = LifeRule()
 
 
+def _tri(name: str) -> int:
+    """GOL_* switch with an auto default: 1 on, 0 off, -1 auto (the engine decides by measurement)."""
+    v = os.environ.get(name, "auto")
+    return -1 if v == "auto" else int(int(v) != 0)
+
+
 def default_backend() -> str:
     b = os.environ.get("GOL_BACKEND", "auto")
     if b != "auto":
@@ -96,9 +102,7 @@ class Simulation:
         self_exchange: bool = os.environ.get("GOL_SELF_EXCHANGE", "0") == "1",
         subtiles: int = -1 if os.environ.get("GOL_SUBTILES", "auto") == "auto" else int(os.environ["GOL_SUBTILES"]),
         width: int = 0,
-        subtile_overlap: int = (
-            -1 if os.environ.get("GOL_SUBTILE_OVERLAP", "0") == "auto" else int(os.environ.get("GOL_SUBTILE_OVERLAP", "0"))
-        ),
+        subtile_overlap: Optional[int] = None,
     ):
         self.transport = transport if transport is not None else _gol.SelfTransport()
         P, rank = self.transport.size(), self.transport.rank()
@@ -122,11 +126,13 @@ class Simulation:
         cfg.tile_waves = int(tile_waves)
         cfg.tune_tile_waves = "GOL_TILE_WAVES" not in os.environ
         cfg.sub_occ = int(sub_occ)
-        cfg.subtile_overlap = int(subtile_overlap)  # 1 / 0 / -1 timed: half 0 overlaps the exchange
+        # 1 on / 0 off / -1 auto: a candidate of the init-time schedule timing (GOL_* env defaults)
+        cfg.subtile_overlap = _tri("GOL_SUBTILE_OVERLAP") if subtile_overlap is None else int(subtile_overlap)
         cfg.self_exchange = bool(self_exchange)
         cfg.force_split = bool(force_split)
         cfg.sched = schedule
-        cfg.graph_rccl = os.environ.get("GOL_GRAPH_RCCL", "0") == "1"
+        cfg.graph_rccl = _tri("GOL_GRAPH_RCCL")
+        cfg.subtile_graphs = _tri("GOL_SUBTILE_GRAPHS")
         cfg.plan_xcds = int(os.environ.get("GOL_PLAN_XCDS", "8"))
         if self.backend == "hip":
             n = _gol.hip_device_count()

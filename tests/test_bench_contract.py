@@ -1,11 +1,13 @@
 """bench.py driver contract on CPU: exactly one JSON line from rank 0 with the BASELINE.json metric,
 for a single process and for a 2-rank torch.distributed.run (gloo) launch — the same launch line the
-driver uses on an 8-GPU node."""
+driver uses on an 8-GPU node; ``--gpus N`` without a launcher must start N ranks (never measure one in
+their place); a hung rank must end the whole job non-zero in bounded time (progress watchdog)."""
 import json
 import os
 import socket
 import subprocess
 import sys
+import time
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 KEYS = {"metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
@@ -18,8 +20,10 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _run(cmd):
+def _run(cmd, env_extra=None):
     env = dict(os.environ, OMP_NUM_THREADS="1")
+    env.pop("WORLD_SIZE", None)
+    env.update(env_extra or {})
     r = subprocess.run(cmd, cwd=REPO, env=env, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr[-3000:]
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
@@ -46,3 +50,40 @@ def test_bench_torchrun_two_ranks():
     assert cfg["parallelism"].endswith("p2 (1x2)")
     # weak scaling: every rank owns a full tile, the global board grows with the rank count
     assert cfg["board"][0] == 2 * cfg["tile_per_rank"][0]
+
+
+def test_bench_reports_start_skew():
+    out = _run([sys.executable, "bench.py", "--steps", "20", "--warmup", "2"])
+    assert out["start_skew_us"] >= 0
+    assert out["timing"]["per_rank_elapsed_max_us"] > 0
+
+
+def test_bench_without_launcher_starts_the_ranks():
+    """The driver's --gpus N run, mis-launched as a plain process, still measures N ranks."""
+    out = _run([sys.executable, "bench.py", "--gpus", "2", "--steps", "20", "--warmup", "2"])
+    assert out["config"]["parallelism"].endswith("p2 (1x2)")
+    assert out["config"]["board"][0] == 2 * out["config"]["tile_per_rank"][0]
+
+
+def test_bench_rank_count_mismatch_fails():
+    env = dict(os.environ, OMP_NUM_THREADS="1", WORLD_SIZE="1")
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", "2", "--steps", "4", "--warmup", "1"], cwd=REPO,
+                       env=env, capture_output=True, text=True, timeout=120)
+    assert r.returncode == 2, r.stderr[-2000:]
+    assert not [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+
+
+def test_bench_hung_rank_ends_the_job():
+    """GOL_FAULT hangs rank 1 inside its run: its watchdog aborts it (exit 4) and the launcher ends the
+    job non-zero within a bounded time, instead of the job hanging until the driver's timeout."""
+    env = dict(os.environ, OMP_NUM_THREADS="1", GOL_FAULT="1:10:hang")
+    env.pop("WORLD_SIZE", None)
+    t0 = time.monotonic()
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                        "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), "bench.py", "--gpus", "2",
+                        "--steps", "20", "--warmup", "2", "--watchdog", "3"],
+                       cwd=REPO, env=env, capture_output=True, text=True, timeout=240)
+    dt = time.monotonic() - t0
+    assert r.returncode != 0
+    assert "watchdog" in r.stderr
+    assert dt < 120, dt
