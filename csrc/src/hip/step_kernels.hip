@@ -30,6 +30,8 @@
 // step_lds — single-generation LDS-tiled variant: a 256-thread workgroup stages a (16+2) x (64+2)
 // word tile + ghost ring in LDS and computes 16 x 64 output words.  Kept as a measured alternative.
 #include <mutex>
+#include <set>
+#include <utility>
 
 #include "gol/bits.hpp"
 #include "gol/hip_kernels.hpp"
@@ -945,14 +947,19 @@ i64 tile_max_rows(int k, int nw_per_wg, u32 flags) {
 static const void* tile_kernel_checked(int nw_per_wg, u32 flags) {
     const void* f = tile_kernel_for(nw_per_wg, flags);
     if (!f) throw Error(strprintf("step_tile: unsupported waves per workgroup %d (4, 8 or 16)", nw_per_wg));
-    static bool attr_set[512] = {};
-    const int lvk = (flags & STEP_TILE_L4) ? 2 : ((flags & STEP_TILE_L2) ? 1 : 0);
-    const int key = (((nw_per_wg & 15) * 2 + ((flags & STEP_WRAP_Y) ? 1 : 0)) * 3 + lvk) * 2 +
-                    ((flags & STEP_TILE_INPLACE) ? 1 : 0) + ((flags & STEP_TILE_FOLD) ? 256 : 0);
-    if (!attr_set[key]) {  // allow the full 160 KiB of dynamic LDS
+    // allow the full 160 KiB of dynamic LDS, once per (device, kernel variant): thread-mode ranks on
+    // different GPUs launch concurrently, and the attribute is per device
+    static std::mutex mu;
+    static std::set<std::pair<int, const void*>> attr_set;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) throw Error("step_tile: no current HIP device");
+    std::lock_guard<std::mutex> lk(mu);
+    if (attr_set.insert({dev, f}).second) {
         hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kMaxLdsBytes);
-        if (e != hipSuccess) throw Error(strprintf("step_tile: hipFuncSetAttribute: %s", hipGetErrorString(e)));
-        attr_set[key] = true;
+        if (e != hipSuccess) {
+            attr_set.erase({dev, f});
+            throw Error(strprintf("step_tile: hipFuncSetAttribute: %s", hipGetErrorString(e)));
+        }
     }
     return f;
 }

@@ -324,24 +324,37 @@ void save_checkpoint(Engine& eng, const std::string& prefix, u64 seed) {
     }
     t.broadcast(&ok, 1, 0);
     if (!ok) throw Error("cannot create checkpoint " + tmp);
+    // Every rank writes its own rectangle into rank 0's file, so the file must be on a filesystem
+    // shared by all ranks.  Failures are agreed on collectively (a rank that threw alone would leave
+    // the others blocked in the next collective): every rank throws, or none does.
+    std::string err;
     const int fd = open(tmp.c_str(), O_WRONLY);
-    if (fd < 0) throw Error("cannot open checkpoint " + tmp);
-    const off_t base = (off_t)sizeof(CkptHeader);
-    if (nw == gw) {  // full-width rows: one contiguous write
-        pwrite_all(fd, words.data(), words.size() * 8, base + (off_t)(g.row0 * gw) * 8, tmp);
+    if (fd < 0) {
+        err = strprintf("rank %d cannot open checkpoint %s created by rank 0 (checkpoints need a filesystem shared "
+                        "by all ranks)",
+                        g.rank, tmp.c_str());
     } else {
-        for (i64 r = 0; r < g.h; ++r)
-            pwrite_all(fd, &words[(size_t)(r * nw)], (size_t)nw * 8, base + (off_t)((g.row0 + r) * gw + g.word0()) * 8,
-                       tmp);
-    }
-    if (fsync(fd) != 0) {
+        try {
+            const off_t base = (off_t)sizeof(CkptHeader);
+            if (nw == gw) {  // full-width rows: one contiguous write
+                pwrite_all(fd, words.data(), words.size() * 8, base + (off_t)(g.row0 * gw) * 8, tmp);
+            } else {
+                for (i64 r = 0; r < g.h; ++r)
+                    pwrite_all(fd, &words[(size_t)(r * nw)], (size_t)nw * 8,
+                               base + (off_t)((g.row0 + r) * gw + g.word0()) * 8, tmp);
+            }
+            if (fsync(fd) != 0) throw Error("cannot flush checkpoint " + tmp);
+        } catch (const Error& e) {
+            err = strprintf("rank %d: %s", g.rank, e.what());
+        }
         close(fd);
-        throw Error("cannot flush checkpoint " + tmp);
     }
-    close(fd);
-    t.barrier();
-    if (g.rank == 0 && rename(tmp.c_str(), name.c_str()) != 0) throw Error("cannot rename checkpoint " + tmp);
-    t.barrier();
+    if (t.allreduce_min(err.empty() ? 1.0 : 0.0) <= 0)
+        throw Error(err.empty() ? "checkpoint " + tmp + " failed on another rank" : err);
+    ok = 1;
+    if (g.rank == 0) ok = rename(tmp.c_str(), name.c_str()) == 0;
+    t.broadcast(&ok, 1, 0);
+    if (!ok) throw Error("cannot rename checkpoint " + tmp + " to " + name);
 }
 
 u64 load_checkpoint(Engine& eng, const std::string& prefix) {

@@ -13,5 +13,5 @@ from ._native import _gol as native  # noqa: F401
 
 __version__ = "0.1.0"
 
-from .models import Simulation, LifeRule, CONWAY  # noqa: E402,F401
+from .models import Simulation  # noqa: E402,F401
 from . import models, ops, parallel, utils  # noqa: E402,F401

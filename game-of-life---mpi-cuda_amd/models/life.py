@@ -11,7 +11,6 @@ The heavy lifting is native: :class:`Simulation` drives a ``_gol.Engine`` (HIP o
 """
 from __future__ import annotations
 
-import dataclasses
 import os
 from typing import Optional
 
@@ -19,26 +18,6 @@ import numpy as np
 
 from .._native import _gol
 from ..ops.bitpack import unpack_words
-
-
-@dataclasses.dataclass(frozen=True)
-class LifeRule:
-    """A Life-like rule in B/S notation.  The native kernels implement B3/S23 (Conway)."""
-
-    birth: tuple = (3,)
-    survive: tuple = (2, 3)
-
-    @property
-    def notation(self) -> str:
-        return "B" + "".join(map(str, self.birth)) + "/S" + "".join(map(str, self.survive))
-
-    def apply(self, alive: np.ndarray, neighbours: np.ndarray) -> np.ndarray:
-        born = np.isin(neighbours, self.birth) & ~alive
-        keep = np.isin(neighbours, self.survive) & alive
-        return born | keep
-
-
-CONWAY = LifeRule()
 
 
 def _tri(name: str) -> int:
@@ -63,8 +42,11 @@ class Simulation:
     transport:    a ``_gol.Transport``; defaults to a single-rank transport.  See
                   :mod:`gol_amd.parallel` for torch.distributed / RCCL / thread transports.
     backend:      ``"hip"``, ``"cpu"`` or ``"auto"``.
-    halo_depth:   generations per halo exchange (<= 128 in 1-D, <= 63 in 2-D; 0 = auto: 32, with
-                  neighbours 64 for 1-D strips / 56 for 2-D tiles of >= 2048 rows).
+    halo_depth:   generations per halo exchange (<= 128 in 1-D, <= 63 in 2-D; 0 = auto, as in
+                  Engine::Engine: 128 for 1-D strips of >= 2048 rows with neighbours (or the
+                  self-exchange) and for ranks that can run two sub-tiles, 56 for 2-D tiles of >= 2048
+                  rows with neighbours, otherwise 32).  The rule is B3/S23 (Conway), the only rule
+                  the bit-sliced kernels implement.
     kernel_depth: generations per kernel pass (HIP; 0 = auto).  A superstep of halo_depth
                   generations runs as several kernel passes in 1-D (communication-avoiding halos).
     decomp/grid:  ``"1d"`` row strips (reference) or ``"2d"`` blocks, optional ``"PxxPy"`` grid.
