@@ -6,7 +6,9 @@ namespace hipeng {
 
 void HipEngine::setup_dual() {
     if (sub_buf_[0][0]) return;
-    const i64 h0 = L_.h / 2;
+    // GOL_SUB_SPLIT (per mille, measurement knob): rows of half 0 as a fraction of the tile
+    const i64 frac = std::max<i64>(100, std::min<i64>(900, env_int("GOL_SUB_SPLIT", 500)));
+    const i64 h0 = std::max<i64>(8 * (i64)L_.R, std::min<i64>(L_.h - 8 * (i64)L_.R, L_.h * frac / 1000));
     sub_r0_[0] = 0;
     sub_r0_[1] = h0;
     for (int s = 0; s < 2; ++s) {
@@ -128,8 +130,10 @@ void HipEngine::dual_superstep(int k) {
     } else {
         const int np = (int)pass_depths(k).size();
         for (int j = 0; j < np; ++j)
-            for (int s = 0; s < 2; ++s)
+            for (int i = 0; i < 2; ++i) {
+                const int s = sub_first_ ^ i;  // GOL_SUB_FIRST=1: half 1's pass first (measurement knob)
                 if (!(ov && s == 0 && j == 0)) launch_half(s, p, k, s ? s_comm_ : s_comp_, j);
+            }
     }
     if (wd_) {
         // with a watchdog the end-of-superstep events are the superstep's progress marker (a fresh

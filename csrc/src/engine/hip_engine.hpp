@@ -496,6 +496,7 @@ class HipEngine : public Engine {
     i64 sub_r0_[2] = {0, 0};
     u64* sub_buf_[2][3] = {{nullptr, nullptr, nullptr}, {nullptr, nullptr, nullptr}};
     int sub_cur_ = 0;  // buffer (0..2) holding both halves' current generation
+    int sub_first_ = (int)(env_int("GOL_SUB_FIRST", 0) != 0);  // half whose pass j is launched first
     bool sub_current_ = false;  // the halves hold the current board
     bool canon_stale_ = false;  // buf_[cur_] lags the halves (sync_canonical before reading it)
     std::map<int, DevPlan> sub_plans_;
