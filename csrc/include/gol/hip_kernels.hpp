@@ -76,6 +76,25 @@ i64 tile_max_rows(int k, int nw_per_wg, u32 flags);
 int tile_blocks_per_cu(int nw_per_wg, i64 rows, int k, u32 flags);
 void launch_step_tile(int nw_per_wg, int k, const u64* src, u64* dst, const LaneDesc* plan, i64 n_tiles, i64 rows,
                       const StepParams& p, hipStream_t s);
+// step_resident (resident_kernel.hip): a run of G generations in one launch, one workgroup of `nw`
+// (8, 16) waves per tile of `plan` (one tile per CU, all co-resident), each wave holding B rows of
+// the tile's extended rows (nrows + 2 kmax) in registers; S supersteps (odd) of <= kmax generations,
+// between which tiles exchange halos through HBM with their neighbour tiles (CSR nbr_off / nbr,
+// plan.hpp resident_neighbours) and per-tile counters.  The result is in dst.
+struct ResidentParams {
+    i64 pitch;
+    i32 h;
+    i32 R;
+    i32 G;       // generations of this launch
+    i32 S;       // supersteps (odd), of G / S or G / S + 1 generations
+    i32 kmax;    // halo rows of the tiles: >= ceil(G / S)
+    u64 timeout_ticks;  // bound of every neighbour wait, in s_memrealtime ticks (100 MHz)
+};
+int resident_band_rows(int rows_needed);  // supported band height >= rows_needed (0: none)
+int resident_blocks_per_cu(int nw, int B, bool wrapy);
+void launch_step_resident(int nw, int B, bool wrapy, u64* src, u64* dst, const LaneDesc* plan, i64 n_tiles,
+                          const u32* nbr_off, const u32* nbr, u32* counters, u32* status, const ResidentParams& rp,
+                          hipStream_t s);
 // Single-generation LDS-tiled kernel over output rows [r0, r1) (all words).
 void launch_step_lds(const u64* src, u64* dst, const Layout& L, i64 r0, i64 r1, u32 flags, hipStream_t s);
 

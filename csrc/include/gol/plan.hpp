@@ -87,4 +87,13 @@ i64 choose_rows_per_chunk(const std::vector<Region>& regions, int k, i64 target_
 i64 balanced_rows_per_chunk(const std::vector<Region>& regions, i64 nw, i64 h, int k, i64 resident_waves,
                             i64 min_rows, bool xwrap, bool fold = false);
 
+// Neighbour tiles of a resident plan (hip_kernels.hpp step_resident: one plan wave = one tile, kept
+// by one workgroup for a whole run).  Tile t reads, for each of its lanes, rows [row0-k, row0+nrows+k)
+// of the lane's word column (modulo h with wrap_y); its neighbours are the OTHER tiles whose store
+// lanes own words there.  CSR: idx[off[t] .. off[t+1]).  Returns an empty string, or a description
+// of why the plan cannot run resident (a column not covered exactly once by store lanes, a lane
+// outside [0, nw), a read outside the owned rows without wrap_y).
+std::string resident_neighbours(const std::vector<LaneDesc>& lanes, i64 nw, i64 h, int k, bool wrap_y,
+                                std::vector<u32>& off, std::vector<u32>& idx);
+
 }  // namespace gol

@@ -5,6 +5,8 @@
 #include <cstdlib>
 #include <string>
 #include <map>
+#include <set>
+#include <tuple>
 
 namespace gol {
 
@@ -217,6 +219,78 @@ std::string validate_plan(const std::vector<LaneDesc>& lanes, i64 nw, i64 h, int
                 if (d.row0 < -R || (i64)d.row0 + d.nrows > h + R) return bad("store rows outside [-R, h+R)");
             }
         }
+    }
+    return "";
+}
+
+std::string resident_neighbours(const std::vector<LaneDesc>& lanes, i64 nw, i64 h, int k, bool wrap_y,
+                                std::vector<u32>& off, std::vector<u32>& idx) {
+    if (lanes.size() % kWaveLanes) return "lane count is not a multiple of 64";
+    const size_t nt = lanes.size() / kWaveLanes;
+    // owners of every word column: (first row, end row, tile), sorted by row
+    std::vector<std::vector<std::tuple<i64, i64, u32>>> own((size_t)nw);
+    for (size_t t = 0; t < nt; ++t)
+        for (int l = 0; l < kWaveLanes; ++l) {
+            const LaneDesc& d = lanes[t * kWaveLanes + l];
+            if (d.nrows <= 0) continue;
+            if (d.col < 0 || d.col >= nw) return strprintf("tile %zu lane %d: column %d outside [0, nw)", t, l, d.col);
+            if (d.flags & LANE_STORE) own[(size_t)d.col].emplace_back(d.row0, (i64)d.row0 + d.nrows, (u32)t);
+        }
+    i64 lo_row = 0, hi_row = h;  // rows the store lanes cover (every column alike)
+    for (i64 c = 0; c < nw; ++c) {
+        auto& v = own[(size_t)c];
+        std::sort(v.begin(), v.end());
+        if (v.empty()) return strprintf("column %lld has no store lane", (long long)c);
+        if (c == 0) {
+            lo_row = std::get<0>(v.front());
+            hi_row = std::get<1>(v.back());
+        }
+        if (std::get<0>(v.front()) != lo_row || std::get<1>(v.back()) != hi_row)
+            return strprintf("column %lld covers other rows than column 0", (long long)c);
+        for (size_t i = 1; i < v.size(); ++i)
+            if (std::get<0>(v[i]) != std::get<1>(v[i - 1]))
+                return strprintf("column %lld: rows not covered exactly once", (long long)c);
+    }
+    if (wrap_y && (lo_row != 0 || hi_row != h)) return "wrapped plans must cover rows [0, h)";
+    off.assign(nt + 1, 0);
+    idx.clear();
+    for (size_t t = 0; t < nt; ++t) {
+        std::set<u32> nb;
+        for (int l = 0; l < kWaveLanes; ++l) {
+            const LaneDesc& d = lanes[t * kWaveLanes + l];
+            if (d.nrows <= 0) continue;
+            const auto& v = own[(size_t)d.col];
+            // the lane's input rows, as intervals inside [lo_row, hi_row)
+            std::vector<std::pair<i64, i64>> iv;
+            i64 a = (i64)d.row0 - k, b = (i64)d.row0 + d.nrows + k;
+            if (wrap_y) {
+                if (b - a >= h) {
+                    iv.push_back({0, h});
+                } else {
+                    a = pmod(a, h);
+                    b = a + (b - ((i64)d.row0 - k));
+                    if (b <= h) {
+                        iv.push_back({a, b});
+                    } else {
+                        iv.push_back({a, h});
+                        iv.push_back({0, b - h});
+                    }
+                }
+            } else {
+                // rows beyond the owned range are the rank's ghost rows: read in the first superstep
+                // only (from the exchange) and beyond the valid extension later, owned by no tile
+                iv.push_back({std::max(a, lo_row), std::min(b, hi_row)});
+            }
+            for (const auto& q : iv) {
+                if (q.second <= q.first) continue;
+                auto it = std::upper_bound(v.begin(), v.end(), std::make_tuple(q.first, (i64)1 << 62, (u32)0));
+                if (it != v.begin()) --it;
+                for (; it != v.end() && std::get<0>(*it) < q.second; ++it)
+                    if (std::get<1>(*it) > q.first && std::get<2>(*it) != (u32)t) nb.insert(std::get<2>(*it));
+            }
+        }
+        off[t + 1] = off[t] + (u32)nb.size();
+        idx.insert(idx.end(), nb.begin(), nb.end());
     }
     return "";
 }

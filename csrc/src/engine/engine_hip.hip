@@ -50,11 +50,11 @@ HipEngine::HipEngine(const Geometry& g, const EngineConfig& c, std::shared_ptr<T
         R = K = 1;
     } else if (kernel_ == "tile") {
         K = std::min(K, 32);  // any depth; LDS rows bound it (tile_max_rows)
-    } else if (kernel_ == "temporal" || kernel_ == "auto") {
+    } else if (kernel_ == "temporal" || kernel_ == "auto" || kernel_ == "resident") {
         // auto: the depth must suit both candidates (instantiated temporal depths)
         K = supported_kernel_depth(std::min(K, hipk::max_step_depth()));
     } else {
-        throw Error("GOL_KERNEL must be auto, temporal, tile or lds (got '" + kernel_ + "')");
+        throw Error("GOL_KERNEL must be auto, temporal, tile, lds or resident (got '" + kernel_ + "')");
     }
     if (!multipass_) R = std::min(R, K);
     kdepth_ = K;
@@ -68,7 +68,8 @@ HipEngine::HipEngine(const Geometry& g, const EngineConfig& c, std::shared_ptr<T
     device_transport_ = t_->device_buffers() && cfg_.transport != "host";
     if (cfg_.transport == "device" && !t_->device_buffers())
         throw Error("GOL_TRANSPORT=device needs a device transport (RCCL)");
-    for (auto& kk : kern_) kk = kernel_;
+    for (auto& kk : kern_) kk = kernel_ == "resident" ? "auto" : kernel_;
+    if (kernel_ == "resident") kernel_ = "auto";
     // The two streams must sit on different hardware queues, or their kernels serialise.  HIP
     // multiplexes streams onto GPU_MAX_HW_QUEUES (4) queues, and once an RCCL communicator exists
     // (it creates streams of its own) two plain streams created afterwards were measured to land
@@ -179,6 +180,11 @@ HipEngine::~HipEngine() {
     for (auto& v : {&hstage_s_, &hstage_r_, &xhs_, &xhr_})
         for (u64* p : *v) hipHostFree(p);
     for (int i = 0; i < 2; ++i) hipFree(buf_[i]);
+    for (auto& kv : res_plans_)
+        for (void* q : {(void*)kv.second.d, (void*)kv.second.nbr_off, (void*)kv.second.nbr, (void*)kv.second.counters})
+            if (q) hipFree(q);
+    for (void* q : {(void*)res_status_, (void*)res_scratch_[0], (void*)res_scratch_[1]})
+        if (q) hipFree(q);
     for (void* p : deferred_free_) hipFree(p);
     hipFree(d_red_);
     hipHostFree(h_red_);
@@ -196,6 +202,7 @@ HipEngine::~HipEngine() {
 std::vector<u64> HipEngine::tile_words() {
     sync_canonical();
     synchronize();
+    check_res_status();
     std::vector<u64> d((size_t)(L_.h * L_.nw));
     // stream-ordered (never the legacy null stream: in thread mode another rank's engine may be
     // capturing a graph, and a null-stream copy would have to depend on the capturing stream)
@@ -279,7 +286,7 @@ void HipEngine::do_init(const PatternSpec& p) {
             if (wd_) wd_->kick(phase);
         };
         kick("init: kernel autotune");
-        if (cfg_.kernel == "auto") autotune_kernel();
+        if (cfg_.kernel == "auto" || cfg_.kernel == "resident") autotune_kernel();
         kick("init: schedule timing");
         choose_schedule();  // collective when ranks have neighbours
         kick("init: pass costs");
@@ -296,6 +303,10 @@ void HipEngine::do_init(const PatternSpec& p) {
                          env_str("GOL_READY_EVENTS", "") == "always";
     }
     stats_.kernel = split_ ? kern_[1] + "+boundary:" + kern_[2] : kern_[0];
+    if (res_) {
+        const ResPlan& rp = res_plan(res_kin_);
+        stats_.kernel = strprintf("resident@%d(%lld tiles x %d waves x %d rows)", res_kin_, (long long)rp.tiles, rp.nw, rp.B);
+    }
     stats_.schedule = split_ ? "split" : (halo_items(L_.R).empty() ? "local" : "full");
     if (dual_) stats_.schedule += sub_overlap_ ? "+subtiles2ov" : "+subtiles2";
     stats_.kernel_depth = kdepth_;
@@ -345,6 +356,11 @@ void HipEngine::do_init(const PatternSpec& p) {
 }
 
 void HipEngine::tile_superstep(int k) {
+    if (res_) {  // the whole superstep is one resident launch (no neighbours: nothing to exchange)
+        res_launch(k, buf_[cur_], buf_[cur_ ^ 1], s_comp_);
+        cur_ ^= 1;
+        return;
+    }
     const std::vector<int>& ps = pass_depths(k);
     first_pass(k, ps[0], ext_after(ps, 0), split_);
     cur_ ^= 1;

@@ -5,6 +5,10 @@ namespace gol {
 namespace hipeng {
 
 void HipEngine::prepare(int k) {
+    if (res_) {
+        res_plan(res_kin_);
+        return;
+    }
     const std::vector<int>& ps = pass_depths(k);
     plan(0, ps[0], ext_after(ps, 0));
     if (can_overlap()) {

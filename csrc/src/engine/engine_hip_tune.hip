@@ -35,7 +35,7 @@ void HipEngine::spin_up() {
 // kernel passes, never the exchanges.
 void HipEngine::measure_pass_costs() {
     pass_us_.clear();
-    if (cfg_.compat || cfg_.kernel_depth > 0 || kernel_ == "lds" || (!dual_ && tile_kernel(0))) return;
+    if (cfg_.compat || cfg_.kernel_depth > 0 || kernel_ == "lds" || res_ || (!dual_ && tile_kernel(0))) return;
     // every instantiated depth up to the pass depth, and the deeper ones a superstep could use: a
     // 20-generation superstep cut 12 + 8 measured cheaper than 8 + 8 + 4 (the K=12 pass runs 2 waves
     // per SIMD at ~10.6 us/gen as two halves, vs 10.3 at K=8; profiles/pingpong_loop_ab.txt)
@@ -378,6 +378,32 @@ void HipEngine::autotune_kernel() {
     HIP_CHECK(hipEventDestroy(e0));
     HIP_CHECK(hipEventDestroy(e1));
     kernel_ = kern_[0];
+    // The resident kernel (small boards without neighbours): one launch per run, halos exchanged
+    // between tiles inside the kernel every kin generations.  Timed on launches of the hinted run's
+    // length (at most 256 generations) against the best pass kernel above.
+    if (resident_eligible() && !split_used()) {
+        const int G = std::min(res_run_depth(), 256);
+        float rbest = 1e30f;
+        int rk = 0;
+        for (int kin : {8, 12, 16, 24}) {
+            if (cfg_.kernel_depth > 0 && kin != cfg_.kernel_depth) continue;
+            const float t = time_resident(kin, G);
+            if (t < 1e29f) tune_ms_[strprintf("0:resident@%d", kin)] = t;
+            if (t < rbest) {
+                rbest = t;
+                rk = kin;
+            }
+        }
+        if (rk && (cfg_.kernel == "resident" || rbest < best)) {
+            res_ = true;
+            res_kin_ = rk;
+            passes_.clear();
+        } else if (cfg_.kernel == "resident") {
+            throw Error("GOL_KERNEL=resident: this board does not fit the resident kernel");
+        }
+    } else if (cfg_.kernel == "resident") {
+        throw Error("GOL_KERNEL=resident needs a rank without neighbours, a 1-D tile of width % 64 == 0 and >= 64 rows");
+    }
 }
 
 void HipEngine::device_barrier() {
@@ -398,6 +424,11 @@ std::map<std::string, double> HipEngine::phase_probe(int k) {
     Armed armed(wd_.get());
     std::map<std::string, double> out;
     k = supported_depth(std::max(1, std::min(k, superstep_depth())));
+    if (res_) {  // one resident launch per superstep, timed on scratch boards
+        out["superstep_us"] = (double)time_resident(res_kin_, k) * 1e3 * k;
+        out["superstep_gens"] = k;
+        return out;
+    }
     sync_canonical();
     synchronize();
     const EngineStats saved = stats_;

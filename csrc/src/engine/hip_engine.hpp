@@ -89,6 +89,7 @@ class HipEngine : public Engine {
 
     std::pair<u64, u64> local_reduce() override {
         sync_canonical();
+        check_res_status();
         HIP_CHECK(hipMemsetAsync(d_red_, 0, 2 * sizeof(u64), s_comp_));
         hipk::launch_reduce_board(buf_[cur_], L_, g_.row0, g_.word0(), g_.global_words(), d_red_, s_comp_);
         HIP_CHECK(hipGetLastError());
@@ -243,6 +244,7 @@ class HipEngine : public Engine {
     // of 24 in 32-generation supersteps ran 24 + 8, and an 8-generation tile pass is 27% slower per
     // generation).  With neighbours every rank keeps R: the exchanges must match.
     int superstep_depth() const override {
+        if (res_) return std::max(L_.R, res_run_depth());
         if (dual_ || !tuned_ || cfg_.compat || kdepth_ <= 0 || kdepth_ >= L_.R || !halo_items(L_.R).empty())
             return L_.R;
         return (L_.R / kdepth_) * kdepth_;
@@ -315,6 +317,7 @@ class HipEngine : public Engine {
     std::vector<u64> read_row(i64 r) override {
         sync_canonical();
         synchronize();
+        check_res_status();
         std::vector<u64> row((size_t)L_.pitch);
         HIP_CHECK(hipMemcpyAsync(row.data(), buf_[cur_] + L_.index(r, -1), (size_t)L_.pitch * 8, hipMemcpyDeviceToHost,
                                  s_comp_));
@@ -424,6 +427,37 @@ class HipEngine : public Engine {
     i64 graph_key(int k, int m, int rem) const { return (((i64)k * 1000 + m) * 1000 + rem) * 2 + par(); }
     hipGraphExec_t graph_for(int k, int m, int rem);
 
+    // ----- resident kernel (step_resident, resident_kernel.hip) -----
+    // Ranks without neighbours whose board fits in the registers of one workgroup per CU (small
+    // boards, BASELINE config 2) may run a whole run() superstep as ONE launch: tiles exchange K-deep
+    // halos with their neighbour tiles through HBM every K generations, inside the kernel.  A
+    // candidate of the kernel autotune (timed against the best streaming / LDS-tile kernel), or forced
+    // with GOL_KERNEL=resident.
+    struct ResPlan {
+        LaneDesc* d = nullptr;
+        u32* nbr_off = nullptr;
+        u32* nbr = nullptr;
+        u32* counters = nullptr;  // per tile: supersteps completed (kernel-maintained)
+        i64 tiles = 0;            // 0: the board does not fit resident at this depth
+        int nw = 16, B = 0, kin = 0;
+        i64 rows = 0;
+    };
+    bool resident_eligible() const {
+        return halo_items(L_.R).empty() && !two_d() && self_y() && xwrap_by_plan() && !cfg_.compat && !cfg_.profile &&
+               !cfg_.force_split && L_.h >= 64;
+    }
+    const ResPlan& res_plan(int kin);
+    // One launch of G generations, src -> dst (the kernel also writes src on its way; odd superstep
+    // count, so the result is in dst).
+    void res_launch(int G, u64* src, u64* dst, hipStream_t s);
+    // Generations per run() superstep of the resident kernel: the hinted run length (one launch per run).
+    int res_run_depth() const {
+        return cfg_.run_hint > 0 ? (int)std::min<u64>(std::max<u64>(cfg_.run_hint, 64), 4096) : 1024;
+    }
+    void check_res_status();
+    // time resident launches of G generations from a scratch copy of the board; ms per generation
+    float time_resident(int kin, int G);
+
     // ----- watchdog support: progress markers -----
     // With a watchdog, every superstep (or graph replay) publishes a marker: HIP events recorded at
     // its end on the streams it used.  The watchdog thread retires completed markers (probe), so GPU
@@ -509,6 +543,11 @@ class HipEngine : public Engine {
     std::map<int, std::vector<HaloItem>> items_;
     std::map<i64, hipGraphExec_t> graphs_;
     std::vector<u64*> dstage_s_, dstage_r_, hstage_s_, hstage_r_;
+    bool res_ = false;  // supersteps run the resident kernel
+    int res_kin_ = 0;   // its generations per in-kernel halo exchange
+    std::map<int, ResPlan> res_plans_;
+    u32* res_status_ = nullptr;
+    u64* res_scratch_[2] = {nullptr, nullptr};  // timing / probe boards (the kernel rewrites its source)
     std::vector<u64*> xhs_, xhr_;  // sub-tile host staging (exchange_rows), xh_bytes_ each
     size_t xh_bytes_ = 0;
 };

@@ -35,49 +35,12 @@
 
 #include "gol/bits.hpp"
 #include "gol/hip_kernels.hpp"
+#include "stencil_device.hpp"
 
 namespace gol {
 namespace hipk {
 
 namespace {
-
-template <unsigned LUT>
-__device__ __forceinline__ u32 b3(u32 a, u32 b, u32 c) {
-    return __builtin_amdgcn_bitop3_b32(a, b, c, LUT);
-}
-
-// lane i <- lane i-1 (lane 0 gets 0: bound_ctrl)
-__device__ __forceinline__ u32 dpp_prev(u32 v) {
-    return (u32)__builtin_amdgcn_mov_dpp((int)v, 0x138 /*wave_shr:1*/, 0xF, 0xF, true);
-}
-// lane i <- lane i+1 (lane 63 gets 0: bound_ctrl)
-__device__ __forceinline__ u32 dpp_next(u32 v) {
-    return (u32)__builtin_amdgcn_mov_dpp((int)v, 0x130 /*wave_shl:1*/, 0xF, 0xF, true);
-}
-
-__device__ __forceinline__ u32 rule32(u32 a0, u32 a1, u32 b0, u32 b1, u32 c0, u32 c1, u32 x) {
-    const u32 x0 = b3<kLutXor3>(a0, b0, c0);
-    const u32 cy = b3<kLutMaj>(a0, b0, c0);
-    const u32 u0 = b3<kLutXor3>(a1, b1, c1);
-    const u32 u1 = b3<kLutMaj>(a1, b1, c1);
-    const u32 g1 = b3<kLutOne3>(x0, cy, u1);
-    const u32 t34 = b3<kLutT34>(u0, u1, g1);
-    return b3<kLutNext>(x0, x, t34);
-}
-
-// Horizontal 3-sums of one split-format word (bits.hpp: lo = even columns, hi = odd columns).
-// Even cell j: left = odd cell j-1 (hi shifted up one, bit 0 from the previous lane's hi), right =
-// odd cell j (hi).  Odd cell j: left = even cell j (lo), right = even cell j+1 (lo shifted down one,
-// bit 31 from the next lane's lo).  2 DPP + 2 funnel shifts + 4 bitop3 per 64 cells.
-__device__ __forceinline__ void hsum_split(u32 lo, u32 hi, u32& s0lo, u32& s1lo, u32& s0hi, u32& s1hi) {
-    const u32 ph = dpp_prev(hi), nl = dpp_next(lo);
-    const u32 Le = __builtin_amdgcn_alignbit(hi, ph, 31);  // (hi << 1) | (ph >> 31)
-    const u32 Ro = __builtin_amdgcn_alignbit(nl, lo, 1);   // (lo >> 1) | (nl << 31)
-    s0lo = b3<kLutXor3>(Le, lo, hi);
-    s1lo = b3<kLutMaj>(Le, lo, hi);
-    s0hi = b3<kLutXor3>(lo, hi, Ro);
-    s1hi = b3<kLutMaj>(lo, hi, Ro);
-}
 
 template <int K>
 struct Pipe {

@@ -370,12 +370,152 @@ static void test_watchdog() {
     }
 }
 
+// Host emulation of step_resident's data flow (resident_kernel.hip): tiles of a plan, bands of B rows
+// per wave, edge slots double-buffered by generation parity (inactive bands leave theirs stale),
+// trapezoid skips, supersteps publishing store lanes' rows into alternating boards and reloading the
+// rest, on split-format words with the device's lane semantics (lanes -1 / 64 read 0).  Checked against
+// the byte oracle; every word a tile reloads must be owned by itself or one of its neighbours.
+static std::string emulate_resident(const std::vector<LaneDesc>& lanes, i64 nw, i64 h, int NW, int Bb, int G, int S,
+                                    int K, std::vector<u64>& A, std::vector<u64>& Bd) {
+    const size_t nt = lanes.size() / 64;
+    std::vector<u32> off, idx;
+    const std::string bad = resident_neighbours(lanes, nw, h, K, true, off, idx);
+    if (!bad.empty()) return bad;
+    std::vector<int> owner((size_t)(h * nw), -1);
+    for (size_t t = 0; t < nt; ++t)
+        for (int l = 0; l < 64; ++l) {
+            const LaneDesc& d = lanes[t * 64 + l];
+            if (d.nrows > 0 && (d.flags & LANE_STORE))
+                for (int r = 0; r < d.nrows; ++r) owner[(size_t)((d.row0 + r) * nw + d.col)] = (int)t;
+        }
+    const int E = NW * Bb;
+    auto word = [&](std::vector<u64>& buf, const LaneDesc& d, int e) -> u64& {
+        return buf[(size_t)(pmod((i64)d.row0 - K + e, h) * nw + d.col)];
+    };
+    // state[t][l][e], slots[t][par][band][first/last][l]
+    std::vector<std::vector<std::vector<u64>>> st(nt, std::vector<std::vector<u64>>(64, std::vector<u64>((size_t)E, 0)));
+    std::vector<u64> slots(nt * 2 * (size_t)NW * 2 * 64, 0);
+    auto slot = [&](size_t t, int par, int b, int fl, int l) -> u64& {
+        return slots[(((t * 2 + (size_t)par) * (size_t)NW + (size_t)b) * 2 + (size_t)fl) * 64 + (size_t)l];
+    };
+    for (size_t t = 0; t < nt; ++t) {
+        const int nrows = lanes[t * 64].nrows;
+        if (nrows <= 0) continue;
+        if (nrows + 2 * K > E) return "tile taller than NW x B";
+        for (int l = 0; l < 64; ++l)
+            for (int e = 0; e < nrows + 2 * K; ++e) st[t][l][(size_t)e] = word(A, lanes[t * 64 + l], e);
+    }
+    for (int s = 1; s <= S; ++s) {
+        const int ks = G / S + (s <= G % S ? 1 : 0);
+        for (int g = 1; g <= ks; ++g) {
+            const int par = g & 1;
+            for (size_t t = 0; t < nt; ++t) {
+                const int T = lanes[t * 64].nrows + 2 * K;
+                if (T <= 2 * K) continue;
+                for (int w = 0; w < NW; ++w) {
+                    const int b0 = w * Bb;
+                    if (!(b0 + Bb > g - 1 && b0 < T - g + 1)) continue;
+                    for (int l = 0; l < 64; ++l) {
+                        slot(t, par, w, 0, l) = st[t][l][(size_t)b0];
+                        slot(t, par, w, 1, l) = st[t][l][(size_t)(b0 + Bb - 1)];
+                    }
+                }
+                std::vector<std::vector<u64>> nx = st[t];
+                for (int w = 0; w < NW; ++w) {
+                    const int b0 = w * Bb;
+                    if (!(b0 + Bb > g - 1 && b0 < T - g + 1)) continue;
+                    // rows -1 .. B of the band for all lanes
+                    auto row = [&](int i, int l) -> u64 {
+                        if (l < 0 || l > 63) return 0;
+                        if (i < 0) return w > 0 ? slot(t, par, w - 1, 1, l) : 0;
+                        if (i >= Bb) return w < NW - 1 ? slot(t, par, w + 1, 0, l) : 0;
+                        return st[t][l][(size_t)(b0 + i)];
+                    };
+                    for (int i = 0; i < Bb; ++i)
+                        for (int l = 0; l < 64; ++l) {
+                            u64 a0, a1, b0s, b1, c0, c1;
+                            hsum64(row(i - 1, l - 1), row(i - 1, l), row(i - 1, l + 1), a0, a1);
+                            hsum64(row(i, l - 1), row(i, l), row(i, l + 1), b0s, b1);
+                            hsum64(row(i + 1, l - 1), row(i + 1, l), row(i + 1, l + 1), c0, c1);
+                            nx[l][(size_t)(b0 + i)] = rule64(a0, a1, b0s, b1, c0, c1, row(i, l));
+                        }
+                }
+                st[t] = nx;
+            }
+        }
+        std::vector<u64>& X = ((S - s) & 1) ? A : Bd;
+        for (size_t t = 0; t < nt; ++t) {
+            const int nrows = lanes[t * 64].nrows;
+            for (int l = 0; l < 64 && nrows > 0; ++l) {
+                const LaneDesc& d = lanes[t * 64 + l];
+                if (d.flags & LANE_STORE)
+                    for (int e = K; e < K + nrows; ++e) word(X, d, e) = st[t][l][(size_t)e];
+            }
+        }
+        if (s == S) break;
+        for (size_t t = 0; t < nt; ++t) {
+            const int nrows = lanes[t * 64].nrows;
+            for (int l = 0; l < 64 && nrows > 0; ++l) {
+                const LaneDesc& d = lanes[t * 64 + l];
+                for (int e = 0; e < nrows + 2 * K; ++e) {
+                    if ((d.flags & LANE_STORE) && e >= K && e < K + nrows) continue;
+                    const int o = owner[(size_t)(pmod((i64)d.row0 - K + e, h) * nw + d.col)];
+                    bool known = o == (int)t;
+                    for (u32 j = off[t]; j < off[t + 1] && !known; ++j) known = (int)idx[j] == o;
+                    if (!known) return strprintf("tile %zu reads a word of tile %d, not a neighbour", t, o);
+                    st[t][l][(size_t)e] = word(X, d, e);
+                }
+            }
+        }
+    }
+    return "";
+}
+
+static void test_resident() {
+    struct Case {
+        i64 h, nw, rows;
+        int K, NW, B, G;
+    };
+    for (const Case& c : std::vector<Case>{{96, 2, 24, 4, 8, 5, 13},
+                                           {96, 2, 24, 4, 8, 5, 12},
+                                           {80, 1, 10, 3, 4, 4, 9},
+                                           {128, 3, 32, 8, 8, 6, 40},
+                                           {64, 2, 64, 6, 8, 10, 17},
+                                           {70, 70, 20, 5, 8, 4, 31}}) {
+        const i64 W = c.nw * 64;
+        auto b = random_board(c.h, W, (unsigned)(c.h * 7 + c.nw + c.G));
+        std::vector<u8> ref = b;
+        for (int g = 0; g < c.G; ++g) ref = byte_step(ref, c.h, W);
+        auto lanes = build_plan({{0, c.h, 0, c.nw}}, c.nw, c.h, c.rows, c.K, true, nullptr, 1, 8);
+        CHECK(validate_plan(lanes, c.nw, c.h, 0, c.K, true).empty());
+        int S = (c.G + c.K - 1) / c.K;
+        S += (S % 2 == 0);
+        const int kmax = (c.G + S - 1) / S;
+        std::vector<u64> A = pack(b, c.h, W), Bd(A.size(), 0);
+        for (auto& x : A) x = split_word(x);
+        const std::string err = emulate_resident(lanes, c.nw, c.h, c.NW, c.B, c.G, S, kmax, A, Bd);
+        if (!err.empty()) fprintf(stderr, "resident emulation: %s\n", err.c_str());
+        CHECK(err.empty());
+        std::vector<u64> want = pack(ref, c.h, W);
+        bool same = true;
+        for (size_t i = 0; i < want.size(); ++i) same &= merge_word(Bd[i]) == want[i];
+        CHECK(same);
+    }
+    // a plan with a hole in one column is refused
+    auto lanes = build_plan({{0, 40, 0, 3}}, 3, 40, 10, 2, true, nullptr, 1, 8);
+    for (auto& d : lanes)
+        if (d.col == 1 && (d.flags & LANE_STORE) && d.row0 == 10) d.flags = 0;
+    std::vector<u32> off, idx;
+    CHECK(!resident_neighbours(lanes, 3, 40, 2, true, off, idx).empty());
+}
+
 int main() {
     test_watchdog();
     test_cli();
     test_geometry();
     test_patterns();
     test_plan();
+    test_resident();
     test_bits();
     test_cpu_step();
     test_dump();
