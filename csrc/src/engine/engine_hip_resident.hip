@@ -18,7 +18,7 @@ const HipEngine::ResPlan& HipEngine::res_plan(int kin) {
     for (int per_cu : {1, 2}) {
         const int bmax = per_cu == 1 ? 8 : 4;
         const i64 rows = balanced_rows_per_chunk(rg, L_.nw, L_.h, kin, (i64)per_cu * cus_, 1, true);
-        if (rows + 2 * (i64)kin > 16 * (i64)bmax || rows < 2) continue;
+        if (rows + 2 * (i64)kin > 16 * (i64)bmax) continue;
         const int B = hipk::resident_band_rows((int)ceil_div(rows + 2 * (i64)kin, 16));
         if (B <= 0 || B > bmax) continue;
         if (hipk::resident_blocks_per_cu(16, B, wrapy) < per_cu) continue;

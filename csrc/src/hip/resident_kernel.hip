@@ -84,6 +84,7 @@ __global__ __launch_bounds__(64 * NW) void step_resident(u64* __restrict__ src, 
     const int T = nrows + 2 * K;
     const int b0 = wv * B;
     const bool out_lane = (d.flags & LANE_STORE) != 0;
+    if (threadIdx.x == 0) abort_all = 0;  // (LDS starts undefined; the first generation's barrier orders it)
     // word of extended row e (tile row d.row0 - K + e) of this lane's column in `buf`.  The row index
     // passes through an opaque scalar move, so the compiler recomputes each address where it is used
     // (once per superstep) instead of keeping 2 x B 64-bit addresses per buffer live across the
