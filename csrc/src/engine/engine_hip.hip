@@ -316,7 +316,7 @@ void HipEngine::do_init(const PatternSpec& p) {
     for (const auto& kv : sched_us_)
         tn += strprintf("%ssched:%s=%.3fus/gen", tn.empty() ? "" : " ", kv.first.c_str(), kv.second);
     for (const auto& kv : pass_us_) tn += strprintf("%spass%d=%.1fus", tn.empty() ? "" : " ", kv.first, kv.second);
-    if (!split_ && !dual_ && tile_kernel(0) && kernel_ != "lds") {  // the tile variant the full superstep runs
+    if (!split_ && !dual_ && !res_ && tile_kernel(0) && kernel_ != "lds") {  // the tile variant the full superstep runs
         const DevPlan& p0 = plan(0, kdepth_, 0);
         tn += strprintf("%stile_plan=%s,%lldrows,%lldtiles", tn.empty() ? "" : " ",
                         p0.fold ? ((p0.tflags & hipk::STEP_TILE_INPLACE) ? "fold-inplace" : "fold")
@@ -349,10 +349,14 @@ void HipEngine::do_init(const PatternSpec& p) {
         stats_.graph_launches = 0;
     }
     spin_up();  // init ends with the GPU at its steady clock (plan building and captures idle it)
-    const DevPlan& fp = full_plan_stats();
-    stats_.plan_waves = fp.waves;
-    stats_.lane_efficiency =
-        fp.st.lane_rows ? (double)fp.st.out_words / (double)fp.st.lane_rows : 0.0;
+    if (res_) {
+        stats_.plan_waves = res_plan(res_kin_).tiles;  // workgroups of the resident launch
+        stats_.lane_efficiency = 0;
+    } else {
+        const DevPlan& fp = full_plan_stats();
+        stats_.plan_waves = fp.waves;
+        stats_.lane_efficiency = fp.st.lane_rows ? (double)fp.st.out_words / (double)fp.st.lane_rows : 0.0;
+    }
 }
 
 void HipEngine::tile_superstep(int k) {
