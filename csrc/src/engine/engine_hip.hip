@@ -308,7 +308,7 @@ void HipEngine::do_init(const PatternSpec& p) {
         stats_.kernel = strprintf("resident@%d(%lld tiles x %d waves x %d rows)", res_kin_, (long long)rp.tiles, rp.nw, rp.B);
     }
     stats_.schedule = split_ ? "split" : (halo_items(L_.R).empty() ? "local" : "full");
-    if (dual_) stats_.schedule += sub_overlap_ ? "+subtiles2ov" : "+subtiles2";
+    if (dual_) stats_.schedule += sub_overlap_ == 2 ? "+subtiles2ov2" : (sub_overlap_ ? "+subtiles2ov" : "+subtiles2");
     stats_.kernel_depth = kdepth_;
     stats_.tile_waves = cfg_.tile_waves;
     std::string tn;

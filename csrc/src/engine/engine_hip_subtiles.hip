@@ -40,7 +40,8 @@ void HipEngine::teardown_dual() {
             if (b) hipFree(b);
             b = nullptr;
         }
-    dual_ = sub_overlap_ = false;
+    dual_ = false;
+    sub_overlap_ = 0;
     sub_current_ = canon_stale_ = false;
 }
 
@@ -49,11 +50,12 @@ const DevPlan& HipEngine::sub_plan(int s, int k, i64 e, int part) {
     auto it = sub_plans_.find(key);
     if (it != sub_plans_.end()) return it->second;
     const Layout& L = sub_L_[s];
-    // output rows -e .. h+e; for half 0, part 1 starts k rows below the tile's top (its inputs never
-    // reach the north ghost rows the exchange writes) and part 2 is the band above that
+    // output rows -e .. h+e; part 1 stops k rows short of the rank's halo (half 0: starts k rows
+    // below its top, half 1: ends k rows above its bottom), so its inputs never reach the ghost rows
+    // the exchange writes; part 2 is that band
     std::vector<Region> rg = {{-e, L.h + e, 0, L.nw}};
-    if (part == 1) rg[0].r0 = k;
-    if (part == 2) rg[0].r1 = k;
+    if (part == 1) (s == 0 ? rg[0].r0 : rg[0].r1) = s == 0 ? k : L.h - k;
+    if (part == 2) (s == 0 ? rg[0].r1 : rg[0].r0) = s == 0 ? k : L.h - k;
     i64 bpc = hipk::step_blocks_per_cu(k, sub_flags());
     // waves/SIMD each half's plan is sized for: two concurrent halves fill the SIMDs between
     // them, so 2-wave plans (taller segments, less halo) measured best (kbench: 9.85 vs 10.11
@@ -71,7 +73,11 @@ const DevPlan& HipEngine::sub_plan(int s, int k, i64 e, int part) {
         // quarter of the runs, profiles/pingpong_loop_ab.txt)
         if (hipk::step_blocks_per_cu(k, sub_flags()) <= 2) bpc = 1;
     }
-    const i64 rows = balanced_rows_per_chunk(rg, L.nw, L.h, k, bpc * kWavesPerBlock * cus_, 2 * (i64)k, true);
+    // A band (part 2) is a few rows tall and runs while little else does: its time is the serial
+    // level pipeline of one wave, ~(S + K) x K row-levels for S rows per wave, so it is cut into
+    // 4-row segments (K = 12, 28-row band: ~38 us as one segment per column, ~14 us in 4-row ones).
+    const i64 rows = part == 2 ? 4
+                               : balanced_rows_per_chunk(rg, L.nw, L.h, k, bpc * kWavesPerBlock * cus_, 2 * (i64)k, true);
     DevPlan p;
     std::vector<LaneDesc> lanes = build_plan(rg, L.nw, L.h, rows, k, true, &p.st, kWavesPerBlock, cfg_.plan_xcds);
     const std::string bad = validate_plan(lanes, L.nw, L.h, L.R, k, false);
@@ -98,8 +104,26 @@ void HipEngine::dual_superstep(int k) {
     // half-tile kernel when both become ready (a kernel that has filled the CUs first would hold
     // it back).  Chosen by measurement (schedule "subtiles+ov"): it costs a second, small kernel
     // per superstep.
-    const bool ov = sub_overlap_ && !self_y() && !graphs;
-    if (!self_y()) {
+    const bool ov = sub_overlap_ == 1 && !self_y() && !graphs;
+    const bool ov2 = sub_overlap_ == 2 && !self_y() && !graphs;
+    if (ov2) {
+        // Both halves' interiors first, each on its stream (half 1 reads half 0's edge across the seam:
+        // its stream waits for half 0's previous superstep); the exchange then runs on the compute
+        // stream after half 0's interior (no extra stream, no cross-queue wait before it), half 0's
+        // band follows it on that stream and half 1's band waits for it on the other.
+        launch_half(0, p, k, s_comp_, 0, 1);
+        wait_pending(s_comm_, ev_sub_a_);
+        launch_half(1, p, k, s_comm_, 0, 1);
+        std::vector<Message> sends, recvs;
+        dual_messages(p, k, sends, recvs);
+        exchange_rows(sends, recvs, s_comp_);
+        stats_.exchanges += 1;
+        stats_.halo_bytes += (u64)(rows_bytes(0, k) + rows_bytes(1, k));
+        HIP_CHECK(hipEventRecord(ev_sub_x_, s_comp_));
+        launch_half(0, p, k, s_comp_, 0, 2);
+        HIP_CHECK(hipStreamWaitEvent(s_comm_, ev_sub_x_, 0));
+        launch_half(1, p, k, s_comm_, 0, 2);
+    } else if (!self_y()) {
         hipStream_t xs = s_comp_;
         if (ov) {
             launch_half(0, p, k, s_comp_, 0, 1);
@@ -132,7 +156,7 @@ void HipEngine::dual_superstep(int k) {
         for (int j = 0; j < np; ++j)
             for (int i = 0; i < 2; ++i) {
                 const int s = sub_first_ ^ i;  // GOL_SUB_FIRST=1: half 1's pass first (measurement knob)
-                if (!(ov && s == 0 && j == 0)) launch_half(s, p, k, s ? s_comm_ : s_comp_, j);
+                if (!((ov && s == 0 && j == 0) || (ov2 && j == 0))) launch_half(s, p, k, s ? s_comm_ : s_comp_, j);
             }
     }
     if (wd_) {

@@ -116,7 +116,11 @@ void HipEngine::choose_schedule() {
         // the overlapped variant needs the exchange (neighbours, or the self-exchange)
         std::vector<std::string> dc;
         if (cfg_.subtile_overlap <= 0 || self_y()) dc.push_back("subtiles");
-        if (cfg_.subtile_overlap != 0 && !self_y()) dc.push_back("subtiles+ov");
+        // (GOL_SUBTILE_OVERLAP: 1 forces the half-0 variant, 2 the symmetric one, auto times both)
+        if (cfg_.subtile_overlap != 0 && !self_y()) {
+            if (cfg_.subtile_overlap != 2) dc.push_back("subtiles+ov");
+            if (cfg_.subtile_overlap != 1) dc.push_back("subtiles+ov2");
+        }
         if (cfg_.subtile_graphs < 0 && cfg_.graph && !cfg_.profile) dc.push_back("subtiles+graph");
         if (cfg_.subtiles == 2) cands.clear();
         cands.insert(cands.end(), dc.begin(), dc.end());
@@ -173,7 +177,7 @@ void HipEngine::choose_schedule() {
     }
     split_ = pick == "split";
     dual_ = pick.rfind("subtiles", 0) == 0;
-    sub_overlap_ = pick == "subtiles+ov";
+    sub_overlap_ = pick == "subtiles+ov" ? 1 : (pick == "subtiles+ov2" ? 2 : 0);
     graph_rccl_on_ = cfg_.graph_rccl == 1 || pick == "full+graph";
     sub_graphs_on_ = cfg_.subtile_graphs == 1 || pick == "subtiles+graph";
     if (!sub_graphs_on_) destroy_dual_graphs();
@@ -191,7 +195,7 @@ void HipEngine::time_schedule(const std::string& c, int k, int reps, bool eager)
     if (c.rfind("subtiles", 0) == 0) {
         setup_dual();
         dual_ = true;
-        sub_overlap_ = c == "subtiles+ov";
+        sub_overlap_ = c == "subtiles+ov" ? 1 : (c == "subtiles+ov2" ? 2 : 0);
         const bool sg = sub_graphs_on_;
         sub_graphs_on_ = c == "subtiles+graph" || cfg_.subtile_graphs == 1;
         if (sub_graphs_on_) {
@@ -199,7 +203,8 @@ void HipEngine::time_schedule(const std::string& c, int k, int reps, bool eager)
             capture_dual_graphs(k);  // once per (half, start buffer, depth)
         }
         for (int i = 0; i < reps; ++i) dual_superstep(k);
-        dual_ = sub_overlap_ = false;
+        dual_ = false;
+        sub_overlap_ = 0;
         sub_graphs_on_ = sg;
         return;
     }
@@ -432,7 +437,8 @@ std::map<std::string, double> HipEngine::phase_probe(int k) {
     sync_canonical();
     synchronize();
     const EngineStats saved = stats_;
-    const bool was_dual = dual_, was_ov = sub_overlap_, was_split = split_;
+    const bool was_dual = dual_, was_split = split_;
+    const int was_ov = sub_overlap_;
     hipEvent_t e0, e1;
     HIP_CHECK(hipEventCreate(&e0));
     HIP_CHECK(hipEventCreate(&e1));
@@ -464,7 +470,7 @@ std::map<std::string, double> HipEngine::phase_probe(int k) {
         }
         out["exchange_us"] = best;
     }
-    const std::string sched = dual_ ? (sub_overlap_ ? "subtiles+ov" : "subtiles")
+    const std::string sched = dual_ ? (sub_overlap_ == 2 ? "subtiles+ov2" : (sub_overlap_ ? "subtiles+ov" : "subtiles"))
                                     : (split_ ? "split" : (halo_items(L_.R).empty() ? "local" : "full"));
     const int reps = 2;
     double best = 1e30;

@@ -172,15 +172,16 @@ class HipEngine : public Engine {
         for (size_t j = 0; j < ps.size(); ++j)
             for (int s = 0; s < 2; ++s) sub_plan(s, ps[j], ext_after(ps, j));
         if (sub_overlap_ && !self_y())
-            for (int part : {1, 2}) sub_plan(0, ps[0], ext_after(ps, 0), part);
+            for (int s = 0; s < (sub_overlap_ == 2 ? 2 : 1); ++s)
+                for (int part : {1, 2}) sub_plan(s, ps[0], ext_after(ps, 0), part);
     }
     void destroy_dual_graphs() {
         for (auto& kv : dual_graphs_) hipGraphExecDestroy(kv.second);
         dual_graphs_.clear();
     }
 
-    // part: 0 the whole pass; a first pass of half 0 split around the exchange (sub_overlap_):
-    // 1 all output rows but the band next to the north halo, 2 that band
+    // part: 0 the whole pass; a first pass split around the exchange (sub_overlap_): 1 all output
+    // rows but the band next to the rank's halo (half 0: north, half 1: south), 2 that band
     const DevPlan& sub_plan(int s, int k, i64 e, int part = 0);
 
     u32 sub_flags() const { return step_flags() & ~hipk::STEP_WRAP_Y; }  // sub-tiles always have ghost rows
@@ -525,7 +526,12 @@ class HipEngine : public Engine {
     std::map<i64, DevPlan> plans_;
     // GOL_SUBTILES=2 state
     bool dual_ = false;
-    bool sub_overlap_ = false;  // half 0's first pass overlaps the exchange (timed candidate "subtiles+ov")
+    // Exchange overlap of the sub-tile superstep (timed candidates): 0 none ("subtiles"); 1 half 0's
+    // first pass, but for its band next to the north halo, runs while the exchange is in flight
+    // ("subtiles+ov"); 2 both halves' first passes, but for their bands next to the rank's halos,
+    // run before the exchange, which then runs on the compute stream between half 0's interior and its
+    // band ("subtiles+ov2")
+    int sub_overlap_ = 0;
     Layout sub_L_[2];
     i64 sub_r0_[2] = {0, 0};
     u64* sub_buf_[2][3] = {{nullptr, nullptr, nullptr}, {nullptr, nullptr, nullptr}};
