@@ -121,7 +121,9 @@ void HipEngine::choose_schedule() {
             if (cfg_.subtile_overlap != 2) dc.push_back("subtiles+ov");
             if (cfg_.subtile_overlap != 1) dc.push_back("subtiles+ov2");
         }
-        if (cfg_.subtile_graphs < 0 && cfg_.graph && !cfg_.profile) dc.push_back("subtiles+graph");
+        // (graph replay excludes the overlapped variants: not a candidate when one is forced)
+        if (cfg_.subtile_graphs < 0 && cfg_.graph && !cfg_.profile && cfg_.subtile_overlap <= 0)
+            dc.push_back("subtiles+graph");
         if (cfg_.subtiles == 2) cands.clear();
         cands.insert(cands.end(), dc.begin(), dc.end());
     }
