@@ -182,7 +182,9 @@ void HipEngine::choose_schedule() {
     sub_overlap_ = pick == "subtiles+ov" ? 1 : (pick == "subtiles+ov2" ? 2 : 0);
     graph_rccl_on_ = cfg_.graph_rccl == 1 || pick == "full+graph";
     sub_graphs_on_ = cfg_.subtile_graphs == 1 || pick == "subtiles+graph";
-    if (!sub_graphs_on_) destroy_dual_graphs();
+    // The timing's per-half graphs baked in the pass cut of that moment; measure_pass_costs may change
+    // the cut (and with it the buffer parity a superstep ends on): always recapture after it (do_init).
+    destroy_dual_graphs();
     if (dual_) {
         setup_dual();
         sub_current_ = false;  // the halves hold timing scratch: load the board at the next run
