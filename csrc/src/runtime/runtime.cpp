@@ -176,7 +176,7 @@ EngineConfig engine_config(const Options& o, const std::string& backend, int dev
     auto tri = [](const char* name) {  // 0 off, 1 on, auto (default) -1: a timed candidate
         return env_str(name, "auto") == "auto" ? -1 : (int)(env_int(name, 0) != 0);
     };
-    c.subtile_overlap = tri("GOL_SUBTILE_OVERLAP");
+    c.subtile_overlap = env_str("GOL_SUBTILE_OVERLAP", "auto") == "auto" ? -1 : (int)env_int("GOL_SUBTILE_OVERLAP", 0);
     c.subtile_graphs = tri("GOL_SUBTILE_GRAPHS");
     c.self_exchange = env_int("GOL_SELF_EXCHANGE", 0) != 0;
     c.force_split = env_int("GOL_FORCE_SPLIT", 0) != 0;

@@ -109,7 +109,10 @@ class Simulation:
         cfg.tune_tile_waves = "GOL_TILE_WAVES" not in os.environ
         cfg.sub_occ = int(sub_occ)
         # 1 on / 0 off / -1 auto: a candidate of the init-time schedule timing (GOL_* env defaults)
-        cfg.subtile_overlap = _tri("GOL_SUBTILE_OVERLAP") if subtile_overlap is None else int(subtile_overlap)
+        if subtile_overlap is None:  # 0 off, 1 half 0 only, 2 both halves, auto: timed candidates
+            v = os.environ.get("GOL_SUBTILE_OVERLAP", "auto")
+            subtile_overlap = -1 if v == "auto" else int(v)
+        cfg.subtile_overlap = int(subtile_overlap)
         cfg.self_exchange = bool(self_exchange)
         cfg.force_split = bool(force_split)
         cfg.sched = schedule
