@@ -62,10 +62,8 @@ void HipEngine::prewarm_graph() {
 // Replays, largest shape first (eager launches of a superstep cost ~15 us of GPU idle each;
 // graph replays none), every ladder shape captured at init.  A rank without neighbours also replays
 // the remainder no shape covers, as a graph of that one short superstep captured on first use (the
-// capture costs milliseconds, once per remainder length): an eager pass right before a replay made
-// the replay's kernels ~1.5% slower each (8192^2 x 1000 after a 100-generation warmup, which ends on a
-// 4-generation eager pass: 1.43-1.46 vs 1.39-1.40 us/gen after 64 or 128; kernel traces of both,
-// profiles/cfg2_warmup_remainder.txt).  With neighbours the remainder stays eager (its exchange).
+// capture costs milliseconds, once per remainder length; a replay has no launch gaps between its
+// passes).  With neighbours the remainder stays eager (its exchange).
 void HipEngine::run_graphed(u64& generations) {
     int k = 0, M = 0;
     if (!graph_shape(k, M)) return;

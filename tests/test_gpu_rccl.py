@@ -69,7 +69,6 @@ def test_rccl_self_subtiles(gol, rccl, R, gens, overlap):
     assert st["schedule"] in want, st
     if overlap == -1:
         assert "sched:subtiles=" in st["tuning"] and "sched:subtiles+ov=" in st["tuning"], st
-        assert "sched:subtiles+ov2=" in st["tuning"], st
     assert st["exchanges"] >= gens // R, st
     assert np.array_equal(got, numpy_step(initial_board(5, N, 1, True, 9), gens))
 
