@@ -58,6 +58,7 @@ constexpr int kTrashWaves = 1024;
 // Allocate the current device's trash buffer (call once per device before any launch or capture;
 // thread safe).
 void ensure_trash();
+u64* trash_of_current_device();  // (throws when ensure_trash has not run on this device)
 
 // Supported temporal depths (template instantiations).
 bool step_depth_supported(int k);
@@ -95,6 +96,16 @@ int resident_blocks_per_cu(int nw, int B, bool wrapy);
 void launch_step_resident(int nw, int B, bool wrapy, u64* src, u64* dst, const LaneDesc* plan, i64 n_tiles,
                           const u32* nbr_off, const u32* nbr, u32* counters, u32* status, const ResidentParams& rp,
                           hipStream_t s);
+// step_pipe (pipe_kernel.hip): K = nw x L generations per launch, one workgroup of `nw` (4, 8, 12,
+// 16) waves per plan wave (a segment of the plan, as step_tile), wave w computing levels
+// w L + 1 .. (w + 1) L of the whole segment and handing its rows to wave w + 1 through an LDS ring.
+size_t pipe_lds_bytes(int nw);
+bool pipe_supported(int nw, int L);
+int pipe_blocks_per_cu(int nw, int L, bool wrapy);
+// True (and cleared) when a step_pipe wait timed out since the last call: the board is invalid.
+bool pipe_fault();
+void launch_step_pipe(int nw, int L, const u64* src, u64* dst, const LaneDesc* plan, i64 n_tiles, const StepParams& p,
+                      hipStream_t s);
 // Single-generation LDS-tiled kernel over output rows [r0, r1) (all words).
 void launch_step_lds(const u64* src, u64* dst, const Layout& L, i64 r0, i64 r1, u32 flags, hipStream_t s);
 

@@ -47,7 +47,7 @@ Engine::Engine(const Geometry& g, const EngineConfig& c, std::shared_ptr<Transpo
     // 9.70-9.79 at 128 (profiles/subtile_superstep_boundaries.txt).  Rank-invariant inputs only.
     const bool sub_tall = cfg_.backend == "hip" && (cfg_.subtiles == 2 || cfg_.subtiles < 0) && !two_d() && strip_rows >= kSubtileMinRows &&
                           g_.dec.W % 64 == 0 && !cfg_.force_split && !cfg_.profile && !cfg_.compat &&
-                          cfg_.kernel != "lds" && cfg_.kernel != "tile";
+                          cfg_.kernel != "lds" && cfg_.kernel != "tile" && cfg_.kernel != "pipe";
     // (1-D strips with neighbours: 128 measured 1-3% faster than 64 through RCCL self-exchange,
     // 4096 x 32768 2.44 -> 2.36, 8192 x 65536 5.93 -> 5.85 us/gen; profiles/per_rank_tiles_self_exchange.txt)
     const int want = cfg_.halo_depth > 0 ? cfg_.halo_depth : (sub_tall || tall_strips ? 128 : (tall_tiles ? 56 : 32));

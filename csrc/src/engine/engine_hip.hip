@@ -53,12 +53,22 @@ HipEngine::HipEngine(const Geometry& g, const EngineConfig& c, std::shared_ptr<T
     } else if (kernel_ == "temporal" || kernel_ == "auto" || kernel_ == "resident") {
         // auto: the depth must suit both candidates (instantiated temporal depths)
         K = supported_kernel_depth(std::min(K, hipk::max_step_depth()));
+    } else if (kernel_ == "pipe") {
+        // GOL_PIPE=nw,L,wg: the step_pipe geometry (default 9,3,2: K = 24)
+        const std::string g = env_str("GOL_PIPE", "9,3,2");
+        int nw = 0, l = 0, wg = 0;
+        if (sscanf(g.c_str(), "%d,%d,%d", &nw, &l, &wg) != 3 || !hipk::pipe_supported(nw, l) || wg < 1 || wg > 8)
+            throw Error("GOL_PIPE must be nw,L,wg with nw in {5,7,9,11,13,16}, L in 1..4 (got '" + g + "')");
+        set_pipe(nw, l, wg);
+        if (pipe_k_ > R)
+            throw Error(strprintf("GOL_KERNEL=pipe: its pass depth %d exceeds the halo depth %d (GOL_HALO_DEPTH)", pipe_k_, R));
+        K = pipe_k_;
     } else {
-        throw Error("GOL_KERNEL must be auto, temporal, tile, lds or resident (got '" + kernel_ + "')");
+        throw Error("GOL_KERNEL must be auto, temporal, tile, pipe, lds or resident (got '" + kernel_ + "')");
     }
     if (!multipass_) R = std::min(R, K);
     kdepth_ = K;
-    tdepth_ = supported_kernel_depth(std::min(K, hipk::max_step_depth()));
+    tdepth_ = supported_kernel_depth(std::min(kernel_ == "pipe" ? 8 : K, hipk::max_step_depth()));
     if (R != L_.R) L_ = Layout(L_.h, L_.w, R);
     stats_.depth = R;
     // slack rows: the temporal kernel prefetches 3 (shallow passes: 6) rows past a segment's last input row
@@ -303,6 +313,8 @@ void HipEngine::do_init(const PatternSpec& p) {
                          env_str("GOL_READY_EVENTS", "") == "always";
     }
     stats_.kernel = split_ ? kern_[1] + "+boundary:" + kern_[2] : kern_[0];
+    if (!split_ && !dual_ && kern_[0] == "pipe")
+        stats_.kernel = strprintf("pipe@%d(%dx%d,%d/CU)", pipe_k_, pipe_nw_ - 1, pipe_l_, pipe_wg_);
     if (res_) {
         const ResPlan& rp = res_plan(res_kin_);
         stats_.kernel = strprintf("resident@%d(%lld tiles x %d waves x %d rows)", res_kin_, (long long)rp.tiles, rp.nw, rp.B);
@@ -467,9 +479,12 @@ void HipEngine::launch(int kind, int k, i64 e, const u64* src, u64* dst, hipStre
         const DevPlan& p = plan(kind, k, e);
         if (p.st.out_words == 0) return;
         hipk::StepParams sp{L_.pitch, (i32)L_.h, (i32)L_.nw, L_.R, step_flags() | p.tflags};
-        if (tile_kernel(kind))
+        if (tile_kernel(kind)) {
             hipk::launch_step_tile(cfg_.tile_waves, k, src, dst, p.d, p.waves, p.rows, sp, s);
-        else
+        } else if (pipe_pass(kind, k)) {
+            hipk::launch_step_pipe(pipe_nw_, pipe_l_, src, dst, p.d, p.waves, sp, s);
+            pipe_used_ = true;
+        } else
             hipk::launch_step(k, src, dst, p.d, p.waves, sp, s);
     }
     HIP_CHECK(hipGetLastError());

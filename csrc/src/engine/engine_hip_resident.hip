@@ -72,6 +72,8 @@ void HipEngine::res_launch(int G, u64* src, u64* dst, hipStream_t s) {
 }
 
 void HipEngine::check_res_status() {
+    if (pipe_used_ && hipk::pipe_fault())
+        throw Error("step_pipe: a ring wait timed out (a stage never got its rows); the board is invalid");
     if (!res_status_) return;
     u32 v = 0;
     HIP_CHECK(hipMemcpyAsync(&v, res_status_, sizeof(u32), hipMemcpyDeviceToHost, s_comp_));

@@ -35,7 +35,9 @@ void HipEngine::spin_up() {
 // kernel passes, never the exchanges.
 void HipEngine::measure_pass_costs() {
     pass_us_.clear();
-    if (cfg_.compat || cfg_.kernel_depth > 0 || kernel_ == "lds" || res_ || (!dual_ && tile_kernel(0))) return;
+    if (cfg_.compat || cfg_.kernel_depth > 0 || kernel_ == "lds" || res_ || (!dual_ && tile_kernel(0)) ||
+        (!dual_ && !split_ && kern_[0] == "pipe"))
+        return;
     // every instantiated depth up to the pass depth, and the deeper ones a superstep could use: a
     // 20-generation superstep cut 12 + 8 measured cheaper than 8 + 8 + 4 (the K=12 pass runs 2 waves
     // per SIMD at ~10.6 us/gen as two halves, vs 10.3 at K=8; profiles/pingpong_loop_ab.txt)
@@ -292,6 +294,7 @@ void HipEngine::autotune_kernel() {
             return 0.f;
         }
         const bool tile = kern_[kind] == "tile";
+        const bool pipe = kern_[kind] == "pipe";
         hipStream_t s = s_comp_;
         launch(kind, k, 0, buf_[cur_], buf_[cur_ ^ 1], s);  // warm-up (and plan build)
         HIP_CHECK(hipEventRecord(e0, s));
@@ -301,9 +304,10 @@ void HipEngine::autotune_kernel() {
         float ms = 0;
         HIP_CHECK(hipEventElapsedTime(&ms, e0, e1));
         const float per_gen = ms / 3 / (float)k;
-        const std::string key = tile ? strprintf("%d:%s@%dx%dw", kind, kern, k, cfg_.tile_waves)
-                                     : (occ_ ? strprintf("%d:%s@%d/%dw", kind, kern, k, occ_)
-                                             : strprintf("%d:%s@%d", kind, kern, k));
+        const std::string key = tile   ? strprintf("%d:%s@%dx%dw", kind, kern, k, cfg_.tile_waves)
+                                : pipe ? strprintf("%d:pipe@%d(%dx%d,%d/CU)", kind, k, pipe_nw_ - 1, pipe_l_, pipe_wg_)
+                                : occ_ ? strprintf("%d:%s@%d/%dw", kind, kern, k, occ_)
+                                       : strprintf("%d:%s@%d", kind, kern, k);
         auto it = tune_ms_.find(key);
         tune_ms_[key] = it == tune_ms_.end() ? per_gen : std::min(it->second, per_gen);  // best round
         return per_gen;
@@ -316,6 +320,7 @@ void HipEngine::autotune_kernel() {
         const char* kern;
         int k, nw;
         int occ = 0;  // temporal: waves per SIMD of the plan (0 = full occupancy)
+        int pnw = 0, pl = 0, pwg = 0;  // pipe: waves per workgroup, generations per stage, workgroups per CU
     };
     const int k0 = cfg_.compat ? 1 : kdepth_;
     const int nw0 = cfg_.tile_waves;
@@ -339,8 +344,24 @@ void HipEngine::autotune_kernel() {
     }
     for (int nw : nws)
         for (int k : kts) cands.push_back({"tile", k, nw});
+    // The level-pipelined workgroup kernel (step_pipe) when the full-tile plan is the only kind a
+    // superstep runs: 8 or 12 stages (balanced over the 4 SIMDs, with the loader), 2 or 3 generations
+    // each.  kbench, one MI355X (docs/PERFORMANCE.md §13): 32768^2 8x3 at 2/CU 10.16-10.21 vs
+    // temporal 10.56 us/gen; 4096 x 32768 12x3 2.15 vs 2.35; 16384^2 8x3 3.45 vs 3.61; 8192^2
+    // loses to the folded tile kernel (1.50 vs 1.38).
+    // (With neighbours it is the kernel of the "full" schedule's first pass and of the later passes;
+    // when the schedule timing then picks "split", the interior / boundary kernels are tuned below
+    // and the later passes run step_temporal at the measured depths.)
+    if (!cfg_.compat && cfg_.kernel_depth == 0 && env_int("GOL_PIPE_TUNE", 1) != 0) {
+        const int geo[][3] = {{9, 3, 2}, {13, 2, 1}, {13, 3, 1}, {9, 2, 2}};
+        for (const auto& g : geo) {
+            const int k = (g[0] - 1) * g[1];
+            if (k <= L_.R && hipk::pipe_supported(g[0], g[1])) cands.push_back({"pipe", k, nw0, 0, g[0], g[1], g[2]});
+        }
+    }
     for (const auto& c : cands) {
         occ_ = c.occ;
+        if (c.pnw) set_pipe(c.pnw, c.pl, c.pwg);
         time_pass(0, c.kern, c.k, true);
     }
     spin_up();
@@ -351,6 +372,7 @@ void HipEngine::autotune_kernel() {
         for (size_t i = 0; i < cands.size(); ++i) {
             cfg_.tile_waves = cands[i].nw;
             occ_ = cands[i].occ;
+            if (cands[i].pnw) set_pipe(cands[i].pnw, cands[i].pl, cands[i].pwg);
             tbest[i] = std::min(tbest[i], time_pass(0, cands[i].kern, cands[i].k));
         }
     float best = 1e30f;
@@ -364,6 +386,12 @@ void HipEngine::autotune_kernel() {
     kdepth_ = pick.k;
     cfg_.tile_waves = pick.nw;
     occ_ = pick.occ;
+    if (pick.pnw) {
+        set_pipe(pick.pnw, pick.pl, pick.pwg);
+        tdepth_ = supported_kernel_depth(std::min(8, hipk::max_step_depth()));  // the remainders' depth
+    } else {
+        pipe_k_ = 0;
+    }
     passes_.clear();
     // interior / boundary plans of split supersteps, at the chosen pass depth
     if (split_used()) {

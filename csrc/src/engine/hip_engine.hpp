@@ -152,7 +152,7 @@ class HipEngine : public Engine {
         const bool want = cfg_.subtiles == 2 ||
                           (cfg_.subtiles < 0 && g_.dec.H / std::max(1, g_.dec.Py) >= kSubtileMinRows && L_.R >= 64);
         return want && !two_d() && !cfg_.compat && !cfg_.profile && !cfg_.force_split && L_.aligned() &&
-               cfg_.kernel != "lds" && cfg_.kernel != "tile";
+               cfg_.kernel != "lds" && cfg_.kernel != "tile" && cfg_.kernel != "pipe";
     }
     // Rank-local conditions (agreed over the ranks by the caller): a tile tall enough for two
     // halves, and memory for one more board pair.  (The halves always run the temporal kernel, at
@@ -357,6 +357,17 @@ class HipEngine : public Engine {
     }
 
     bool tile_kernel(int kind) const { return kern_[kind] == "tile"; }
+    // A pass of the level-pipelined workgroup kernel (step_pipe): its one depth (pipe_k_); the other
+    // passes of a superstep (remainders) of a "pipe" kind run step_temporal.
+    bool pipe_pass(int kind, int k) const { return kern_[kind] == "pipe" && pipe_k_ > 0 && k == pipe_k_; }
+    // Set the step_pipe geometry: nw waves per workgroup (one loader + nw - 1 stages of l generations),
+    // wg workgroups per CU in its plans.
+    void set_pipe(int nw, int l, int wg) {
+        pipe_nw_ = nw;
+        pipe_l_ = l;
+        pipe_wg_ = wg;
+        pipe_k_ = (nw - 1) * l;
+    }
 
     // Rounds of one-tile-per-CU the LDS tile kernel needs for a plan (cheap estimate, no plan).
     // Plans are explicit (one descriptor row per tile), so huge boards are left to step_temporal.
@@ -493,6 +504,8 @@ class HipEngine : public Engine {
     // tile kernel: one LDS buffer updated in place (1), double-buffered (0), or per plan (-1, auto)
     int tile_inplace_ = (int)env_int("GOL_TILE_INPLACE", -1);
     int tile_fold_ = (int)env_int("GOL_TILE_FOLD", -1);
+    int pipe_nw_ = 0, pipe_l_ = 0, pipe_wg_ = 0, pipe_k_ = 0;  // step_pipe geometry (set_pipe)
+    bool pipe_used_ = false;                                    // some pass ran step_pipe (fault check)
     int tile_lv_ = (int)env_int("GOL_TILE_LEVELS", 0);  // tile kernel: generations per LDS pass (1, 2, 4; 0 auto)
     bool multipass_ = false;
     std::map<int, std::vector<int>> passes_;

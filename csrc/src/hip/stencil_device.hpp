@@ -51,6 +51,38 @@ __device__ __forceinline__ void hsum_split(u32 lo, u32 hi, u32& s0lo, u32& s1lo,
     s1hi = b3<kLutMaj>(lo, hi, Ro);
 }
 
+// The K-level register pipeline of the streaming kernels (step_temporal, step_tile's band stream,
+// step_pipe's stages): level l keeps a 3-row window of horizontal sums and centre rows.
+template <int K>
+struct Pipe {
+    u32 s0[K][3][2];  // horizontal sum bit 0, per level, ring slot, half
+    u32 s1[K][3][2];  // horizontal sum bit 1
+    u32 x[K][3][2];   // the level's input rows (centre cells)
+};
+
+// Push one row (lo, hi) through the K levels.  Input index i (0-based within the segment's input
+// rows).  PH == i % 3 selects the ring slots at compile time.  Returns false while the pipeline is
+// still filling (GUARD instantiation only); otherwise (lo, hi) is the output row i - 2K.
+template <int K, int PH, bool GUARD>
+__device__ __forceinline__ bool advance(Pipe<K>& P, u32& lo, u32& hi, int i) {
+#pragma unroll
+    for (int l = 0; l < K; ++l) {
+        if (GUARD && i < 2 * l) return false;
+        const int s = (PH + l) % 3;     // slot of the arriving row
+        const int sp = (s + 2) % 3;     // previous row (centre of the output)
+        const int spp = (s + 1) % 3;    // two rows back
+        hsum_split(lo, hi, P.s0[l][s][0], P.s1[l][s][0], P.s0[l][s][1], P.s1[l][s][1]);
+        P.x[l][s][0] = lo;
+        P.x[l][s][1] = hi;
+        if (GUARD && i < 2 * l + 2) return false;
+        lo = rule32(P.s0[l][spp][0], P.s1[l][spp][0], P.s0[l][sp][0], P.s1[l][sp][0], P.s0[l][s][0],
+                    P.s1[l][s][0], P.x[l][sp][0]);
+        hi = rule32(P.s0[l][spp][1], P.s1[l][spp][1], P.s0[l][sp][1], P.s1[l][sp][1], P.s0[l][s][1],
+                    P.s1[l][s][1], P.x[l][sp][1]);
+    }
+    return true;
+}
+
 }  // namespace
 }  // namespace hipk
 }  // namespace gol

@@ -42,36 +42,6 @@ namespace hipk {
 
 namespace {
 
-template <int K>
-struct Pipe {
-    u32 s0[K][3][2];  // horizontal sum bit 0, per level, ring slot, half
-    u32 s1[K][3][2];  // horizontal sum bit 1
-    u32 x[K][3][2];   // the level's input rows (centre cells)
-};
-
-// Push one row (lo, hi) through the K levels.  Input index i (0-based within the segment's input
-// rows).  PH == i % 3 selects the ring slots at compile time.  Returns false while the pipeline is
-// still filling (GUARD instantiation only); otherwise (lo, hi) is the output row i - 2K.
-template <int K, int PH, bool GUARD>
-__device__ __forceinline__ bool advance(Pipe<K>& P, u32& lo, u32& hi, int i) {
-#pragma unroll
-    for (int l = 0; l < K; ++l) {
-        if (GUARD && i < 2 * l) return false;
-        const int s = (PH + l) % 3;     // slot of the arriving row
-        const int sp = (s + 2) % 3;     // previous row (centre of the output)
-        const int spp = (s + 1) % 3;    // two rows back
-        hsum_split(lo, hi, P.s0[l][s][0], P.s1[l][s][0], P.s0[l][s][1], P.s1[l][s][1]);
-        P.x[l][s][0] = lo;
-        P.x[l][s][1] = hi;
-        if (GUARD && i < 2 * l + 2) return false;
-        lo = rule32(P.s0[l][spp][0], P.s1[l][spp][0], P.s0[l][sp][0], P.s1[l][sp][0], P.s0[l][s][0],
-                    P.s1[l][s][0], P.x[l][sp][0]);
-        hi = rule32(P.s0[l][spp][1], P.s1[l][spp][1], P.s0[l][sp][1], P.s1[l][sp][1], P.s0[l][s][1],
-                    P.s1[l][s][1], P.x[l][sp][1]);
-    }
-    return true;
-}
-
 // Row prefetch: a register triple loaded one row-triple ahead, pinned above the compute with a
 // sched_barrier (otherwise the scheduler sinks the loads to the end of the loop body).  (An LDS
 // DMA ring and a skewed level pipeline were built and measured slower; docs/PERFORMANCE.md §2.)
@@ -878,7 +848,7 @@ void ensure_trash() {
     if (hipMalloc(&t, (size_t)kTrashWaves * 64 * sizeof(u64)) != hipSuccess) throw Error("ensure_trash: hipMalloc failed");
     g_trash[dev] = (u64*)t;
 }
-static u64* trash_of_current_device() {
+u64* trash_of_current_device() {
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64 || !g_trash[dev])
         throw Error("step kernels: the device's trash buffer is not allocated (hipk::ensure_trash)");

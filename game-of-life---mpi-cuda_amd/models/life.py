@@ -49,6 +49,9 @@ class Simulation:
                   the bit-sliced kernels implement.
     kernel_depth: generations per kernel pass (HIP; 0 = auto).  A superstep of halo_depth
                   generations runs as several kernel passes in 1-D (communication-avoiding halos).
+    kernel:       HIP stencil kernel: ``"auto"`` (candidates timed at init), ``"temporal"``,
+                  ``"tile"``, ``"pipe"`` (level-pipelined workgroups; geometry GOL_PIPE=nw,L,wg),
+                  ``"resident"`` or ``"lds"`` (GOL_KERNEL).
     decomp/grid:  ``"1d"`` row strips (reference) or ``"2d"`` blocks, optional ``"PxxPy"`` grid.
     width:        board columns (0 = N: the reference's square tiles).  With ``width`` the per-rank
                   strip (or, in global mode, the board) is N rows x ``width`` columns.

@@ -3,7 +3,8 @@
 //   hipcc --offload-arch=gfx950 -O3 -Icsrc/include [variant flags] tools/kbench.cpp \
 //         csrc/src/hip/step_kernels.hip csrc/src/hip/aux_kernels.hip csrc/src/core/plan.cpp \
 //         csrc/src/core/geometry.cpp csrc/src/core/config.cpp -o build/kbench_<variant>
-//   build/kbench_<variant> [N=32768] [K=8] [gens=960] [pf=0|1]
+//   build/kbench_<variant> [N=32768] [K=8] [gens=960] [pf=0|1] [skew] [tile_nw] [rows] [tile_lv]
+//   (KB_PIPE=L with tile_nw = NW: step_pipe, K = (NW - 1) L)
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -57,6 +58,14 @@ int main(int argc, char** argv) {
     CK(hipGetDeviceProperties(&prop, 0));
     const int tile_lv = argc > 8 ? atoi(argv[8]) : 1;  // tile kernel: generations per LDS pass
     const bool fold = tile_nw > 0 && getenv("KB_FOLD") && atoi(getenv("KB_FOLD"));  // folded 32-lane tiles
+    // KB_PIPE=L: step_pipe with tile_nw waves (one loader + tile_nw - 1 stages of L generations; K must
+    // be (tile_nw - 1) L), KB_PIPE_WG workgroups per CU in the plan (default 1)
+    const int pipe_l = tile_nw > 0 && getenv("KB_PIPE") ? atoi(getenv("KB_PIPE")) : 0;
+    const int pipe_wg = getenv("KB_PIPE_WG") ? atoi(getenv("KB_PIPE_WG")) : 1;
+    if (pipe_l > 0 && K != (tile_nw - 1) * pipe_l) {
+        fprintf(stderr, "KB_PIPE: K must be (tile_nw - 1) x L = %d\n", (tile_nw - 1) * pipe_l);
+        return 1;
+    }
     (void)pf;
     (void)skew;  // the LDS-ring prefetch and skewed pipeline variants were removed (measured slower)
     const u32 flags = hipk::STEP_WRAP_Y |
@@ -65,7 +74,9 @@ int main(int argc, char** argv) {
                       (fold ? hipk::STEP_TILE_FOLD : 0u);
     std::vector<Region> rg = {{0, N, 0, L.nw}};
     i64 rows = rows_arg;
-    if (tile_nw > 0) {
+    if (pipe_l > 0) {
+        if (rows <= 0) rows = balanced_rows_per_chunk(rg, L.nw, N, K, (i64)pipe_wg * prop.multiProcessorCount, 1, true);
+    } else if (tile_nw > 0) {
         const i64 rmax = hipk::tile_max_rows(K, tile_nw, flags);
         if (rows > rmax) rows = rmax;
         for (i64 rounds = 1; rows <= 0; ++rounds) {
@@ -123,7 +134,9 @@ int main(int argc, char** argv) {
     auto launch = [&](const u64* s, u64* d) {
         if (split2) {
             for (int h = 0; h < nparts; ++h) hipk::launch_step(K, s, d, dplan2[h], waves2[h], sp, ss[h]);
-        } else if (tile_nw > 0)
+        } else if (pipe_l > 0)
+            hipk::launch_step_pipe(tile_nw, pipe_l, s, d, dplan, st.waves, sp, 0);
+        else if (tile_nw > 0)
             hipk::launch_step_tile(tile_nw, K, s, d, dplan, st.waves, rows, sp, 0);
         else
             hipk::launch_step(K, s, d, dplan, st.waves, sp, 0);
@@ -156,6 +169,10 @@ int main(int argc, char** argv) {
         if (ms < best) best = ms;
     }
     CK(hipGetLastError());
+    if (pipe_l > 0 && hipk::pipe_fault()) {
+        fprintf(stderr, "step_pipe: a ring wait timed out\n");
+        return 3;
+    }
 #ifdef GOL_TILE_STAMPS
     if (tile_nw > 0) {  // time breakdown of the last launch: cycles from the kernel start, median over workgroups
         const int slots = 48;
@@ -209,7 +226,7 @@ int main(int argc, char** argv) {
         if (bad) return 2;
     }
     const double per_gen_us = best * 1e3 / (steps * K);
-    const int bpc = tile_nw > 0 ? hipk::tile_blocks_per_cu(tile_nw, rows, K, flags) : hipk::step_blocks_per_cu(K, flags);
+    const int bpc = pipe_l > 0 ? hipk::pipe_blocks_per_cu(tile_nw, pipe_l, true) : tile_nw > 0 ? hipk::tile_blocks_per_cu(tile_nw, rows, K, flags) : hipk::step_blocks_per_cu(K, flags);
     printf("{\"N\": %lld, \"K\": %d, \"skew\": %d, \"pf\": %d, \"tile_nw\": %d, \"rows\": %lld, \"waves\": %lld, "
            "\"blocks_per_cu\": %d, \"us_per_gen\": %.3f, \"cells_per_s\": %.4e}\n",
            (long long)N, K, skew, pf, tile_nw, (long long)rows, (long long)st.waves, bpc, per_gen_us,
