@@ -312,7 +312,7 @@ void HipEngine::do_init(const PatternSpec& p) {
         events_needed_ = cfg_.force_split || (split_ && !halo_items(L_.R).empty()) ||
                          env_str("GOL_READY_EVENTS", "") == "always";
     }
-    stats_.kernel = split_ ? kern_[1] + "+boundary:" + kern_[2] : kern_[0];
+    stats_.kernel = split_ ? kern_[1] + "+boundary:" + kern_[2] : (dual_ ? std::string("temporal") : kern_[0]);
     if (!split_ && !dual_ && kern_[0] == "pipe")
         stats_.kernel = strprintf("pipe@%d(%dx%d,%d/CU)", pipe_k_, pipe_nw_ - 1, pipe_l_, pipe_wg_);
     if (res_) {
@@ -321,7 +321,7 @@ void HipEngine::do_init(const PatternSpec& p) {
     }
     stats_.schedule = split_ ? "split" : (halo_items(L_.R).empty() ? "local" : "full");
     if (dual_) stats_.schedule += sub_overlap_ == 2 ? "+subtiles2ov2" : (sub_overlap_ ? "+subtiles2ov" : "+subtiles2");
-    stats_.kernel_depth = kdepth_;
+    stats_.kernel_depth = dual_ ? tdepth_ : kdepth_;
     stats_.tile_waves = cfg_.tile_waves;
     std::string tn;
     for (const auto& kv : tune_ms_) tn += strprintf("%s%s=%.3fus/gen", tn.empty() ? "" : " ", kv.first.c_str(), kv.second * 1e3);

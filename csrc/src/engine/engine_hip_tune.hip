@@ -15,8 +15,15 @@ void HipEngine::spin_up() {
     const double budget_ms = (double)env_int("GOL_SPINUP_MS", big ? 100 : 20);
     if (budget_ms <= 0 || cfg_.compat || kernel_ == "lds") return;
     const std::string saved = kern_[0];
-    if (cfg_.kernel != "tile") kern_[0] = "temporal";  // the register kernel runs on any board
-    const int k = tile_kernel(0) ? kdepth_ : supported_kernel_depth(std::min(kdepth_, hipk::max_step_depth()));
+    int k = 0;
+    if (!dual_ && kern_[0] == "pipe" && pipe_k_ > 0) {
+        k = pipe_k_;  // the kernel the runs use
+    } else {
+        if (cfg_.kernel != "tile") kern_[0] = "temporal";  // the register kernel runs on any board
+        // (sub-tiles: their own pass depth; a deep full-tile depth, e.g. a pipe candidate's 36, would
+        // spin the GPU up on a 1-wave-per-SIMD kernel of a different power draw)
+        k = tile_kernel(0) ? kdepth_ : supported_kernel_depth(std::min(dual_ ? tdepth_ : kdepth_, hipk::max_step_depth()));
+    }
     const auto t0 = std::chrono::steady_clock::now();
     for (int it = 0; it < 100000; ++it) {
         for (int j = 0; j < 4; ++j) launch(0, k, 0, buf_[cur_], buf_[cur_ ^ 1], s_comp_);
