@@ -140,6 +140,15 @@ def main() -> int:
     else:
         transport = native.SelfTransport()
 
+    import torch
+
+    use_torch_sync = backend == "hip" and torch.cuda.is_available()
+    if use_torch_sync:
+        # torch's lazy device initialisation (its first synchronize) before the engine's init: the
+        # engine's init ends by spinning the GPU up to its steady clock (GOL_SPINUP_MS), and the
+        # warmup and timed run should follow it without an idle gap
+        torch.cuda.synchronize()
+
     t_init = time.perf_counter()
     sim = gol_amd.Simulation(
         size,
@@ -170,17 +179,11 @@ def main() -> int:
     dec = sim.decomposition
     cells = dec.H * dec.W
 
-    import torch
-
-    use_torch_sync = backend == "hip" and torch.cuda.is_available()
-
     def device_sync():
         sim.synchronize()  # the engine's own HIP streams (watchdog-armed)
         if use_torch_sync:
             torch.cuda.synchronize()
 
-    # torch's lazy device initialisation (the first torch.cuda.synchronize) takes ~1 ms: do it before
-    # the warmup, so the GPU goes from the warmup straight into the timed region
     device_sync()
     sim.step(warmup)
     device_sync()
