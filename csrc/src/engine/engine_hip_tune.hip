@@ -326,7 +326,12 @@ void HipEngine::autotune_kernel() {
         HIP_CHECK(hipEventSynchronize(e1));
         float ms = 0;
         HIP_CHECK(hipEventElapsedTime(&ms, e0, e1));
-        const float per_gen = ms / 3 / (float)k;
+        float per_gen = ms / 3 / (float)k;
+        if (pipe && hipk::pipe_fault()) {  // a ring wait timed out: never pick this geometry
+            fprintf(stderr, "[gol] step_pipe %dx%d: a ring wait timed out in the kernel autotune; candidate dropped\n",
+                    pipe_nw_ - 1, pipe_l_);
+            per_gen = 1e30f;
+        }
         const std::string key = tile   ? strprintf("%d:%s@%dx%dw", kind, kern, k, cfg_.tile_waves)
                                 : pipe ? strprintf("%d:pipe@%d(%dx%d,%d/CU)", kind, k, pipe_nw_ - 1, pipe_l_, pipe_wg_)
                                 : occ_ ? strprintf("%d:%s@%d/%dw", kind, kern, k, occ_)
@@ -437,6 +442,7 @@ void HipEngine::autotune_kernel() {
     HIP_CHECK(hipEventDestroy(e0));
     HIP_CHECK(hipEventDestroy(e1));
     kernel_ = kern_[0];
+    pipe_used_ = false;  // (the candidates ran on scratch; faults were checked above)
     // The resident kernel (small boards without neighbours): one launch per run, halos exchanged
     // between tiles inside the kernel every kin generations.  Timed on launches of the hinted run's
     // length (at most 256 generations) against the best pass kernel above.
