@@ -336,8 +336,10 @@ __device__ __forceinline__ void stage(RingIn<RIN>& in, Out& out, int n) {
 }
 
 // NW waves: wave 0 loads, waves 1 .. NW-1 compute L generations each (K = (NW - 1) L per pass).
+// At most 102 VGPRs (5 waves per SIMD): two workgroups of 9 waves per CU at any L (unbounded, L = 4
+// took 167 VGPRs and ran one workgroup per CU)
 template <int NW, int L, bool WRAPY>
-__global__ __launch_bounds__(64 * NW) void step_pipe(const u64* __restrict__ src, u64* __restrict__ dst,
+__global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(5))) void step_pipe(const u64* __restrict__ src, u64* __restrict__ dst,
                                                      const LaneDesc* __restrict__ plan, StepParams p) {
     // Progress (no wait cycle): a consumer that has released rows < c waits for at most rows < c + kPipeU
     // (+ the producer's publish group of 3); the producer of those rows needs slots of rows < c + kPipeU + 3
