@@ -598,8 +598,32 @@ for l in sys.stdin:
     d=json.loads(l); c=d['config']; print(c['board'][0], round(d['ms_per_step']*1e3,3), c['kernel'], c['kernel_depth'], c['autotune'][:150])"
 }
 
+cmd_oneshot() {
+# Round 3: one-shot full-board passes at 32768^2 (one launch per timed rep, best of 3): the pass kernels a
+# 20-generation run could use, temporal K=8/12 and step_pipe geometries (NW x L at 1-2 workgroups per CU).
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out/oneshot
+out=gpurun_out/oneshot/oneshot.txt; : > $out
+kb=build/kbench_${1:-default}
+for rep in 1 2; do
+  for spec in "t:8" "t:12" "t:16" "p:9:3:2" "p:9:3:1" "p:11:2:1" "p:11:2:2" "p:5:4:2" "p:9:2:2" "p:13:2:1" "p:9:32:2" "p:9:32:1"; do
+    IFS=: read kind a b c <<< "$spec"
+    if [ $kind = t ]; then
+      r=$(timeout -k 5 60 $kb 32768 $a $a) || exit 3
+    else
+      if [ $b -ge 10 ]; then k=$(( (a - 1) / 2 * (b / 10) + (a - 1 - (a - 1) / 2) * (b % 10) )); else k=$(( (a - 1) * b )); fi
+      r=$(KB_PIPE=$b KB_PIPE_WG=$c timeout -k 5 60 $kb 32768 $k $k 0 0 $a) || exit 3
+    fi
+    echo "$spec $r" | python3 -c "
+import sys,json
+l=sys.stdin.read(); sp,js=l.split(' ',1); d=json.loads(js)
+print(sp, 'K', d['K'], 'pass_us', round(d['us_per_gen']*d['K'],1), 'us_per_gen', d['us_per_gen'], 'bpc', d['blocks_per_cu'])" | tee -a $out
+  done
+done
+}
+
 name=${1:-}; shift || true
 if ! declare -F "cmd_$name" >/dev/null; then
-  echo "usage: $0 <name> [args]; names: cfg2_check cfg2_steps_ab cfg2_sweep cfg2_trace cfg2_warmup_ab driver_trace events_ab fold_ab fold_check fold_depth fold_strip kb_ab kb_bperm kb_depth_sweep kb_occ_sweep kb_rounds kb_split2 kb_tile_sweep occ_check pmc_fold pmc_k7 pmc_k7_after pmc_temporal pmc_tile pmc_tile_round2 power_probe prof_ab split_bench split_cost split_cost_r split_trace subtiles_check subtiles_check2 subtiles_occ subtiles_r128 sync_spin_ab tune_check" >&2; exit 2
+  echo "usage: $0 <name> [args]; names: oneshot cfg2_check cfg2_steps_ab cfg2_sweep cfg2_trace cfg2_warmup_ab driver_trace events_ab fold_ab fold_check fold_depth fold_strip kb_ab kb_bperm kb_depth_sweep kb_occ_sweep kb_rounds kb_split2 kb_tile_sweep occ_check pmc_fold pmc_k7 pmc_k7_after pmc_temporal pmc_tile pmc_tile_round2 power_probe prof_ab split_bench split_cost split_cost_r split_trace subtiles_check subtiles_check2 subtiles_occ subtiles_r128 sync_spin_ab tune_check" >&2; exit 2
 fi
 "cmd_$name" "$@"
