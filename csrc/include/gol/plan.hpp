@@ -87,6 +87,18 @@ i64 choose_rows_per_chunk(const std::vector<Region>& regions, int k, i64 target_
 i64 balanced_rows_per_chunk(const std::vector<Region>& regions, i64 nw, i64 h, int k, i64 resident_waves,
                             i64 min_rows, bool xwrap, bool fold = false);
 
+// Segment height for the streaming kernel on BIG regions: one round (balanced_rows_per_chunk) while its
+// segments are at most about `round_rows` tall, otherwise the whole number of rounds (at most
+// `max_rounds`) that brings them nearest to it.  Waves of one round start together and stream equal
+// work, but they do not finish together (the co-resident waves of a SIMD compete for issue), and a
+// one-round pass ends on its slowest wave; with several rounds a finished wave's slot takes the next
+// segment, at the price of 2k halo rows per extra segment.  Measured, K = 8, one tile, kbench
+// (profiles/bigboard_rounds.txt): 131072^2 one round (1425 rows) 163 us/gen, 2 rounds 149.4-150, 4
+// rounds (360 rows) 145-145.6, 8 rounds 145.7-147.3; 65536^2 keeps one round (365 rows; 2 rounds of
+// 180: 46.7 vs 44.8-45.8).  round_rows <= 0 disables it (one round).
+i64 round_balanced_rows(const std::vector<Region>& regions, i64 nw, i64 h, int k, i64 resident_waves, i64 min_rows,
+                        bool xwrap, i64 round_rows, i64 max_rounds = 32);
+
 // Neighbour tiles of a resident plan (hip_kernels.hpp step_resident: one plan wave = one tile, kept
 // by one workgroup for a whole run).  Tile t reads, for each of its lanes, rows [row0-k, row0+nrows+k)
 // of the lane's word column (modulo h with wrap_y); its neighbours are the OTHER tiles whose store

@@ -59,6 +59,15 @@ i64 balanced_rows_per_chunk(const std::vector<Region>& regions, i64 nw, i64 h, i
     return hi;
 }
 
+i64 round_balanced_rows(const std::vector<Region>& regions, i64 nw, i64 h, int k, i64 resident_waves, i64 min_rows,
+                        bool xwrap, i64 round_rows, i64 max_rounds) {
+    const i64 r1 = balanced_rows_per_chunk(regions, nw, h, k, resident_waves, min_rows, xwrap);
+    if (round_rows <= 0 || r1 < 2 * round_rows) return r1;  // (rounds would be 1)
+    const i64 rounds = std::max<i64>(1, std::min<i64>(max_rounds, (r1 + round_rows / 2) / round_rows));
+    // the tallest segments whose plan fits `rounds` full rounds of resident waves
+    return balanced_rows_per_chunk(regions, nw, h, k, rounds * resident_waves, min_rows, xwrap);
+}
+
 namespace {
 
 // Cut the regions into segments of <= rows_per_chunk rows x <= 62 words and pack them into waves:

@@ -188,7 +188,8 @@ const DevPlan& HipEngine::plan(int kind, int k, i64 e) {
             // only (shallower passes are memory bound and want every resident wave)
             if (occ_ > 0 && k == kdepth_) bpc = std::min<i64>(bpc, occ_);
             const i64 resident = bpc * kWavesPerBlock * cus_;
-            rows = balanced_rows_per_chunk(rg, L_.nw, L_.h, k, resident, 2 * (i64)k, xwrap_by_plan());
+            // big tiles: several rounds of segments near round_rows() rows (plan.hpp round_balanced_rows)
+            rows = round_balanced_rows(rg, L_.nw, L_.h, k, resident, 2 * (i64)k, xwrap_by_plan(), round_rows(k));
         }
     }
     std::vector<LaneDesc> lanes = build_plan(rg, L_.nw, L_.h, rows, k, xwrap_by_plan(), &p.st,

@@ -502,6 +502,10 @@ class HipEngine : public Engine {
     // waves can win there; the autotuner tries 2 per SIMD against the full occupancy (3 at K=8).
     int occ_ = 0;
     // tile kernel: one LDS buffer updated in place (1), double-buffered (0), or per plan (-1, auto)
+    // Streaming-kernel segment height beyond which a plan takes several rounds (plan.hpp
+    // round_balanced_rows): GOL_ROUND_ROWS_PER_LEVEL (default 45) x the pass depth; 0 = one round always
+    i64 round_rows_per_level_ = env_int("GOL_ROUND_ROWS_PER_LEVEL", 45);
+    i64 round_rows(int k) const { return round_rows_per_level_ > 0 ? round_rows_per_level_ * k : 0; }
     int tile_inplace_ = (int)env_int("GOL_TILE_INPLACE", -1);
     int tile_fold_ = (int)env_int("GOL_TILE_FOLD", -1);
     int pipe_nw_ = 0, pipe_l_ = 0, pipe_wg_ = 0, pipe_k_ = 0;  // step_pipe geometry (set_pipe)

@@ -509,8 +509,45 @@ static void test_resident() {
     CHECK(!resident_neighbours(lanes, 3, 40, 2, true, off, idx).empty());
 }
 
+// Multi-round segment heights for big regions (plan.hpp round_balanced_rows): small regions keep the
+// one-round height; big ones get a whole number of full rounds with segments near round_rows.
+static void test_plan_rounds() {
+    const i64 resident = 3 * 4 * 256;  // 3 waves per SIMD on 256 CUs
+    {
+        const i64 h = 32768, nw = 512;
+        std::vector<Region> rg = {{0, h, 0, nw}};
+        const i64 r1 = balanced_rows_per_chunk(rg, nw, h, 8, resident, 16, true);
+        CHECK(round_balanced_rows(rg, nw, h, 8, resident, 16, true, 360) == r1);  // one round: ~97 rows
+    }
+    {
+        const i64 h = 65536, nw = 1024;  // one round is ~365 rows: stays one round
+        std::vector<Region> rg = {{0, h, 0, nw}};
+        const i64 r1 = balanced_rows_per_chunk(rg, nw, h, 8, resident, 16, true);
+        CHECK(round_balanced_rows(rg, nw, h, 8, resident, 16, true, 360) == r1);
+    }
+    {
+        const i64 h = 131072, nw = 2048;  // one round is ~1425 rows: four rounds of ~360
+        std::vector<Region> rg = {{0, h, 0, nw}};
+        const i64 r1 = balanced_rows_per_chunk(rg, nw, h, 8, resident, 16, true);
+        const i64 r4 = round_balanced_rows(rg, nw, h, 8, resident, 16, true, 360);
+        CHECK(r1 > 1300 && r4 < r1);
+        CHECK(r4 >= 330 && r4 <= 400);
+        CHECK(plan_waves(rg, nw, h, r4) <= 4 * resident && plan_waves(rg, nw, h, r4) > 3 * resident);
+        CHECK(round_balanced_rows(rg, nw, h, 8, resident, 16, true, 0) == r1);  // disabled
+        // at most max_rounds rounds
+        const i64 r2 = round_balanced_rows(rg, nw, h, 8, resident, 16, true, 90, 2);
+        CHECK(plan_waves(rg, nw, h, r2) <= 2 * resident && plan_waves(rg, nw, h, r2) > resident);
+        // the plan still covers every output word exactly once
+        PlanStats st;
+        std::vector<LaneDesc> lanes = build_plan(rg, nw, h, r4, 8, true, &st, 4, 8);
+        CHECK(validate_plan(lanes, nw, h, 8, 8, true).empty());
+        CHECK(st.out_words == h * nw);
+    }
+}
+
 int main() {
     test_watchdog();
+    test_plan_rounds();
     test_cli();
     test_geometry();
     test_patterns();

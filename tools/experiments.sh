@@ -622,8 +622,53 @@ print(sp, 'K', d['K'], 'pass_us', round(d['us_per_gen']*d['K'],1), 'us_per_gen',
 done
 }
 
+cmd_bigboard_rounds() {
+# Round 3: one-tile K=8 passes on big boards, kbench: one-round plan (default rows) vs multi-round plans (fewer rows per
+# wave) vs two concurrent half-board kernels on two streams (KB_SPLIT2=1, no cross-stream ordering: an upper bound).
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out/bigb
+out=gpurun_out/bigb/bigboard_rounds.txt; : > $out
+kb=build/kbench_${1:-default}
+for rep in 1 2; do
+  for n in 65536 131072; do
+    for rows in 0 720 360 180; do
+      r=$(timeout -k 5 120 $kb $n 8 64 0 0 0 $rows) || exit 3
+      echo "N=$n rows=$rows $r" | tee -a $out
+    done
+    r=$(KB_SPLIT2=1 timeout -k 5 120 $kb $n 8 64) || exit 3
+    echo "N=$n split2 $r" | tee -a $out
+  done
+done
+}
+
+cmd_rounds_engine() {
+# Round 3: the engine with multi-round plans for big tiles (default, GOL_ROUND_ROWS_PER_LEVEL=45) vs one round (=0):
+# bench.py at 131072^2 and BASELINE config 5 (2^20 x 2^20, 256 GB of boards), alternating; the driver command as a check.
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out/rounds
+out=gpurun_out/rounds/rounds_engine.txt; : > $out
+summ() { grep '^{' "$1" | python3 -c "
+import sys,json
+d=json.loads(sys.stdin.read()); c=d['config']
+print('$2', c['board'][0], round(d['ms_per_step']*1e3,3), 'us/gen', '%.4e'%d['value'], c['schedule'], 'plan_waves', c['plan_waves'], c['autotune'][:120])" | tee -a $out; }
+for rep in 1 2; do
+  for v in 45 0; do
+    GOL_ROUND_ROWS_PER_LEVEL=$v timeout -k 10 240 python bench.py --size 131072 --steps 256 --warmup 32 > gpurun_out/rounds/b131k_$v.log 2>&1 || exit 3
+    summ gpurun_out/rounds/b131k_$v.log "rr=$v"
+  done
+done
+for v in 45 0; do
+  GOL_ROUND_ROWS_PER_LEVEL=$v timeout -k 10 400 python bench.py --size 1048576 --steps 16 --warmup 8 > gpurun_out/rounds/b1m_$v.log 2>&1 || exit 3
+  summ gpurun_out/rounds/b1m_$v.log "rr=$v"
+done
+for i in 1 2; do
+  timeout -k 10 120 python bench.py --gpus 1 --steps 20 --warmup 5 > gpurun_out/rounds/drv.log 2>&1 || exit 3
+  summ gpurun_out/rounds/drv.log driver
+done
+}
+
 name=${1:-}; shift || true
 if ! declare -F "cmd_$name" >/dev/null; then
-  echo "usage: $0 <name> [args]; names: oneshot cfg2_check cfg2_steps_ab cfg2_sweep cfg2_trace cfg2_warmup_ab driver_trace events_ab fold_ab fold_check fold_depth fold_strip kb_ab kb_bperm kb_depth_sweep kb_occ_sweep kb_rounds kb_split2 kb_tile_sweep occ_check pmc_fold pmc_k7 pmc_k7_after pmc_temporal pmc_tile pmc_tile_round2 power_probe prof_ab split_bench split_cost split_cost_r split_trace subtiles_check subtiles_check2 subtiles_occ subtiles_r128 sync_spin_ab tune_check" >&2; exit 2
+  echo "usage: $0 <name> [args]; names: rounds_engine oneshot bigboard_rounds cfg2_check cfg2_steps_ab cfg2_sweep cfg2_trace cfg2_warmup_ab driver_trace events_ab fold_ab fold_check fold_depth fold_strip kb_ab kb_bperm kb_depth_sweep kb_occ_sweep kb_rounds kb_split2 kb_tile_sweep occ_check pmc_fold pmc_k7 pmc_k7_after pmc_temporal pmc_tile pmc_tile_round2 power_probe prof_ab split_bench split_cost split_cost_r split_trace subtiles_check subtiles_check2 subtiles_occ subtiles_r128 sync_spin_ab tune_check" >&2; exit 2
 fi
 "cmd_$name" "$@"
