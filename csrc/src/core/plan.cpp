@@ -45,13 +45,29 @@ i64 balanced_rows_per_chunk(const std::vector<Region>& regions, i64 nw, i64 h, i
     for (const Region& r : regions) max_rows = std::max(max_rows, r.r1 - r.r0);
     (void)k;
     (void)xwrap;
-    auto waves = [&](i64 S) { return plan_waves(regions, nw, h, S, fold); };
+    // fits(S): the plan of S-row segments has at most resident_waves waves.  The full-width segments
+    // alone (one wave each) bound the count from below, so a height whose bound already exceeds the
+    // target is rejected without packing the plan: packing materialises every segment, which for
+    // short segments of a big tile is hundreds of millions of them (a 2^20-row board's search used to
+    // start by packing 1-row segments and spent minutes in the kernel autotune).
+    const i64 lw = pack_lanes(fold), sw = lw - 2;
+    auto fits = [&](i64 S) {
+        double full = 0, narrow_lanes = 0;  // (narrow segments: their lanes incl. 2 halo lanes, packed <= lw per wave)
+        for (const Region& r : regions) {
+            const i64 rows = r.r1 - r.r0, words = r.c1 - r.c0;
+            if (rows <= 0 || words <= 0) continue;
+            full += (double)ceil_div(rows, S) * (double)(words / sw);
+            if (words % sw) narrow_lanes += (double)ceil_div(rows, S) * (double)(words % sw + 2);
+        }
+        if (full + narrow_lanes / (double)lw > (double)resident_waves) return false;
+        return plan_waves(regions, nw, h, S, fold) <= resident_waves;
+    };
     i64 lo = std::max<i64>(1, std::min(min_rows, max_rows)), hi = max_rows;
-    if (waves(lo) <= resident_waves) return lo;
-    if (waves(hi) > resident_waves) return hi;  // cannot fit one round: fewest, tallest segments
-    while (hi - lo > 1) {  // waves(lo) > target >= waves(hi)
+    if (fits(lo)) return lo;
+    if (!fits(hi)) return hi;  // cannot fit one round: fewest, tallest segments
+    while (hi - lo > 1) {  // !fits(lo), fits(hi)
         i64 mid = (lo + hi) / 2;
-        if (waves(mid) <= resident_waves)
+        if (fits(mid))
             hi = mid;
         else
             lo = mid;

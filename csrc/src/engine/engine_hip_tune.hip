@@ -108,6 +108,7 @@ void HipEngine::measure_pass_costs() {
             HIP_CHECK(hipEventElapsedTime(&ms, e0, e1));
             const double us = ms * 1e3 / reps;
             best[d] = round == 0 ? us : std::min(best[d], us);
+            init_step("init: pass costs", "pass", d, (float)(us / d));
         }
     HIP_CHECK(hipEventDestroy(e0));
     HIP_CHECK(hipEventDestroy(e1));
@@ -174,6 +175,7 @@ void HipEngine::choose_schedule() {
                 synchronize();
                 const double dt = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
                 best[c] = std::min(best[c], t_->allreduce_max(dt) * 1e6 / (reps * k));
+                init_step("init: schedule timing", cands[c].c_str(), k, (float)best[c]);
             }
         const bool graph_failed = t_->allreduce_max(sched_graph_failed_ ? 1.0 : 0.0) > 0;
         size_t bi = 0;
@@ -327,6 +329,7 @@ void HipEngine::autotune_kernel() {
         float ms = 0;
         HIP_CHECK(hipEventElapsedTime(&ms, e0, e1));
         float per_gen = ms / 3 / (float)k;
+        init_step("init: kernel autotune", kern, k, per_gen);
         if (pipe && hipk::pipe_fault()) {  // a ring wait timed out: never pick this geometry
             fprintf(stderr, "[gol] step_pipe %dx%d: a ring wait timed out in the kernel autotune; candidate dropped\n",
                     pipe_nw_ - 1, pipe_l_);

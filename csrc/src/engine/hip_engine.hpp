@@ -502,6 +502,17 @@ class HipEngine : public Engine {
     // waves can win there; the autotuner tries 2 per SIMD against the full occupancy (3 at K=8).
     int occ_ = 0;
     // tile kernel: one LDS buffer updated in place (1), double-buffered (0), or per plan (-1, auto)
+    // One timed step of the init measurements is done: progress for the watchdog (a big board's
+    // autotune can take longer than its timeout in total), and with GOL_INIT_LOG=1 a line on stderr.
+    const bool init_log_ = env_int("GOL_INIT_LOG", 0) != 0;
+    const std::chrono::steady_clock::time_point init_t0_ = std::chrono::steady_clock::now();
+    void init_step(const char* phase, const char* what, int k, float us_per_gen) {
+        if (wd_) wd_->kick(phase);
+        if (init_log_)
+            fprintf(stderr, "[gol] rank %d init %.2f s: %s %s@%d %.3f us/gen\n", g_.rank,
+                    std::chrono::duration<double>(std::chrono::steady_clock::now() - init_t0_).count(), phase, what, k,
+                    us_per_gen);
+    }
     // Streaming-kernel segment height beyond which a plan takes several rounds (plan.hpp
     // round_balanced_rows): GOL_ROUND_ROWS_PER_LEVEL (default 45) x the pass depth; 0 = one round always
     i64 round_rows_per_level_ = env_int("GOL_ROUND_ROWS_PER_LEVEL", 45);

@@ -1,3 +1,4 @@
+#include <chrono>
 // gol-mi355x: host-side C++ unit tests (no GPU needed).  Run: build/gol_unit
 //
 // Covers: CLI parsing, decomposition geometry, pattern placement (survey §2.9), planner coverage,
@@ -542,6 +543,19 @@ static void test_plan_rounds() {
         std::vector<LaneDesc> lanes = build_plan(rg, nw, h, r4, 8, true, &st, 4, 8);
         CHECK(validate_plan(lanes, nw, h, 8, 8, true).empty());
         CHECK(st.out_words == h * nw);
+    }
+    {
+        // BASELINE config 5's 2^20 x 2^20 tile: the row search of a 512-workgroup plan from 1-row
+        // segments up must not pack the candidate plans it can reject by counting (it took minutes)
+        const i64 h = 1 << 20, nw = 1 << 14;
+        std::vector<Region> rg = {{0, h, 0, nw}};
+        const auto t0 = std::chrono::steady_clock::now();
+        const i64 r = balanced_rows_per_chunk(rg, nw, h, 24, 512, 1, true);
+        const i64 r32 = round_balanced_rows(rg, nw, h, 8, resident, 16, true, 360);
+        const double s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+        CHECK(s < 10.0);
+        CHECK(r > 500000 && plan_waves(rg, nw, h, r) <= 512);
+        CHECK(plan_waves(rg, nw, h, r32) <= 32 * resident && plan_waves(rg, nw, h, r32) > 31 * resident);
     }
 }
 
