@@ -76,9 +76,10 @@ const DevPlan& HipEngine::sub_plan(int s, int k, i64 e, int part) {
     // A band (part 2) is a few rows tall and runs while little else does: its time is the serial
     // level pipeline of one wave, ~(S + K) x K row-levels for S rows per wave, so it is cut into
     // 4-row segments (K = 12, 28-row band: ~38 us as one segment per column, ~14 us in 4-row ones).
+    // One round per half even on big tiles: the two halves' kernels already fill each other's tails
+    // (131072^2: multi-round halves 141.9-142.4 vs 140.2-141.0 us/gen, profiles/bigboard_rounds.txt).
     const i64 rows = part == 2 ? 4
-                               : round_balanced_rows(rg, L.nw, L.h, k, bpc * kWavesPerBlock * cus_, 2 * (i64)k, true,
-                                                     round_rows(k));
+                               : balanced_rows_per_chunk(rg, L.nw, L.h, k, bpc * kWavesPerBlock * cus_, 2 * (i64)k, true);
     DevPlan p;
     std::vector<LaneDesc> lanes = build_plan(rg, L.nw, L.h, rows, k, true, &p.st, kWavesPerBlock, cfg_.plan_xcds);
     const std::string bad = validate_plan(lanes, L.nw, L.h, L.R, k, false);

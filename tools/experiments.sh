@@ -643,23 +643,24 @@ done
 
 cmd_rounds_engine() {
 # Round 3: the engine with multi-round plans for big tiles (default, GOL_ROUND_ROWS_PER_LEVEL=45) vs one round (=0):
-# bench.py at 131072^2 and BASELINE config 5 (2^20 x 2^20, 256 GB of boards), alternating; the driver command as a check.
+# bench.py at 131072^2 with one tile (GOL_SUBTILES=0) and BASELINE config 5 (2^20 x 2^20, 256 GB of boards); the driver
+# command as a check.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out/rounds
 out=gpurun_out/rounds/rounds_engine.txt; : > $out
 summ() { grep '^{' "$1" | python3 -c "
 import sys,json
 d=json.loads(sys.stdin.read()); c=d['config']
-print('$2', c['board'][0], round(d['ms_per_step']*1e3,3), 'us/gen', '%.4e'%d['value'], c['schedule'], 'plan_waves', c['plan_waves'], c['autotune'][:120])" | tee -a $out; }
+print('$2', c['board'][0], round(d['ms_per_step']*1e3,3), 'us/gen', '%.4e'%d['value'], c['schedule'], 'plan_waves', c['plan_waves'], 'init_s', d['timing']['init_s'], c['autotune'][:160])" | tee -a $out; }
 for rep in 1 2; do
   for v in 45 0; do
-    GOL_ROUND_ROWS_PER_LEVEL=$v timeout -k 10 240 python bench.py --size 131072 --steps 256 --warmup 32 > gpurun_out/rounds/b131k_$v.log 2>&1 || exit 3
-    summ gpurun_out/rounds/b131k_$v.log "rr=$v"
+    GOL_SUBTILES=0 GOL_ROUND_ROWS_PER_LEVEL=$v timeout -k 10 240 python bench.py --size 131072 --steps 256 --warmup 32 > gpurun_out/rounds/b131k_$v.log 2>&1 || exit 3
+    summ gpurun_out/rounds/b131k_$v.log "onetile rr=$v"
   done
 done
 for v in 45 0; do
-  GOL_ROUND_ROWS_PER_LEVEL=$v timeout -k 10 400 python bench.py --size 1048576 --steps 16 --warmup 8 > gpurun_out/rounds/b1m_$v.log 2>&1 || exit 3
-  summ gpurun_out/rounds/b1m_$v.log "rr=$v"
+  GOL_INIT_LOG=1 GOL_ROUND_ROWS_PER_LEVEL=$v timeout -k 10 400 python bench.py --size 1048576 --steps 16 --warmup 8 > gpurun_out/rounds/b1m_$v.log 2>&1 || exit 3
+  summ gpurun_out/rounds/b1m_$v.log "cfg5 rr=$v"
 done
 for i in 1 2; do
   timeout -k 10 120 python bench.py --gpus 1 --steps 20 --warmup 5 > gpurun_out/rounds/drv.log 2>&1 || exit 3
