@@ -548,3 +548,21 @@ def test_uneven_strips_collective_schedule(gol, N, R):
     assert len({o[2] for o in out}) == 1, [o[2] for o in out]  # one schedule on every rank
     board = np.vstack([b for _, b, _ in sorted(out, key=lambda o: o[0])])
     assert np.array_equal(board, numpy_step(random_board(N, 320, 31), gens))
+
+
+def test_multi_round_plans(gol, monkeypatch):
+    """Streaming plans of several rounds (plan.hpp round_balanced_rows, big tiles by default), forced on a
+    16384^2 board by a tiny segment target (GOL_ROUND_ROWS_PER_LEVEL=1, read when the engine is built):
+    the plan must hold more waves than the one-round plan, and the board must match a torch oracle."""
+    import torch
+
+    N, gens, seed = 16384, 8 * 3 + 5, 21
+    one = _sim(gol, N, halo_depth=8, kernel="temporal", subtiles=False).init(5, seed=seed)
+    waves1 = one.stats()["plan_waves"]
+    del one
+    monkeypatch.setenv("GOL_ROUND_ROWS_PER_LEVEL", "1")
+    s = _sim(gol, N, halo_depth=8, kernel="temporal", subtiles=False).init(5, seed=seed)
+    assert s.stats()["plan_waves"] > waves1
+    s.step(gens)
+    ref = torch_step(torch.as_tensor(initial_board(5, N, 1, True, seed), device="cuda:0"), gens, device="cuda:0")
+    assert np.array_equal(s.board(), ref.cpu().numpy())
