@@ -158,7 +158,11 @@ void HipEngine::dual_superstep(int k) {
         for (int j = 0; j < np; ++j)
             for (int i = 0; i < 2; ++i) {
                 const int s = sub_first_ ^ i;  // GOL_SUB_FIRST=1: half 1's pass first (measurement knob)
-                if (!((ov && s == 0 && j == 0) || (ov2 && j == 0))) launch_half(s, p, k, s ? s_comm_ : s_comp_, j);
+                if (!((ov && s == 0 && j == 0) || (ov2 && j == 0))) {
+                    if (j == 0 && i == 0) trace::mark("gol.launch0");  // (GOL_ROCTX: host side of the launch latency)
+                    launch_half(s, p, k, s ? s_comm_ : s_comp_, j);
+                    if (j == 0 && i == 0) trace::mark("gol.launch0_done");
+                }
             }
     }
     if (wd_) {

@@ -668,8 +668,32 @@ for i in 1 2; do
 done
 }
 
+cmd_launch_trace() {
+# Round 3: where the driver command's ~15 us from run() to the first kernel go: roctx marks around the first launch of the
+# sub-tile superstep (host side) vs the first kernel's start (kernel trace), three traced runs.
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out/ltrace
+export TMPDIR=/tmp GOL_ROCTX=1
+for kv in "${@:-X=0}"; do
+for i in 1 2 3; do
+  rm -rf gpurun_out/ltrace/p$i
+  echo "== $kv run $i" | tee -a gpurun_out/ltrace/summary.txt
+  export "$kv"
+  timeout -k 10 180 rocprofv3 --kernel-trace --marker-trace --output-format csv -d gpurun_out/ltrace/p$i -o run -- python3 bench.py --gpus 1 --steps 20 --warmup 5 --no-phases > gpurun_out/ltrace/b$i.log 2>&1 || exit 3
+  python3 tools/timed_trace.py gpurun_out/ltrace/p$i | tail -5 | tee -a gpurun_out/ltrace/summary.txt
+done
+done
+unset GOL_ROCTX
+for rep in 1 2 3; do
+  for kv in "${@:-X=0}"; do
+    env "$kv" timeout -k 10 120 python bench.py --gpus 1 --steps 20 --warmup 5 > gpurun_out/ltrace/d.log 2>&1 || exit 3
+    grep '^{' gpurun_out/ltrace/d.log | python3 -c "import sys,json; d=json.loads(sys.stdin.read()); print('driver $kv', round(d['ms_per_step']*1e3,3), 'us/gen')" | tee -a gpurun_out/ltrace/summary.txt
+  done
+done
+}
+
 name=${1:-}; shift || true
 if ! declare -F "cmd_$name" >/dev/null; then
-  echo "usage: $0 <name> [args]; names: rounds_engine oneshot bigboard_rounds cfg2_check cfg2_steps_ab cfg2_sweep cfg2_trace cfg2_warmup_ab driver_trace events_ab fold_ab fold_check fold_depth fold_strip kb_ab kb_bperm kb_depth_sweep kb_occ_sweep kb_rounds kb_split2 kb_tile_sweep occ_check pmc_fold pmc_k7 pmc_k7_after pmc_temporal pmc_tile pmc_tile_round2 power_probe prof_ab split_bench split_cost split_cost_r split_trace subtiles_check subtiles_check2 subtiles_occ subtiles_r128 sync_spin_ab tune_check" >&2; exit 2
+  echo "usage: $0 <name> [args]; names: launch_trace rounds_engine oneshot bigboard_rounds cfg2_check cfg2_steps_ab cfg2_sweep cfg2_trace cfg2_warmup_ab driver_trace events_ab fold_ab fold_check fold_depth fold_strip kb_ab kb_bperm kb_depth_sweep kb_occ_sweep kb_rounds kb_split2 kb_tile_sweep occ_check pmc_fold pmc_k7 pmc_k7_after pmc_temporal pmc_tile pmc_tile_round2 power_probe prof_ab split_bench split_cost split_cost_r split_trace subtiles_check subtiles_check2 subtiles_occ subtiles_r128 sync_spin_ab tune_check" >&2; exit 2
 fi
 "cmd_$name" "$@"

@@ -64,6 +64,11 @@ def main():
     busy += cur_e - cur_s
     first, end = sel[0][0], max(e for _, e, _, _ in sel)
     print(f"first kernel starts {(first - t0) / 1e3:.1f} us after run() was entered; last kernel ends at {(end - t0) / 1e3:.1f} us")
+    # host side of the first launch (sub-tile supersteps mark it): run() entry -> launch call -> its return
+    for tag in ("gol.launch0", "gol.launch0_done"):
+        mk = [m for m in ms if any(tag == str(v) for v in m.values()) and t0 <= int(m["Start_Timestamp"]) <= t_host_end]
+        if mk:
+            print(f"  {tag}: {(int(mk[0]['Start_Timestamp']) - t0) / 1e3:.1f} us after run() was entered")
     print(f"GPU busy {busy / 1e3:.1f} us of the {(end - first) / 1e3:.1f} us from first start to last end "
           f"(idle {(end - first - busy) / 1e3:.1f} us)")
 
