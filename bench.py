@@ -179,8 +179,16 @@ def main() -> int:
     dec = sim.decomposition
     cells = dec.H * dec.W
 
-    def device_sync():
-        sim.synchronize()  # the engine's own HIP streams (watchdog-armed)
+    # The timed run ends with torch.cuda.synchronize() alone: hipDeviceSynchronize waits for every stream
+    # of the device, the engine's two included (tools/sync_check.py checks it), and a hang is still
+    # caught (the watchdog fires on GPU work outstanding without progress).  The engine's own stream
+    # syncs before it cost ~6.6 us per run: driver command 11.29 vs 11.62 us/gen, mean of 10 alternating
+    # pairs (profiles/end_sync_round3.txt).  BENCH_END_SYNC=both restores them (measurement knob).
+    end_sync = os.environ.get("BENCH_END_SYNC", "torch")
+
+    def device_sync(end=False):
+        if not (end and use_torch_sync and end_sync == "torch"):
+            sim.synchronize()  # the engine's own HIP streams (watchdog-armed)
         if use_torch_sync:
             torch.cuda.synchronize()
 
@@ -190,7 +198,7 @@ def main() -> int:
     sim.engine.device_barrier()  # host barrier + RCCL all-reduce completed on every GPU
     t0 = time.perf_counter()
     sim.step(steps)
-    device_sync()
+    device_sync(end=True)
     t1 = time.perf_counter()
     elapsed = transport.allreduce_max(t1 - t0)
     # perf_counter is CLOCK_MONOTONIC: comparable across the processes of one node

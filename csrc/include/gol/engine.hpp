@@ -104,6 +104,8 @@ class Engine {
     void init(const PatternSpec& p);
     virtual void run(u64 generations);
     virtual void synchronize() = 0;
+    // True when none of the engine's own GPU work is outstanding (non-blocking query; CPU: always).
+    virtual bool gpu_idle() { return true; }
 
     // Local tile as dense masked words (h * nw), and the reverse (halos are refreshed).
     virtual std::vector<u64> tile_words() = 0;

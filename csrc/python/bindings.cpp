@@ -277,6 +277,7 @@ PYBIND11_MODULE(_gol, m) {
         .def("init", &Engine::init, py::call_guard<py::gil_scoped_release>())
         .def("run", &Engine::run, py::call_guard<py::gil_scoped_release>())
         .def("synchronize", &Engine::synchronize, py::call_guard<py::gil_scoped_release>())
+        .def("gpu_idle", &Engine::gpu_idle)
         .def("tile_words",
              [](Engine& e) {
                  std::vector<u64> w;

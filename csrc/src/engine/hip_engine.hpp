@@ -83,6 +83,15 @@ class HipEngine : public Engine {
         HIP_CHECK(hipStreamSynchronize(s_comp_));
     }
 
+    bool gpu_idle() override {
+        for (hipStream_t s : {s_comp_, s_comm_}) {
+            const hipError_t e = hipStreamQuery(s);
+            if (e == hipErrorNotReady) return false;
+            HIP_CHECK(e);
+        }
+        return true;
+    }
+
     std::vector<u64> tile_words() override;
 
     void set_tile_words(const std::vector<u64>& dense) override;

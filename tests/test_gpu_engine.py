@@ -566,3 +566,18 @@ def test_multi_round_plans(gol, monkeypatch):
     s.step(gens)
     ref = torch_step(torch.as_tensor(initial_board(5, N, 1, True, seed), device="cuda:0"), gens, device="cuda:0")
     assert np.array_equal(s.board(), ref.cpu().numpy())
+
+
+def test_torch_device_sync_covers_engine_streams(gol):
+    """bench.py ends the timed run with torch.cuda.synchronize() alone: hipDeviceSynchronize must wait for
+    the engine's own non-blocking streams (both sub-tile halves at 32768^2)."""
+    import torch
+
+    torch.cuda.synchronize()
+    s = _sim(gol, 32768).init(5, seed=2)
+    s.step(8)
+    s.synchronize()
+    assert s.engine.gpu_idle()
+    s.step(1000)  # ~10 ms of GPU work, enqueued in well under that
+    torch.cuda.synchronize()
+    assert s.engine.gpu_idle()

@@ -692,8 +692,23 @@ for rep in 1 2 3; do
 done
 }
 
+cmd_end_sync_ab() {
+# Round 3: the driver command with the engine's stream syncs + torch's device sync after the timed run (both) vs torch's
+# device sync alone (torch), alternating; then a check that torch's sync alone waits for the engine's streams.
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out/esync
+out=gpurun_out/esync/end_sync.txt; : > $out
+for rep in $(seq ${1:-4}); do
+  for v in both torch; do
+    BENCH_END_SYNC=$v timeout -k 10 120 python bench.py --gpus 1 --steps 20 --warmup 5 > gpurun_out/esync/d.log 2>&1 || exit 3
+    grep '^{' gpurun_out/esync/d.log | python3 -c "import sys,json; d=json.loads(sys.stdin.read()); print('$v', round(d['ms_per_step']*1e3,3), 'us/gen')" | tee -a $out
+  done
+done
+timeout -k 10 120 python tools/sync_check.py | tee -a $out
+}
+
 name=${1:-}; shift || true
 if ! declare -F "cmd_$name" >/dev/null; then
-  echo "usage: $0 <name> [args]; names: launch_trace rounds_engine oneshot bigboard_rounds cfg2_check cfg2_steps_ab cfg2_sweep cfg2_trace cfg2_warmup_ab driver_trace events_ab fold_ab fold_check fold_depth fold_strip kb_ab kb_bperm kb_depth_sweep kb_occ_sweep kb_rounds kb_split2 kb_tile_sweep occ_check pmc_fold pmc_k7 pmc_k7_after pmc_temporal pmc_tile pmc_tile_round2 power_probe prof_ab split_bench split_cost split_cost_r split_trace subtiles_check subtiles_check2 subtiles_occ subtiles_r128 sync_spin_ab tune_check" >&2; exit 2
+  echo "usage: $0 <name> [args]; names: end_sync_ab launch_trace rounds_engine oneshot bigboard_rounds cfg2_check cfg2_steps_ab cfg2_sweep cfg2_trace cfg2_warmup_ab driver_trace events_ab fold_ab fold_check fold_depth fold_strip kb_ab kb_bperm kb_depth_sweep kb_occ_sweep kb_rounds kb_split2 kb_tile_sweep occ_check pmc_fold pmc_k7 pmc_k7_after pmc_temporal pmc_tile pmc_tile_round2 power_probe prof_ab split_bench split_cost split_cost_r split_trace subtiles_check subtiles_check2 subtiles_occ subtiles_r128 sync_spin_ab tune_check" >&2; exit 2
 fi
 "cmd_$name" "$@"
