@@ -707,8 +707,32 @@ done
 timeout -k 10 120 python tools/sync_check.py | tee -a $out
 }
 
+cmd_driver_ab() {
+# Round 3: the driver command with extra bench.py flags A vs B, alternating pairs: tools/experiments.sh driver_ab "<A flags>" "<B flags>" [pairs]
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out/dab
+out=gpurun_out/dab/driver_ab.txt; : > $out; : > gpurun_out/dab/detail.txt
+for rep in $(seq ${3:-8}); do
+  for v in "$1" "$2"; do
+    timeout -k 10 120 python bench.py --gpus 1 --steps 20 --warmup 5 $v > gpurun_out/dab/d.log 2>&1 || exit 3
+    grep '^{' gpurun_out/dab/d.log | python3 -c "import sys,json; d=json.loads(sys.stdin.read()); print('[$v]', round(d['ms_per_step']*1e3,3))" | tee -a $out
+    grep '^{' gpurun_out/dab/d.log | python3 -c "import sys,json; d=json.loads(sys.stdin.read()); c=d['config']; print(round(d['ms_per_step']*1e3,3), c['schedule'], c['kernel'], c['kernel_depth'], c['plan_waves'], ' '.join(x for x in c['autotune'].split() if x.startswith(('sched:','pass8','pass12','0:temporal'))), 'init', d['timing']['init_s'])" >> gpurun_out/dab/detail.txt
+  done
+done
+python3 - $out <<'PY'
+import sys
+from statistics import mean, median
+d = {}
+for l in open(sys.argv[1]):
+    k, v = l.rsplit(' ', 1)
+    d.setdefault(k, []).append(float(v))
+for k, v in d.items():
+    print(k, len(v), 'mean %.3f median %.3f min %.3f max %.3f' % (mean(v), median(v), min(v), max(v)))
+PY
+}
+
 name=${1:-}; shift || true
 if ! declare -F "cmd_$name" >/dev/null; then
-  echo "usage: $0 <name> [args]; names: end_sync_ab launch_trace rounds_engine oneshot bigboard_rounds cfg2_check cfg2_steps_ab cfg2_sweep cfg2_trace cfg2_warmup_ab driver_trace events_ab fold_ab fold_check fold_depth fold_strip kb_ab kb_bperm kb_depth_sweep kb_occ_sweep kb_rounds kb_split2 kb_tile_sweep occ_check pmc_fold pmc_k7 pmc_k7_after pmc_temporal pmc_tile pmc_tile_round2 power_probe prof_ab split_bench split_cost split_cost_r split_trace subtiles_check subtiles_check2 subtiles_occ subtiles_r128 sync_spin_ab tune_check" >&2; exit 2
+  echo "usage: $0 <name> [args]; names: driver_ab end_sync_ab launch_trace rounds_engine oneshot bigboard_rounds cfg2_check cfg2_steps_ab cfg2_sweep cfg2_trace cfg2_warmup_ab driver_trace events_ab fold_ab fold_check fold_depth fold_strip kb_ab kb_bperm kb_depth_sweep kb_occ_sweep kb_rounds kb_split2 kb_tile_sweep occ_check pmc_fold pmc_k7 pmc_k7_after pmc_temporal pmc_tile pmc_tile_round2 power_probe prof_ab split_bench split_cost split_cost_r split_trace subtiles_check subtiles_check2 subtiles_occ subtiles_r128 sync_spin_ab tune_check" >&2; exit 2
 fi
 "cmd_$name" "$@"
