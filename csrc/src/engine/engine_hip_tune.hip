@@ -398,9 +398,13 @@ void HipEngine::autotune_kernel() {
     spin_up();
     // Three interleaved rounds, best of each candidate: some candidates are within 1-2% of each
     // other (32768^2: the 3- and 2-waves/SIMD plans), and one 3-pass sample picks on noise.
+    // Candidates more than 1.5x slower than the best one after the first round are not timed again
+    // (they cannot win on noise; on a 2^20-row tile the losing step_pipe geometries took ~24 s of the
+    // ~37 s init).
     std::vector<float> tbest(cands.size(), 1e30f);
     for (int round = 0; round < 3; ++round)
         for (size_t i = 0; i < cands.size(); ++i) {
+            if (round > 0 && tbest[i] > 1.5f * *std::min_element(tbest.begin(), tbest.end())) continue;
             cfg_.tile_waves = cands[i].nw;
             occ_ = cands[i].occ;
             if (cands[i].pnw) set_pipe(cands[i].pnw, cands[i].pl, cands[i].pwg);
