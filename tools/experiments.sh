@@ -708,13 +708,15 @@ timeout -k 10 120 python tools/sync_check.py | tee -a $out
 }
 
 cmd_driver_ab() {
-# Round 3: the driver command with extra bench.py flags A vs B, alternating pairs: tools/experiments.sh driver_ab "<A flags>" "<B flags>" [pairs]
+# Round 3: the driver command with extra bench.py flags (or one VAR=value environment setting) A vs B, alternating pairs:
+# tools/experiments.sh driver_ab "<A>" "<B>" [pairs]
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out/dab
 out=gpurun_out/dab/driver_ab.txt; : > $out; : > gpurun_out/dab/detail.txt
 for rep in $(seq ${3:-8}); do
   for v in "$1" "$2"; do
-    timeout -k 10 120 python bench.py --gpus 1 --steps 20 --warmup 5 $v > gpurun_out/dab/d.log 2>&1 || exit 3
+    case "$v" in *=*) ev="$v"; fl="";; *) ev="X_AB=1"; fl="$v";; esac
+    env "$ev" timeout -k 10 120 python bench.py --gpus 1 --steps 20 --warmup 5 $fl > gpurun_out/dab/d.log 2>&1 || exit 3
     grep '^{' gpurun_out/dab/d.log | python3 -c "import sys,json; d=json.loads(sys.stdin.read()); print('[$v]', round(d['ms_per_step']*1e3,3))" | tee -a $out
     grep '^{' gpurun_out/dab/d.log | python3 -c "import sys,json; d=json.loads(sys.stdin.read()); c=d['config']; print(round(d['ms_per_step']*1e3,3), c['schedule'], c['kernel'], c['kernel_depth'], c['plan_waves'], ' '.join(x for x in c['autotune'].split() if x.startswith(('sched:','pass8','pass12','0:temporal'))), 'init', d['timing']['init_s'])" >> gpurun_out/dab/detail.txt
   done
