@@ -673,6 +673,7 @@ cmd_launch_trace() {
 # sub-tile superstep (host side) vs the first kernel's start (kernel trace), three traced runs.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out/ltrace
+: > gpurun_out/ltrace/summary.txt
 export TMPDIR=/tmp GOL_ROCTX=1
 for kv in "${@:-X=0}"; do
 for i in 1 2 3; do
