@@ -255,6 +255,7 @@ void HipEngine::run(u64 generations) {
         for (int s = 0; s < 2; ++s)
             dual_copy(sub_rows(s, sub_cur_, 0), buf_[cur_] + L_.index(sub_r0_[s], -1), rows_bytes(s, sub_L_[s].h));
         // both halves' first superstep waits for the copy (each waits on the other's "done" event)
+        events_synced_ = false;
         HIP_CHECK(hipEventRecord(ev_sub_a_, s_comp_));
         HIP_CHECK(hipEventRecord(ev_sub_b_, s_comp_));
         sub_current_ = true;

@@ -173,6 +173,7 @@ void HipEngine::dual_superstep(int k) {
         ev_sub_b_ = m.ev[1];
         m.n = 2;
     }
+    events_synced_ = false;
     HIP_CHECK(hipEventRecord(ev_sub_a_, s_comp_));
     HIP_CHECK(hipEventRecord(ev_sub_b_, s_comm_));
     if (wd_) {

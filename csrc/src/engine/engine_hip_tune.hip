@@ -97,6 +97,7 @@ void HipEngine::measure_pass_costs() {
                         hipk::launch_step(d, sub_buf_[sub][sub_cur_], sub_buf_[sub][(sub_cur_ + 1) % 3], pl.d,
                                           pl.waves, sp, sub ? s_comm_ : s_comp_);
                     }
+                events_synced_ = false;
                 HIP_CHECK(hipEventRecord(ev_sub_b_, s_comm_));
                 HIP_CHECK(hipStreamWaitEvent(s_comp_, ev_sub_b_, 0));
             } else {

@@ -81,6 +81,7 @@ class HipEngine : public Engine {
         Armed armed(wd_.get());
         HIP_CHECK(hipStreamSynchronize(s_comm_));
         HIP_CHECK(hipStreamSynchronize(s_comp_));
+        events_synced_ = true;
     }
 
     bool gpu_idle() override {
@@ -218,6 +219,10 @@ class HipEngine : public Engine {
     // that follows a synchronisation every event has completed.  (Never inside a graph capture: the
     // sub-tile supersteps are not captured.)
     void wait_pending(hipStream_t s, hipEvent_t ev) {
+        // ev_sub_a_ / ev_sub_b_ are recorded only where events_synced_ is cleared: after synchronize()
+        // and before the next record they are complete, so the query (a runtime call before the
+        // superstep's first launch) is skipped
+        if (events_synced_ && skip_synced_query_) return;
         const hipError_t q = hipEventQuery(ev);
         if (q == hipSuccess) return;
         if (q != hipErrorNotReady) HIP_CHECK(q);
@@ -579,6 +584,8 @@ class HipEngine : public Engine {
     std::map<int, DevPlan> sub_plans_;
     std::map<int, hipGraphExec_t> dual_graphs_;  // (half, start buffer, depth) -> launch_half graph
     hipEvent_t ev_sub_a_ = nullptr, ev_sub_b_ = nullptr;  // half 0 / half 1 done with its last superstep
+    bool events_synced_ = false;  // both streams synchronised since ev_sub_a_ / ev_sub_b_ were last recorded
+    const bool skip_synced_query_ = env_int("GOL_SKIP_SYNCED_QUERY", 1) != 0;  // (measurement knob)
                                                            // (ev_sub_own_, or a progress marker's pair)
     hipEvent_t ev_sub_own_[2] = {nullptr, nullptr};
     hipEvent_t ev_sub_x_ = nullptr;                        // the rank's exchange (into both halves) done
