@@ -75,7 +75,8 @@ struct EngineConfig {
                                       // one rank (e.g. a 1-rank RCCL communicator)
     double watchdog_s = 0;            // abort the job after this long without progress (0 = off)
     bool force_split = false;         // run the interior/boundary edge schedule even without neighbours
-    std::string sched = "auto";       // with neighbours: auto (timed at init) | split (overlap) | full
+    std::string sched = "auto";       // auto (timed at init) | split (overlap, with neighbours) | full | flow
+                                      // (one dependency-driven launch per superstep, step_flow)
 };
 
 struct EngineStats {

@@ -106,6 +106,32 @@ int pipe_blocks_per_cu(int nw, int L, bool wrapy);
 bool pipe_fault();
 void launch_step_pipe(int nw, int L, const u64* src, u64* dst, const LaneDesc* plan, i64 n_tiles, const StepParams& p,
                       hipStream_t s);
+// step_flow (flow_kernel.hip): a superstep of several step_temporal passes as ONE launch of a
+// persistent grid whose waves draw the items of a flow plan (plan.hpp build_flow_plan) in ticket
+// order and wait for each item's dependencies through per-item completion flags.
+struct FlowCtl {  // device memory, zero-initialised once; the kernel leaves next = done = 0
+    u32 next;     // ticket counter
+    u32 done;     // waves that drew their last ticket
+    u32 epoch;    // launches completed (flags of the running launch hold epoch + 1)
+    u32 fault;    // a dependency wait timed out: the board is invalid
+};
+struct FlowArgs {
+    u64* a;                  // even passes read a and write b, odd passes the reverse
+    u64* b;
+    const LaneDesc* lanes;   // n_items x 64
+    const FlowItem* items;
+    const u32* deps;
+    u32* flags;              // n_items completion flags (zero-initialised once per plan)
+    FlowCtl* ctl;
+    u32 n_items;
+};
+bool flow_depth_supported(int k);
+int flow_max_depth();
+// Resident 256-thread workgroups per CU of the flow kernel (its persistent grid is this x CUs).
+int flow_blocks_per_cu(u32 flags);
+void launch_step_flow(const FlowArgs& a, i64 n_blocks, const StepParams& p, hipStream_t s);
+// True (and cleared) when a wait of a flow launch timed out since the last call (synchronises s).
+bool flow_fault(FlowCtl* ctl, hipStream_t s);
 // Single-generation LDS-tiled kernel over output rows [r0, r1) (all words).
 void launch_step_lds(const u64* src, u64* dst, const Layout& L, i64 r0, i64 r1, u32 flags, hipStream_t s);
 

@@ -190,6 +190,10 @@ HipEngine::~HipEngine() {
     for (auto& v : {&hstage_s_, &hstage_r_, &xhs_, &xhr_})
         for (u64* p : *v) hipHostFree(p);
     for (int i = 0; i < 2; ++i) hipFree(buf_[i]);
+    for (auto& kv : flow_plans_)
+        for (void* q : {(void*)kv.second.lanes, (void*)kv.second.items, (void*)kv.second.deps, (void*)kv.second.flags})
+            if (q) hipFree(q);
+    if (flow_ctl_) hipFree(flow_ctl_);
     for (auto& kv : res_plans_)
         for (void* q : {(void*)kv.second.d, (void*)kv.second.nbr_off, (void*)kv.second.nbr, (void*)kv.second.counters})
             if (q) hipFree(q);
@@ -322,7 +326,11 @@ void HipEngine::do_init(const PatternSpec& p) {
     }
     stats_.schedule = split_ ? "split" : (halo_items(L_.R).empty() ? "local" : "full");
     if (dual_) stats_.schedule += sub_overlap_ == 2 ? "+subtiles2ov2" : (sub_overlap_ ? "+subtiles2ov" : "+subtiles2");
-    stats_.kernel_depth = dual_ ? tdepth_ : kdepth_;
+    if (flow_) {
+        stats_.schedule += flow_graph_ ? "+flow+graph" : "+flow";
+        stats_.kernel = strprintf("flow(temporal K<=%d)", hipk::flow_max_depth());
+    }
+    stats_.kernel_depth = dual_ ? tdepth_ : (flow_ ? hipk::flow_max_depth() : kdepth_);
     stats_.tile_waves = cfg_.tile_waves;
     std::string tn;
     for (const auto& kv : tune_ms_) tn += strprintf("%s%s=%.3fus/gen", tn.empty() ? "" : " ", kv.first.c_str(), kv.second * 1e3);
@@ -346,6 +354,7 @@ void HipEngine::do_init(const PatternSpec& p) {
             capture_dual_graphs(k);
         } else {
             prepare(k);
+            if (flow_) flow_plan(k);
         }
     }
     prewarm_graph();
@@ -365,6 +374,10 @@ void HipEngine::do_init(const PatternSpec& p) {
     if (res_) {
         stats_.plan_waves = res_plan(res_kin_).tiles;  // workgroups of the resident launch
         stats_.lane_efficiency = 0;
+    } else if (flow_) {
+        const FlowDev& fd = flow_plan(superstep_depth());
+        stats_.plan_waves = flow_blocks_ * kWavesPerBlock;  // the persistent grid
+        stats_.lane_efficiency = fd.st.lane_rows ? (double)fd.st.out_words / (double)fd.st.lane_rows : 0.0;
     } else {
         const DevPlan& fp = full_plan_stats();
         stats_.plan_waves = fp.waves;

@@ -1,0 +1,124 @@
+// gol-mi355x: HipEngine — supersteps as ONE dependency-driven launch (step_flow, flow_kernel.hip).
+//
+// A one-tile superstep of k generations normally runs k / K kernel passes, each a launch that starts
+// only when the previous pass's last wave has drained (docs/PERFORMANCE.md §6).  In flow mode the
+// whole superstep is one launch of a persistent grid: the passes' plan waves become work items in one
+// ticket order, and each item waits only for the items of the previous pass it reads from or
+// overwrites (plan.hpp build_flow_plan).  With neighbours the exchange runs first on the compute
+// stream (the "full" schedule: the first pass reads the ghost rows it wrote).  The mode is a
+// candidate of the schedule timing ("local+flow" / "full+flow", engine_hip_tune.hip), so the
+// measured rate decides whether a run uses it.
+// Reference: the generation loop gol-main.c:93-116, one launch + device sync per generation in
+// gol-with-cuda.cu:264-284.
+#include "hip_engine.hpp"
+
+namespace gol {
+namespace hipeng {
+
+bool HipEngine::flow_eligible() const {
+    // one tile; every pass is a step_temporal pass (no LDS-tile / pipe / LDS kernels, no split bands);
+    // ghost words of a non-aligned self-wrapping width are refreshed by a kernel after every pass,
+    // which a single launch cannot do
+    if (cfg_.compat || cfg_.profile || cfg_.force_split || kernel_ == "lds" || res_) return false;
+    if (cfg_.kernel == "tile" || cfg_.kernel == "pipe" || cfg_.kernel == "resident") return false;
+    if (self_x() && !L_.aligned()) return false;
+    return env_int("GOL_FLOW", 1) != 0;
+}
+
+// Passes of a flow superstep: as few as the flow kernel's deepest depth allows, as equal as
+// possible (20 = 7 + 7 + 6).  GOL_FLOW_KMAX lowers the deepest depth (measurement knob).
+std::vector<int> HipEngine::flow_cut(int k) const {
+    const int kmax = std::max(1, std::min<int>(hipk::flow_max_depth(), (int)env_int("GOL_FLOW_KMAX", hipk::flow_max_depth())));
+    const int n = (k + kmax - 1) / kmax;
+    std::vector<int> ps;
+    for (int j = 0; j < n; ++j) ps.push_back(k / n + (j < k % n ? 1 : 0));
+    return ps;
+}
+
+const HipEngine::FlowDev& HipEngine::flow_plan(int k) {
+    auto it = flow_plans_.find(k);
+    if (it != flow_plans_.end()) return it->second;
+    if (!flow_ctl_) {
+        HIP_CHECK(hipMalloc(&flow_ctl_, sizeof(hipk::FlowCtl)));
+        HIP_CHECK(hipMemsetAsync(flow_ctl_, 0, sizeof(hipk::FlowCtl), s_comp_));
+    }
+    const std::vector<int> ps = flow_cut(k);
+    const bool wrapy = (step_flags() & hipk::STEP_WRAP_Y) != 0;
+    if (flow_blocks_ <= 0) flow_blocks_ = (i64)hipk::flow_blocks_per_cu(step_flags()) * cus_;
+    const i64 resident = flow_blocks_ * kWavesPerBlock;
+    // items per pass: one round of the persistent grid (GOL_FLOW_ROUNDS in percent scales it; big
+    // tiles take several rounds of ~45K-row segments, as the pass kernels' plans)
+    const double scale = (double)env_int("GOL_FLOW_ROUNDS", 100) / 100.0;
+    std::vector<FlowPass> fps;
+    for (size_t j = 0; j < ps.size(); ++j) {
+        const std::vector<Region> rg = regions(0, ps[j], ext_after(ps, j));
+        const i64 target = std::max<i64>(1, (i64)(scale * (double)resident));
+        const i64 rows = round_balanced_rows(rg, L_.nw, L_.h, ps[j], target, 2 * (i64)ps[j], xwrap_by_plan(),
+                                             round_rows(ps[j]));
+        fps.push_back({ps[j], rg, rows});
+    }
+    FlowPlan fp;
+    const std::string err = build_flow_plan(fps, L_.nw, L_.h, xwrap_by_plan(), wrapy, fp);
+    if (!err.empty()) throw Error("flow plan: " + err);
+    for (size_t j = 0; j < ps.size(); ++j) {
+        const std::vector<LaneDesc> part(fp.lanes.begin() + (size_t)fp.pass_begin[j] * kWaveLanes,
+                                         fp.lanes.begin() + (size_t)fp.pass_begin[j + 1] * kWaveLanes);
+        const std::string bad = validate_plan(part, L_.nw, L_.h, L_.R, ps[j], wrapy);
+        if (!bad.empty())
+            throw Error(strprintf("refusing to launch an unsafe flow plan (k %d, pass %zu): %s", k, j, bad.c_str()));
+    }
+    FlowDev fd;
+    fd.cut = ps;
+    fd.n_items = (u32)fp.items.size();
+    fd.st = fp.st;
+    fd.max_deps = fp.max_deps;
+    HIP_CHECK(hipMalloc(&fd.lanes, std::max<size_t>(1, fp.lanes.size()) * sizeof(LaneDesc)));
+    HIP_CHECK(hipMalloc(&fd.items, std::max<size_t>(1, fp.items.size()) * sizeof(FlowItem)));
+    HIP_CHECK(hipMalloc(&fd.deps, std::max<size_t>(1, fp.deps.size()) * sizeof(u32)));
+    HIP_CHECK(hipMalloc(&fd.flags, std::max<size_t>(1, fp.items.size()) * sizeof(u32)));
+    if (!fp.lanes.empty()) upload(fd.lanes, fp.lanes.data(), fp.lanes.size() * sizeof(LaneDesc));
+    if (!fp.items.empty()) upload(fd.items, fp.items.data(), fp.items.size() * sizeof(FlowItem));
+    if (!fp.deps.empty()) upload(fd.deps, fp.deps.data(), fp.deps.size() * sizeof(u32));
+    // flags start below every epoch a launch will wait for
+    HIP_CHECK(hipMemsetAsync(fd.flags, 0, std::max<size_t>(1, fp.items.size()) * sizeof(u32), s_comp_));
+    HIP_CHECK(hipStreamSynchronize(s_comp_));
+    return flow_plans_.emplace(k, fd).first->second;
+}
+
+void HipEngine::flow_launch(int k, const u64* src, u64* dst, hipStream_t s) {
+    const FlowDev& fd = flow_plan(k);
+    if (fd.n_items == 0) return;
+    hipk::FlowArgs a{};
+    a.a = const_cast<u64*>(src);  // (pass 0 reads it; an odd pass count never writes it, an even one does)
+    a.b = dst;
+    a.lanes = fd.lanes;
+    a.items = fd.items;
+    a.deps = fd.deps;
+    a.flags = fd.flags;
+    a.ctl = flow_ctl_;
+    a.n_items = fd.n_items;
+    hipk::StepParams sp{L_.pitch, (i32)L_.h, (i32)L_.nw, L_.R, step_flags()};
+    hipk::launch_step_flow(a, flow_blocks_, sp, s);
+    HIP_CHECK(hipGetLastError());
+    flow_used_ = true;
+}
+
+// One flow superstep: (with neighbours) the exchange of the k-deep halo on the compute stream, then
+// the single launch; the result lands in buf[cur ^ (passes & 1)].
+void HipEngine::flow_superstep(int k) {
+    const std::vector<int>& ps = pass_depths(k);
+    const std::vector<HaloItem>& items = items_for(k);
+    if (!items.empty()) {
+        prepare(k);
+        if (device_transport_)
+            exchange_device(k, items, cur_, s_comp_);
+        else
+            exchange_staged(k, items, cur_, s_comp_);
+    }
+    flow_launch(k, buf_[cur_], buf_[cur_ ^ 1], s_comp_);
+    if (ps.size() & 1) cur_ ^= 1;
+    mark_ready();
+}
+
+}  // namespace hipeng
+}  // namespace gol

@@ -58,7 +58,7 @@ void HipEngine::spin_up() {
 // kernel passes, never the exchanges.
 void HipEngine::measure_pass_costs() {
     pass_us_.clear();
-    if (cfg_.compat || cfg_.kernel_depth > 0 || kernel_ == "lds" || res_ || (!dual_ && tile_kernel(0)) ||
+    if (cfg_.compat || cfg_.kernel_depth > 0 || kernel_ == "lds" || res_ || flow_ || (!dual_ && tile_kernel(0)) ||
         (!dual_ && !split_ && kern_[0] == "pipe"))
         return;
     // every instantiated depth up to the pass depth, and the deeper ones a superstep could use: a
@@ -118,6 +118,19 @@ void HipEngine::measure_pass_costs() {
     passes_.clear();
 }
 
+bool HipEngine::flow_timing_buffers() {
+    if (flow_scratch_) return true;
+    size_t fr = 0, tot = 0;
+    if (hipMemGetInfo(&fr, &tot) != hipSuccess || fr < alloc_bytes_ + ((size_t)1 << 30)) return false;
+    if (hipMalloc(&flow_scratch_, alloc_bytes_) != hipSuccess) {
+        hipGetLastError();
+        flow_scratch_ = nullptr;
+        return false;
+    }
+    HIP_CHECK(hipMemsetAsync(flow_scratch_, 0, alloc_bytes_, s_comp_));
+    return true;
+}
+
 void HipEngine::choose_schedule() {
     const bool nbrs = !halo_items(L_.R).empty();  // identical on every rank (uniform grid)
     std::vector<std::string> cands;
@@ -153,6 +166,24 @@ void HipEngine::choose_schedule() {
         if (cfg_.subtiles == 2) cands.clear();
         cands.insert(cands.end(), dc.begin(), dc.end());
     }
+    // The one-tile superstep as ONE dependency-driven launch (step_flow, engine_hip_flow.hip), eager and
+    // replayed from a graph (with neighbours only where RCCL may be captured).  Timed on scratch: the
+    // candidate needs memory for one more board (agreed over the ranks: the timing is collective).
+    if (cands[0] != "split" && flow_eligible()) {
+        double ok = flow_timing_buffers() ? 1.0 : 0.0;
+        if (t_->size() > 1) ok = t_->allreduce_min(ok);
+        if (ok > 0) {
+            cands.push_back("flow");
+            if (cfg_.graph && (!nbrs || (device_transport_ && t_->graph_capturable() && cfg_.graph_rccl != 0)))
+                cands.push_back("flow+graph");
+        }
+        if (cfg_.sched == "flow") {  // GOL_SCHEDULE=flow: the only candidate
+            if (ok <= 0) throw Error("GOL_SCHEDULE=flow: no device memory for the flow timing scratch");
+            cands = {"flow"};
+        }
+    } else if (cfg_.sched == "flow") {
+        throw Error("GOL_SCHEDULE=flow: this tile cannot run flow supersteps (GOL_KERNEL / GOL_COMPAT / width)");
+    }
     std::string pick = cands[0];
     if (cands.size() > 1) {
         // Supersteps of the length the runs will use: kSchedReps back-to-back R-generation supersteps,
@@ -178,10 +209,10 @@ void HipEngine::choose_schedule() {
                 best[c] = std::min(best[c], t_->allreduce_max(dt) * 1e6 / (reps * k));
                 init_step("init: schedule timing", cands[c].c_str(), k, (float)best[c]);
             }
-        const bool graph_failed = t_->allreduce_max(sched_graph_failed_ ? 1.0 : 0.0) > 0;
         size_t bi = 0;
         for (size_t c = 0; c < cands.size(); ++c) {
-            if (graph_failed && cands[c] == "full+graph") best[c] = 1e30;
+            // a candidate whose timing graph could not be captured on some rank is dropped
+            if (t_->allreduce_max(sched_graph_failed_.count(cands[c]) ? 1.0 : 0.0) > 0) best[c] = 1e30;
             sched_us_[cands[c]] = best[c];
             if (best[c] < best[bi]) bi = c;
         }
@@ -199,11 +230,11 @@ void HipEngine::choose_schedule() {
         stats_.halo_bytes = 0;
         stats_.graph_launches = 0;
     }
-    if (sched_graph_) {  // (it captured the communicator: destroy it before the comm can go)
-        HIP_CHECK(hipStreamSynchronize(s_comp_));
-        HIP_CHECK(hipGraphExecDestroy(sched_graph_));
-        sched_graph_ = nullptr;
-    }
+    destroy_sched_graphs();  // (they captured the communicator: destroy them before the comm can go)
+    free_flow_scratch();
+    sched_pick_ = pick;
+    flow_ = pick.rfind("flow", 0) == 0;
+    flow_graph_ = pick == "flow+graph";
     split_ = pick == "split";
     dual_ = pick.rfind("subtiles", 0) == 0;
     sub_overlap_ = pick == "subtiles+ov" ? 1 : (pick == "subtiles+ov2" ? 2 : 0);
@@ -239,19 +270,20 @@ void HipEngine::time_schedule(const std::string& c, int k, int reps, bool eager)
         sub_graphs_on_ = sg;
         return;
     }
-    // One-tile supersteps as the runs replay them (graphs: "local" always, "full+graph" candidate):
-    // `reps` supersteps captured once (round 0's warm-up call, after one eager superstep that loads
-    // every kernel variant), one replay per call.
-    const bool graphed =
-        !eager && (c == "full+graph" || (c == "local" && cfg_.graph && !cfg_.profile && !cfg_.compat && graph_ok_));
+    // One-tile supersteps as the runs replay them (graphs: "local" always, "full+graph" and
+    // "flow+graph" candidates): `reps` supersteps captured once per candidate (round 0's warm-up call,
+    // after one eager superstep that loads every kernel variant), one replay per call.
+    const bool graphed = !eager && (c == "full+graph" || c == "flow+graph" ||
+                                    (c == "local" && cfg_.graph && !cfg_.profile && !cfg_.compat && graph_ok_));
     if (graphed) {
-        const std::string base = c == "local" ? "local" : "full";
-        if (sched_graph_ && sched_graph_reps_ != reps) {
+        const std::string base = c == "local" ? "local" : (c == "flow+graph" ? "flow" : "full");
+        SchedGraph& sg = sched_graphs_[c];
+        if (sg.exec && sg.reps != reps) {
             HIP_CHECK(hipStreamSynchronize(s_comp_));
-            HIP_CHECK(hipGraphExecDestroy(sched_graph_));
-            sched_graph_ = nullptr;
+            HIP_CHECK(hipGraphExecDestroy(sg.exec));
+            sg.exec = nullptr;
         }
-        if (!sched_graph_ && !sched_graph_failed_) {
+        if (!sg.exec && !sched_graph_failed_.count(c)) {
             prepare(k);
             time_schedule(base, k, 1, true);
             HIP_CHECK(hipStreamSynchronize(s_comp_));
@@ -260,24 +292,46 @@ void HipEngine::time_schedule(const std::string& c, int k, int reps, bool eager)
                 HIP_CHECK(hipStreamBeginCapture(s_comp_, hipStreamCaptureModeRelaxed));
                 time_schedule(base, k, reps, true);
                 HIP_CHECK(hipStreamEndCapture(s_comp_, &graph));
-                HIP_CHECK(hipGraphInstantiate(&sched_graph_, graph, nullptr, nullptr, 0));
+                HIP_CHECK(hipGraphInstantiate(&sg.exec, graph, nullptr, nullptr, 0));
                 HIP_CHECK(hipGraphDestroy(graph));
-                HIP_CHECK(hipGraphUpload(sched_graph_, s_comp_));
+                HIP_CHECK(hipGraphUpload(sg.exec, s_comp_));
             } catch (const Error& e) {
                 hipGraph_t g2 = nullptr;
                 hipStreamEndCapture(s_comp_, &g2);
                 if (g2) hipGraphDestroy(g2);
                 hipGetLastError();
-                sched_graph_ = nullptr;
-                sched_graph_failed_ = true;  // the candidate is dropped (agreed over the ranks)
+                sg.exec = nullptr;
+                sched_graph_failed_.insert(c);  // the candidate is dropped (agreed over the ranks)
                 fprintf(stderr, "[gol] rank %d: schedule graph capture failed: %s\n", g_.rank, e.what());
             }
-            sched_graph_reps_ = reps;
+            sg.reps = reps;
         }
-        if (sched_graph_)
-            HIP_CHECK(hipGraphLaunch(sched_graph_, s_comp_));
+        if (sg.exec)
+            HIP_CHECK(hipGraphLaunch(sg.exec, s_comp_));
         else
             time_schedule(base, k, reps, true);  // the same exchanges as the peers' replays
+        return;
+    }
+    if (c == "flow") {
+        // flow supersteps on scratch (a flow launch writes both of its buffers): the launches run between
+        // flow_scratch_ and buf[cur ^ 1]; the exchange writes the board's ghost rows, as the other
+        // candidates' do (the next real superstep rewrites them).  The kernel's run time does not depend
+        // on the cell values, so the scratch's are never refreshed.
+        if (!flow_timing_buffers()) throw Error("flow schedule timing: no scratch buffer");
+        const bool f = flow_;
+        flow_ = true;
+        const std::vector<HaloItem>& items = items_for(k);
+        for (int i = 0; i < reps; ++i) {
+            if (!items.empty()) {
+                prepare(k);
+                if (device_transport_)
+                    exchange_device(k, items, cur_, s_comp_);
+                else
+                    exchange_staged(k, items, cur_, s_comp_);
+            }
+            flow_launch(k, flow_scratch_, buf_[cur_ ^ 1], s_comp_);
+        }
+        flow_ = f;
         return;
     }
     split_ = c == "split";
@@ -538,8 +592,12 @@ std::map<std::string, double> HipEngine::phase_probe(int k) {
         }
         out["exchange_us"] = best;
     }
-    const std::string sched = dual_ ? (sub_overlap_ == 2 ? "subtiles+ov2" : (sub_overlap_ ? "subtiles+ov" : "subtiles"))
-                                    : (split_ ? "split" : (halo_items(L_.R).empty() ? "local" : "full"));
+    // the schedule the runs use, as choose_schedule timed it (graph variants included)
+    std::string sched = sched_pick_;
+    if (sched.empty())
+        sched = dual_ ? (sub_overlap_ == 2 ? "subtiles+ov2" : (sub_overlap_ ? "subtiles+ov" : "subtiles"))
+                      : (split_ ? "split" : (halo_items(L_.R).empty() ? "local" : "full"));
+    if (sched.rfind("flow", 0) == 0 && !flow_timing_buffers()) sched = halo_items(L_.R).empty() ? "local" : "full";
     const int reps = 2;
     double best = 1e30;
     for (int round = 0; round < 3; ++round) {
@@ -554,10 +612,8 @@ std::map<std::string, double> HipEngine::phase_probe(int k) {
     out["superstep_us"] = best;
     out["superstep_gens"] = k;
     synchronize();
-    if (sched_graph_) {
-        HIP_CHECK(hipGraphExecDestroy(sched_graph_));
-        sched_graph_ = nullptr;
-    }
+    destroy_sched_graphs();
+    free_flow_scratch();
     HIP_CHECK(hipEventDestroy(e0));
     HIP_CHECK(hipEventDestroy(e1));
     dual_ = was_dual;

@@ -7,6 +7,7 @@
 //   engine_hip_subtiles.hip  two sub-tiles per rank on two streams
 //   engine_hip_graph.hip     hipGraph capture and replay of one-tile supersteps
 //   engine_hip_halo.hip      halo exchange (device transport or host staging)
+//   engine_hip_flow.hip      supersteps as one dependency-driven launch (step_flow)
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -17,6 +18,7 @@
 #include <cstring>
 #include <map>
 #include <mutex>
+#include <set>
 #include <thread>
 
 #include "gol/bits.hpp"
@@ -260,7 +262,7 @@ class HipEngine : public Engine {
     // generation).  With neighbours every rank keeps R: the exchanges must match.
     int superstep_depth() const override {
         if (res_) return std::max(L_.R, res_run_depth());
-        if (dual_ || !tuned_ || cfg_.compat || kdepth_ <= 0 || kdepth_ >= L_.R || !halo_items(L_.R).empty())
+        if (dual_ || flow_ || !tuned_ || cfg_.compat || kdepth_ <= 0 || kdepth_ >= L_.R || !halo_items(L_.R).empty())
             return L_.R;
         return (L_.R / kdepth_) * kdepth_;
     }
@@ -283,6 +285,8 @@ class HipEngine : public Engine {
     void do_superstep(int k) override {
         if (dual_)
             dual_superstep(k);
+        else if (flow_)
+            flow_superstep(k);
         else
             tile_superstep(k);
     }
@@ -484,6 +488,22 @@ class HipEngine : public Engine {
     // time resident launches of G generations from a scratch copy of the board; ms per generation
     float time_resident(int kin, int G);
 
+    // ----- flow supersteps (step_flow, engine_hip_flow.hip) -----
+    struct FlowDev {
+        LaneDesc* lanes = nullptr;
+        FlowItem* items = nullptr;
+        u32* deps = nullptr;
+        u32* flags = nullptr;
+        u32 n_items = 0, max_deps = 0;
+        std::vector<int> cut;
+        PlanStats st;
+    };
+    bool flow_eligible() const;
+    std::vector<int> flow_cut(int k) const;
+    const FlowDev& flow_plan(int k);
+    void flow_launch(int k, const u64* src, u64* dst, hipStream_t s);
+    void flow_superstep(int k);
+
     // ----- watchdog support: progress markers -----
     // With a watchdog, every superstep (or graph replay) publishes a marker: HIP events recorded at
     // its end on the streams it used.  The watchdog thread retires completed markers (probe), so GPU
@@ -560,9 +580,32 @@ class HipEngine : public Engine {
     bool graph_ok_ = true;
     bool graph_rccl_on_ = false;  // one-tile supersteps with an RCCL exchange are captured (choose_schedule)
     bool sub_graphs_on_ = false;  // sub-tile passes replay per-half graphs (choose_schedule)
-    hipGraphExec_t sched_graph_ = nullptr;  // the "full+graph" candidate's timing graph (choose_schedule)
-    bool sched_graph_failed_ = false;
-    int sched_graph_reps_ = 0;
+    // timing graphs of the graphed schedule candidates ("local", "full+graph", "flow+graph"), by name
+    struct SchedGraph {
+        hipGraphExec_t exec = nullptr;
+        int reps = 0;
+    };
+    std::map<std::string, SchedGraph> sched_graphs_;
+    std::set<std::string> sched_graph_failed_;  // candidates whose capture failed (dropped)
+    void destroy_sched_graphs() {
+        if (sched_graphs_.empty()) return;
+        hipStreamSynchronize(s_comp_);
+        for (auto& kv : sched_graphs_)
+            if (kv.second.exec) hipGraphExecDestroy(kv.second.exec);
+        sched_graphs_.clear();
+    }
+    std::string sched_pick_;     // the schedule candidate choose_schedule picked (phase_probe times it)
+    bool flow_graph_ = false;    // flow supersteps replay captured graphs ("flow+graph")
+    u64* flow_scratch_ = nullptr;  // timing scratch of flow candidates (a flow launch writes both buffers)
+    // Flow candidates are timed on scratch: the board copied to flow_scratch_, the launch between it and
+    // buf[cur ^ 1].  False when there is no memory for one more board.
+    bool flow_timing_buffers();
+    void free_flow_scratch() {
+        if (!flow_scratch_) return;
+        hipStreamSynchronize(s_comp_);
+        hipFree(flow_scratch_);
+        flow_scratch_ = nullptr;
+    }
     bool events_needed_ = true;  // another stream waits on ev_ready_
     std::vector<void*> deferred_free_;
     std::map<i64, DevPlan> plans_;
@@ -593,6 +636,11 @@ class HipEngine : public Engine {
     std::map<int, std::vector<HaloItem>> items_;
     std::map<i64, hipGraphExec_t> graphs_;
     std::vector<u64*> dstage_s_, dstage_r_, hstage_s_, hstage_r_;
+    bool flow_ = false;                     // supersteps run as one step_flow launch (schedule "+flow")
+    bool flow_used_ = false;                // a flow launch ran (fault check at readouts)
+    hipk::FlowCtl* flow_ctl_ = nullptr;     // its ticket / epoch / fault words
+    i64 flow_blocks_ = 0;                   // its persistent grid (workgroups)
+    std::map<int, FlowDev> flow_plans_;     // by superstep depth
     bool res_ = false;  // supersteps run the resident kernel
     int res_kin_ = 0;   // its generations per in-kernel halo exchange
     std::map<int, ResPlan> res_plans_;

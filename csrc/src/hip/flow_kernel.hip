@@ -1,0 +1,207 @@
+// gol-mi355x: step_flow — a whole superstep (several register-pipeline passes) as ONE launch, its
+// work items scheduled by data dependencies instead of kernel boundaries.
+//
+// The pass kernels (step_temporal, step_kernels.hip) run a superstep of G generations as G / K
+// launches: every launch streams the board once through K levels of the register pipeline and the
+// next pass starts only when the LAST wave of the previous one has finished.  On MI355X the co-resident
+// waves of a SIMD do not finish together (VALU issue is arbitrated by age), so every pass boundary
+// idles most wave slots while its slowest waves drain, and the first waves of the next pass start
+// late (docs/PERFORMANCE.md §6: ~20 us of a 20-generation superstep).  Here:
+//
+//  * A superstep's passes are cut into work items (FlowItem, plan.hpp build_flow_plan): one plan wave
+//    of one pass each (the same segments and lane layout as step_temporal's plans), listed in ONE
+//    global ticket order: every item of pass j comes before any item of pass j + 1, and inside a pass
+//    the items run down the board in row bands (with the torus wrap, pass j starts one band further
+//    down than pass j - 1, so its first items read only the rows pass j - 1 finished first).
+//  * A persistent grid of waves (one full round of resident slots) takes tickets from a device
+//    counter; a wave that draws item t waits for the items t depends on (host-computed: the items of
+//    pass j - 1 that WRITE rows it reads, and those that READ rows it overwrites — two buffers
+//    alternate, so pass j + 1 writes the buffer pass j reads), streams the item with the
+//    step_temporal wave (wave_runner.hpp), and publishes its completion flag.  So an early-finishing
+//    wave starts on pass j + 1 as soon as its neighbourhood of pass j is done, instead of idling at a
+//    kernel boundary; only the superstep's end drains.
+//  * Deadlock freedom (no residency assumption, no cooperative launch): tickets are issued in a total
+//    order and an item depends only on items with SMALLER tickets.  A ticket is only ever drawn by a
+//    running wave, which then works on it without waiting for anything but its dependencies.  The
+//    unfinished item with the smallest ticket therefore has all its dependencies finished, so it
+//    progresses; by induction every item finishes.  Every wait is also bounded (2 s of s_memrealtime),
+//    after which the wave records a fault (FlowCtl::fault, read by the engine at every board readout)
+//    and goes on, so a bug cannot hang the GPU.
+//  * Cross-CU visibility (MI355X_MICROARCH.md, "inter-workgroup visibility", valid hand-off forms):
+//    every board-row load and store of an item is an agent-scope relaxed atomic, `global_load/store
+//    ... sc1` (write-through stores, loads that bypass the CU's L1); a wave's stores are complete at
+//    its `s_waitcnt vmcnt(0)`, after which ONE lane stores the item's flag (`sc1`); a consumer polls
+//    flags with `sc1` loads and issues its row loads only after every flag matched.  Flags hold an
+//    epoch (FlowCtl::epoch + 1 of the running launch), so they are never reset between launches: the
+//    last wave to leave a launch resets the ticket counters and advances the epoch, and the stream
+//    order puts that before the next launch.  (No scalar-cache stores or atomics anywhere: every
+//    store and atomic here is a vector memory instruction.)
+//  * Kernel boundaries still order supersteps (exchanges, graph replays and readouts see finished
+//    boards), and the launch is replayable from a captured graph: nothing in its arguments changes.
+//
+// Reference: the generation loop gol-main.c:93-116 and its per-generation launch + device sync,
+// gol-with-cuda.cu:264-284.
+#include <mutex>
+
+#include "gol/hip_kernels.hpp"
+#include "stencil_device.hpp"
+#include "wave_runner.hpp"
+
+namespace gol {
+namespace hipk {
+
+namespace {
+
+constexpr u64 kFlowWaitTicks = 200000000ull;  // 2 s of s_memrealtime (100 MHz): no real wait is that long
+
+// Wait until every dependency of an item carries the running launch's epoch.  One lane per
+// dependency (64 per sweep), `sc1` loads, a short sleep between polls.  Every branch here is on a
+// wave-uniform value (ballot, readfirstlane): a branch on a per-lane atomic load (each lane's load is
+// its own atomic, so the compiler must treat the value as divergent) makes the loops divergent, and
+// the structurizer then moved lane 0's flag store and next ticket draw out of step with the other
+// lanes' item loop (seen in the ISA of the first version).
+__device__ __forceinline__ void flow_wait(const FlowArgs& a, u32 dep_off, u32 ndeps, u32 target, int lane) {
+    for (u32 b = 0; b < ndeps; b += 64) {
+        const bool act = b + (u32)lane < ndeps;
+        const u32 dep = act ? a.deps[dep_off + b + (u32)lane] : 0u;
+        u64 t0 = 0;
+        for (int spin = 0;; ++spin) {
+            const u32 v = act ? __hip_atomic_load(&a.flags[dep], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : target;
+            const bool ready = (int)(v - target) >= 0;
+            if (__builtin_amdgcn_ballot_w64(!ready) == 0) break;
+            if (spin == 0) t0 = __builtin_amdgcn_s_memrealtime();
+            const u32 fault = __builtin_amdgcn_readfirstlane(
+                __hip_atomic_load(&a.ctl->fault, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+            if (__builtin_amdgcn_s_memrealtime() - t0 > kFlowWaitTicks || fault != 0) {
+                __hip_atomic_store(&a.ctl->fault, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // (all lanes, one word)
+                break;
+            }
+            __builtin_amdgcn_s_sleep(4);
+        }
+    }
+    asm volatile("" ::: "memory");  // the item's loads stay after the wait
+}
+
+template <int K, int ROWS>
+__device__ __forceinline__ void flow_item(const u64* src, u64* dst, const LaneDesc& d, int nrows, const StepParams& p,
+                                          i64 wave) {
+    WaveRunner<K, ROWS, true> w(src, dst, d, nrows, p, wave);
+    w.run();
+}
+
+// The depths one flow kernel instantiates (a superstep's cut uses any of them).
+#define GOL_FLOW_DEPTHS(X) X(1) X(2) X(3) X(4) X(5) X(6) X(7) X(8)
+
+// Three waves per SIMD, as step_temporal<8> (163 VGPRs): the persistent item loop around the
+// pipelines needs ~190 by default, and capping it spills 3-5 registers to scratch, reloaded once per
+// item (outside the row loops).
+template <int ROWS>
+__global__ __launch_bounds__(64 * kWavesPerBlock) __attribute__((amdgpu_waves_per_eu(3))) void step_flow(FlowArgs a,
+                                                                                                    StepParams p) {
+    const int lane = threadIdx.x & 63;
+    const i64 wave = (i64)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
+    const u32 n_waves = gridDim.x * (u32)kWavesPerBlock;
+    const u32 target = __builtin_amdgcn_readfirstlane(
+                           __hip_atomic_load(&a.ctl->epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) + 1u;
+    // (No lane-conditional code in this loop: a `lane == 0` branch around the ticket draw or the flag
+    // store let the compiler thread that condition across the loop's back edge, and lanes 1-63 went on
+    // re-running ticket 0 — the first version hung.  The draw is an all-lane atomic adding 1 from lane
+    // 0 and 0 from the others; the flag is stored by every lane to the same word.)
+    for (;;) {
+        const u32 t = __builtin_amdgcn_readfirstlane(
+            __hip_atomic_fetch_add(&a.ctl->next, lane == 0 ? 1u : 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+        if (t >= a.n_items) break;
+        // the item's fields as wave-uniform values (they steer every branch below)
+        const FlowItem* ip = a.items + t;
+        const u32 depth = __builtin_amdgcn_readfirstlane(ip->depth);
+        const u32 pass = __builtin_amdgcn_readfirstlane(ip->pass);
+        const u32 dep_off = __builtin_amdgcn_readfirstlane(ip->dep_off);
+        const u32 ndeps = __builtin_amdgcn_readfirstlane(ip->ndeps);
+        flow_wait(a, dep_off, ndeps, target, lane);
+        const LaneDesc d = a.lanes[(i64)t * kWaveLanes + lane];
+        const int nrows = __builtin_amdgcn_readfirstlane(d.nrows);
+        const bool odd = pass & 1u;
+        const u64* src = odd ? a.b : a.a;
+        u64* dst = odd ? a.a : a.b;
+        if (nrows > 0) {
+            switch (depth) {
+#define GOL_CASE(K)                                             \
+    case K:                                                     \
+        flow_item<K, ROWS>(src, dst, d, nrows, p, wave);        \
+        break;
+                GOL_FLOW_DEPTHS(GOL_CASE)
+#undef GOL_CASE
+                default:
+                    break;
+            }
+        }
+        // every store of the item has left the wave (write-through) before its flag does
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __hip_atomic_store(&a.flags[t], target, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    // The last wave out resets the tickets and advances the epoch for the next launch (every other
+    // wave has drawn its last ticket before its `done` increment).
+    {
+        const u32 left = __builtin_amdgcn_readfirstlane(
+            __hip_atomic_fetch_add(&a.ctl->done, lane == 0 ? 1u : 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+        if (left == n_waves - 1) {
+            __hip_atomic_store(&a.ctl->next, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(&a.ctl->done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(&a.ctl->epoch, target, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+}
+
+const void* flow_kernel_for(u32 flags) {
+    return (flags & STEP_WRAP_Y) ? (const void*)step_flow<ROWS_WRAP> : (const void*)step_flow<ROWS_GHOST>;
+}
+
+}  // namespace
+
+bool flow_depth_supported(int k) {
+    switch (k) {
+#define GOL_CASE(K) \
+    case K:         \
+        return true;
+        GOL_FLOW_DEPTHS(GOL_CASE)
+#undef GOL_CASE
+        default:
+            return false;
+    }
+}
+
+int flow_max_depth() { return 8; }
+
+int flow_blocks_per_cu(u32 flags) {
+    int nb = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, flow_kernel_for(flags), 64 * kWavesPerBlock, 0) != hipSuccess ||
+        nb < 1)
+        return 1;
+    return std::min(nb, 32 / kWavesPerBlock);
+}
+
+void launch_step_flow(const FlowArgs& a, i64 n_blocks, const StepParams& p, hipStream_t s) {
+    if (p.flags & STEP_SEAM) throw Error("step_flow: seam-reading passes are not supported");
+    if (n_blocks < 1) throw Error("step_flow: empty grid");
+    StepParams pp = p;
+    if (!pp.trash) pp.trash = trash_of_current_device();
+    FlowArgs aa = a;
+    void* args[] = {(void*)&aa, (void*)&pp};
+    hipError_t e = hipLaunchKernel(flow_kernel_for(p.flags), dim3((unsigned)n_blocks), dim3(64 * kWavesPerBlock), args, 0, s);
+    if (e != hipSuccess) throw Error(strprintf("step_flow launch failed: %s", hipGetErrorString(e)));
+}
+
+bool flow_fault(FlowCtl* ctl, hipStream_t s) {
+    u32 v[4] = {0, 0, 0, 0};
+    if (hipMemcpyAsync(v, ctl, sizeof(v), hipMemcpyDeviceToHost, s) != hipSuccess || hipStreamSynchronize(s) != hipSuccess)
+        throw Error("flow_fault: cannot read the control block");
+    if (v[3] == 0) return false;
+    // clear it, and the ticket state of the faulted launch (its waves all left)
+    const u32 z[4] = {0, 0, v[2], 0};
+    if (hipMemcpyAsync(ctl, z, sizeof(z), hipMemcpyHostToDevice, s) != hipSuccess || hipStreamSynchronize(s) != hipSuccess)
+        throw Error("flow_fault: cannot reset the control block");
+    return true;
+}
+
+}  // namespace hipk
+}  // namespace gol
