@@ -93,8 +93,11 @@ def main() -> int:
         return launch_children(args)
     world = int(world_env or "1")
     if world != args.gpus:
-        print(f"[bench] error: --gpus {args.gpus} but the launcher started WORLD_SIZE={world} ranks",
-              file=sys.stderr, flush=True)
+        msg = f"--gpus {args.gpus} but the launcher started WORLD_SIZE={world} ranks"
+        print(f"[bench] error: {msg}", file=sys.stderr, flush=True)
+        if os.environ.get("RANK", "0") == "0":  # the one-JSON-line contract holds for failures too
+            print(json.dumps({"metric": METRIC, "value": None, "unit": "cell-updates/s", "n_gpus": world,
+                              "error": msg}), flush=True)
         return 2
 
     import gol_amd
@@ -205,6 +208,19 @@ def main() -> int:
     start_skew = transport.allreduce_max(t0) - transport.allreduce_min(t0)
     span = transport.allreduce_max(t1) - transport.allreduce_min(t0)
     transport.barrier()
+
+    def gather(obj):
+        """Every rank's value, in rank order (rank 0 reports them)."""
+        if P == 1:
+            return [obj]
+        import torch.distributed as dist
+
+        out = [None] * P
+        dist.all_gather_object(out, obj, group=cpu_group)
+        return out
+
+    t0_min = transport.allreduce_min(t0)
+    per_rank = gather({"elapsed_us": round((t1 - t0) * 1e6, 2), "t0_offset_us": round((t0 - t0_min) * 1e6, 2)})
     pop = sim.population()
     st = sim.stats()
     halo_bytes = transport.allreduce_sum(int(st["halo_bytes"]))  # all ranks, init + warmup + timed
@@ -218,6 +234,35 @@ def main() -> int:
             if key in ph:
                 phases[key + "_max"] = round(transport.allreduce_max(ph[key]), 2)
                 phases[key + "_min"] = round(transport.allreduce_min(ph[key]), 2)
+
+    # Per-rank diagnosis of the first multi-GPU records: every rank's timing, probe
+    # phases and chosen schedule; a run whose ranks disagree on the schedule, or whose RCCL
+    # communicator does not span every rank, is an error record (non-zero exit), not a number.
+    mine = {"schedule": st["schedule"], "kernel": st["kernel"], "depth": st["depth"],
+            "kernel_depth": st["kernel_depth"],
+            "exchange_us": round(ph["exchange_us"], 2) if phases is not None and "exchange_us" in ph else None,
+            "superstep_us": round(ph["superstep_us"], 2) if phases is not None and "superstep_us" in ph else None}
+    ranks = gather(mine)
+    problems = []
+    if len({(r["schedule"], r["kernel"], r["depth"]) for r in ranks}) > 1:
+        problems.append("ranks disagree on the schedule: " +
+                        ", ".join(f"{i}:{r['schedule']}/{r['kernel']}/{r['depth']}" for i, r in enumerate(ranks)))
+    if rccl is not None and P > 1 and transport.data_plane_ranks() != P:
+        problems.append(f"the RCCL communicator spans {transport.data_plane_ranks()} of {P} ranks")
+    per_rank_block = {
+        "per_rank_elapsed_us": [r["elapsed_us"] for r in per_rank],
+        "per_rank_t0_offset_us": [r["t0_offset_us"] for r in per_rank],
+        "per_rank_exchange_us": [r["exchange_us"] for r in ranks],
+        "per_rank_superstep_us": [r["superstep_us"] for r in ranks],
+        "per_rank_schedule": [r["schedule"] for r in ranks],
+        "per_rank_kernel": [r["kernel"] for r in ranks],
+        "per_rank_depth": [r["depth"] for r in ranks],
+    }
+    if problems:
+        if rank == 0:
+            print(json.dumps({"metric": METRIC, "value": None, "unit": "cell-updates/s", "n_gpus": P,
+                              "error": "; ".join(problems), "per_rank": per_rank_block}), flush=True)
+        return 5
 
     yard = None
     if args.yardstick and rank == 0 and have_gpu:
@@ -275,6 +320,7 @@ def main() -> int:
             },
             "start_skew_us": round(start_skew * 1e6, 2),
             "phases": phases,
+            "per_rank": per_rank_block,
             "baseline_note": "reference publishes no numbers (BASELINE.md); vs_baseline is null",
         }
         if yard:

@@ -66,12 +66,17 @@ void HipEngine::res_launch(int G, u64* src, u64* dst, hipStream_t s) {
     p.G = G;
     p.S = S;
     p.kmax = (G + S - 1) / S;
-    p.timeout_ticks = 200000000ull;  // 2 s of s_memrealtime (100 MHz): a neighbour wait never takes that long
+    // 2 s of s_memrealtime (100 MHz): a neighbour wait never takes that long (GOL_RESIDENT_TIMEOUT_TICKS:
+    // test knob, e.g. 0 makes the first unsatisfied wait time out)
+    p.timeout_ticks = (u64)env_int("GOL_RESIDENT_TIMEOUT_TICKS", 200000000ll);
     hipk::launch_step_resident(rp.nw, rp.B, true, src, dst, rp.d, rp.tiles, rp.nbr_off, rp.nbr, rp.counters,
                                res_status_, p, s);
 }
 
 void HipEngine::check_res_status() {
+    // every launch enqueued so far must be done before its fault words are read (pipe_fault reads its
+    // flag with a null-stream copy, which the engine's non-blocking streams do not order)
+    if (flow_used_ || pipe_used_ || res_status_) synchronize();
     if (flow_used_ && flow_ctl_ && hipk::flow_fault(flow_ctl_, s_comp_))
         throw Error("step_flow: a dependency wait timed out (an item never saw its inputs); the board is invalid");
     if (pipe_used_ && hipk::pipe_fault())
@@ -106,7 +111,23 @@ float HipEngine::time_resident(int kin, int G) {
     HIP_CHECK(hipEventDestroy(e0));
     HIP_CHECK(hipEventDestroy(e1));
     res_kin_ = saved;
-    check_res_status();
+    // A candidate whose launches timed out (a tile gave up waiting for its neighbours: not co-resident
+    // on this box, or the test knob above) is dropped, as a step_pipe candidate whose ring wait timed
+    // out is: read and clear the status, and re-zero this plan's counters (the tiles that gave up left
+    // theirs behind the others', so later launches would wait for supersteps that never come).  Only a
+    // forced GOL_KERNEL=resident makes it fatal.
+    u32 v = 0;
+    HIP_CHECK(hipMemcpyAsync(&v, res_status_, sizeof(u32), hipMemcpyDeviceToHost, s_comp_));
+    HIP_CHECK(hipStreamSynchronize(s_comp_));
+    if (v != 0) {
+        HIP_CHECK(hipMemsetAsync(res_status_, 0, sizeof(u32), s_comp_));
+        HIP_CHECK(hipMemsetAsync(rp.counters, 0, (size_t)rp.tiles * sizeof(u32), s_comp_));
+        HIP_CHECK(hipStreamSynchronize(s_comp_));
+        if (cfg_.kernel == "resident")
+            throw Error(strprintf("GOL_KERNEL=resident: a tile timed out waiting for its neighbours (depth %d)", kin));
+        fprintf(stderr, "[gol] step_resident@%d: a neighbour wait timed out in the timing; candidate dropped\n", kin);
+        return 1e30f;
+    }
     return ms / 3 / (float)G;
 }
 

@@ -48,6 +48,13 @@ def test_bench_torchrun_two_ranks():
                 "--steps", "20", "--warmup", "2"])
     cfg = out["config"]
     assert cfg["parallelism"].endswith("p2 (1x2)")
+    # per-rank diagnosis arrays, one entry per rank, consistent with the aggregates
+    pr = out["per_rank"]
+    for key in ("per_rank_elapsed_us", "per_rank_t0_offset_us", "per_rank_exchange_us", "per_rank_superstep_us",
+                "per_rank_schedule", "per_rank_kernel", "per_rank_depth"):
+        assert len(pr[key]) == 2, (key, pr)
+    assert max(pr["per_rank_elapsed_us"]) == out["timing"]["per_rank_elapsed_max_us"]
+    assert min(pr["per_rank_t0_offset_us"]) == 0 and len(set(pr["per_rank_schedule"])) == 1
     # weak scaling: every rank owns a full tile, the global board grows with the rank count
     assert cfg["board"][0] == 2 * cfg["tile_per_rank"][0]
 
@@ -70,7 +77,10 @@ def test_bench_rank_count_mismatch_fails():
     r = subprocess.run([sys.executable, "bench.py", "--gpus", "2", "--steps", "4", "--warmup", "1"], cwd=REPO,
                        env=env, capture_output=True, text=True, timeout=120)
     assert r.returncode == 2, r.stderr[-2000:]
-    assert not [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout  # the one-JSON-line contract holds for the failure too
+    rec = json.loads(lines[0])
+    assert rec["value"] is None and "WORLD_SIZE=1" in rec["error"] and rec["n_gpus"] == 1
 
 
 def test_bench_hung_rank_ends_the_job():

@@ -67,3 +67,17 @@ def test_resident_config2_vs_torch(gol):
 def test_resident_refuses_unfit_boards(gol):
     with pytest.raises(Exception, match="resident"):
         _sim(gol, 100).init(5, seed=1)  # width % 64 != 0
+
+
+def test_resident_timeout_drops_candidate(gol, monkeypatch):
+    """A resident candidate whose neighbour waits time out in the init timing (GOL_RESIDENT_TIMEOUT_TICKS=0:
+    the first unsatisfied wait gives up) is dropped by the auto kernel choice, the board stays exact,
+    and only a forced GOL_KERNEL=resident fails."""
+    monkeypatch.setenv("GOL_RESIDENT_TIMEOUT_TICKS", "0")
+    N = 1024
+    s = _sim(gol, N, kernel="auto", subtiles=0).init(5, seed=11)
+    assert not s.stats()["kernel"].startswith("resident"), s.stats()
+    s.step(40)
+    assert np.array_equal(s.board(), numpy_step(initial_board(5, N, 1, True, 11), 40))
+    with pytest.raises(Exception, match="timed out"):
+        _sim(gol, N, kernel="resident").init(5, seed=11)
