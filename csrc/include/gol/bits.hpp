@@ -22,9 +22,9 @@
 
 #if defined(__HIPCC__)
 #include <hip/hip_runtime.h>
-#define GOL_HD __host__ __device__ __forceinline__
+#define BITS_HD __host__ __device__ __forceinline__
 #else
-#define GOL_HD inline
+#define BITS_HD inline
 #endif
 
 namespace gol {
@@ -48,7 +48,7 @@ constexpr unsigned kLutNext = lut3([](unsigned x0, unsigned alive, unsigned t34)
 static_assert(kLutOne3 == 0x16 && kLutT34 == 0x29 && kLutNext == 0xA8, "rule LUTs");
 
 // Host/reference evaluation of a 3-input LUT on 64-bit words.
-GOL_HD u64 bitop3_ref(u64 a, u64 b, u64 c, unsigned lut) {
+BITS_HD u64 bitop3_ref(u64 a, u64 b, u64 c, unsigned lut) {
     u64 r = 0;
     for (unsigned i = 0; i < 8; ++i) {
         if (!((lut >> i) & 1u)) continue;
@@ -68,7 +68,7 @@ GOL_HD u64 bitop3_ref(u64 a, u64 b, u64 c, unsigned lut) {
 // (init, pattern cells, masks, dumps) converts with split_word / merge_word.
 // ---------------------------------------------------------------------------------------------
 
-GOL_HD u64 compact_even_bits(u64 x) {  // bits 0,2,4,.. -> 0..31
+BITS_HD u64 compact_even_bits(u64 x) {  // bits 0,2,4,.. -> 0..31
     x &= 0x5555555555555555ull;
     x = (x | (x >> 1)) & 0x3333333333333333ull;
     x = (x | (x >> 2)) & 0x0F0F0F0F0F0F0F0Full;
@@ -77,7 +77,7 @@ GOL_HD u64 compact_even_bits(u64 x) {  // bits 0,2,4,.. -> 0..31
     x = (x | (x >> 16)) & 0x00000000FFFFFFFFull;
     return x;
 }
-GOL_HD u64 spread_even_bits(u64 x) {  // bits 0..31 -> 0,2,4,..
+BITS_HD u64 spread_even_bits(u64 x) {  // bits 0..31 -> 0,2,4,..
     x &= 0x00000000FFFFFFFFull;
     x = (x | (x << 16)) & 0x0000FFFF0000FFFFull;
     x = (x | (x << 8)) & 0x00FF00FF00FF00FFull;
@@ -87,19 +87,19 @@ GOL_HD u64 spread_even_bits(u64 x) {  // bits 0..31 -> 0,2,4,..
     return x;
 }
 // natural (bit b = column 64c+b) -> split storage
-GOL_HD u64 split_word(u64 v) { return compact_even_bits(v) | (compact_even_bits(v >> 1) << 32); }
+BITS_HD u64 split_word(u64 v) { return compact_even_bits(v) | (compact_even_bits(v >> 1) << 32); }
 // split storage -> natural
-GOL_HD u64 merge_word(u64 s) { return spread_even_bits(s) | (spread_even_bits(s >> 32) << 1); }
+BITS_HD u64 merge_word(u64 s) { return spread_even_bits(s) | (spread_even_bits(s >> 32) << 1); }
 // storage bit of column c within its word
-GOL_HD int storage_bit(i64 c) {
+BITS_HD int storage_bit(i64 c) {
     const int b = (int)(c & 63);
     return (b & 1) ? 32 + (b >> 1) : (b >> 1);
 }
 // valid-cell mask of storage word c of a row of width w
-GOL_HD u64 storage_mask(i64 c, i64 w) { return split_word(word_mask(c, w)); }
+BITS_HD u64 storage_mask(i64 c, i64 w) { return split_word(word_mask(c, w)); }
 
 // Horizontal 3-sum (L + C + R, 2 bits per cell) of a split-format word given its row neighbours.
-GOL_HD void hsum64(u64 prev, u64 cur, u64 next, u64& s0, u64& s1) {
+BITS_HD void hsum64(u64 prev, u64 cur, u64 next, u64& s0, u64& s1) {
     const u32 lo = (u32)cur, hi = (u32)(cur >> 32);
     const u32 prevhi = (u32)(prev >> 32), nextlo = (u32)next;
     const u32 Le = (hi << 1) | (prevhi >> 31);  // even cells: left = odd half shifted, right = odd half
@@ -111,7 +111,7 @@ GOL_HD void hsum64(u64 prev, u64 cur, u64 next, u64& s0, u64& s1) {
 }
 
 // B3/S23 from three horizontal sums (rows above, centre, below) and the centre word.
-GOL_HD u64 rule64(u64 a0, u64 a1, u64 b0, u64 b1, u64 c0, u64 c1, u64 x) {
+BITS_HD u64 rule64(u64 a0, u64 a1, u64 b0, u64 b1, u64 c0, u64 c1, u64 x) {
     u64 x0 = a0 ^ b0 ^ c0;
     u64 cy = (a0 & b0) | (a0 & c0) | (b0 & c0);
     u64 u0 = a1 ^ b1 ^ c1;
@@ -125,28 +125,28 @@ GOL_HD u64 rule64(u64 a0, u64 a1, u64 b0, u64 b1, u64 c0, u64 c1, u64 x) {
 // storage words merged back to natural order on the fly.
 struct NaturalRow {
     const u64* p;
-    GOL_HD u64 operator[](i64 i) const { return p[i]; }
+    BITS_HD u64 operator[](i64 i) const { return p[i]; }
 };
 struct SplitRow {
     const u64* p;
-    GOL_HD u64 operator[](i64 i) const { return merge_word(p[i]); }
+    BITS_HD u64 operator[](i64 i) const { return merge_word(p[i]); }
 };
 
 // Extract `n` (1..64) bits (natural order) of a row starting at column s (no wrap; s + n <= w).
 template <typename Row>
-GOL_HD u64 extract_bits(Row row, i64 s, int n) {
+BITS_HD u64 extract_bits(Row row, i64 s, int n) {
     i64 i = s >> 6;
     int off = (int)(s & 63);
     u64 v = row[i] >> off;
     if (off && off + n > 64) v |= row[i + 1] << (64 - off);
     return n >= 64 ? v : (v & ((1ull << n) - 1ull));
 }
-GOL_HD u64 extract_bits(const u64* row, i64 s, int n) { return extract_bits(NaturalRow{row}, s, n); }
+BITS_HD u64 extract_bits(const u64* row, i64 s, int n) { return extract_bits(NaturalRow{row}, s, n); }
 
 // 64 cells (natural order) of a periodic row of width w starting at (any) column `start`, i.e.
 // columns start .. start+63 taken mod w.  Used to refresh the ghost bits of an x-periodic row.
 template <typename Row>
-GOL_HD u64 wrap64(Row row, i64 w, i64 start) {
+BITS_HD u64 wrap64(Row row, i64 w, i64 start) {
     i64 s = start % w;
     if (s < 0) s += w;
     u64 res = 0;
@@ -160,12 +160,12 @@ GOL_HD u64 wrap64(Row row, i64 w, i64 start) {
     }
     return res;
 }
-GOL_HD u64 wrap64(const u64* row, i64 w, i64 start) { return wrap64(NaturalRow{row}, w, start); }
+BITS_HD u64 wrap64(const u64* row, i64 w, i64 start) { return wrap64(NaturalRow{row}, w, start); }
 
 // Ghost words of one x-periodic row in split storage.  `row` points at word 0 of the row; words
 // -1 and nw are the ghost words and columns >= w of word nw-1 are ghost cells.  Only cells in
 // [0, w) are read.  (Word-aligned widths are a pure word copy, independent of the format.)
-GOL_HD void wrap_row_ghosts(u64* row, i64 w, i64 nw) {
+BITS_HD void wrap_row_ghosts(u64* row, i64 w, i64 nw) {
     int rem = (int)(w & 63);
     if (rem == 0) {
         u64 first = row[0], last = row[nw - 1];
@@ -185,6 +185,6 @@ GOL_HD void wrap_row_ghosts(u64* row, i64 w, i64 nw) {
 
 // Fingerprint contribution of one (masked) word at global word index `gidx`.  The fingerprint is
 // the wrapping sum over all words, so it is independent of how the board is split across ranks.
-GOL_HD u64 fingerprint_word(u64 gidx, u64 word) { return word ? mix64(mix64(gidx) ^ word) : 0ull; }
+BITS_HD u64 fingerprint_word(u64 gidx, u64 word) { return word ? mix64(mix64(gidx) ^ word) : 0ull; }
 
 }  // namespace gol

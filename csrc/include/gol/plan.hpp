@@ -41,10 +41,7 @@ struct Region {
 
 static constexpr int kWaveLanes = 64;
 static constexpr int kSegWords = kWaveLanes - 2;  // output words of a full-width segment
-#ifndef GOL_WAVES_PER_BLOCK  // measurement builds (kbench) may change it
-#define GOL_WAVES_PER_BLOCK 4
-#endif
-static constexpr int kWavesPerBlock = GOL_WAVES_PER_BLOCK;  // 256-thread workgroups of independent waves
+static constexpr int kWavesPerBlock = 4;  // 256-thread workgroups of independent waves
 
 struct PlanStats {
     i64 waves = 0;        // including padding waves
@@ -58,7 +55,7 @@ struct PlanStats {
 // (only used to account for the 2k extra input rows per segment in the stats).  With `xwrap` the
 // tile is its own E/W neighbour (w % 64 == 0): halo lanes left of word 0 stream word nw-1 and halo
 // lanes right of word nw-1 stream word 0, so no ghost words are needed.
-// Waves are ordered for L2 locality: column-major, and whole workgroups of `wg_waves` waves
+// Waves are ordered for L2 locality: row-major, and whole workgroups of `wg_waves` waves
 // permuted so each of the `xcds` XCDs (workgroup b runs on XCD b % xcds) gets a contiguous stretch.
 // With `fold` (the tile kernel's STEP_TILE_FOLD) segments are packed into 32-lane tiles of <= 30
 // output words, and each tile's 64 lanes are its 32 lanes twice: the kernel folds the tile's rows so

@@ -34,23 +34,23 @@ bool mpi_launched() {
 namespace {
 
 struct MpiApi {
-#define GOL_MPI_FN(name) decltype(&::name) name = nullptr;
-    GOL_MPI_FN(MPI_Init)
-    GOL_MPI_FN(MPI_Initialized)
-    GOL_MPI_FN(MPI_Finalized)
-    GOL_MPI_FN(MPI_Finalize)
-    GOL_MPI_FN(MPI_Comm_rank)
-    GOL_MPI_FN(MPI_Comm_size)
-    GOL_MPI_FN(MPI_Send)
-    GOL_MPI_FN(MPI_Recv)
-    GOL_MPI_FN(MPI_Isend)
-    GOL_MPI_FN(MPI_Irecv)
-    GOL_MPI_FN(MPI_Waitall)
-    GOL_MPI_FN(MPI_Barrier)
-    GOL_MPI_FN(MPI_Bcast)
-    GOL_MPI_FN(MPI_Allreduce)
-    GOL_MPI_FN(MPI_Abort)
-#undef GOL_MPI_FN
+#define MPI_FN_SLOT(name) decltype(&::name) name = nullptr;
+    MPI_FN_SLOT(MPI_Init)
+    MPI_FN_SLOT(MPI_Initialized)
+    MPI_FN_SLOT(MPI_Finalized)
+    MPI_FN_SLOT(MPI_Finalize)
+    MPI_FN_SLOT(MPI_Comm_rank)
+    MPI_FN_SLOT(MPI_Comm_size)
+    MPI_FN_SLOT(MPI_Send)
+    MPI_FN_SLOT(MPI_Recv)
+    MPI_FN_SLOT(MPI_Isend)
+    MPI_FN_SLOT(MPI_Irecv)
+    MPI_FN_SLOT(MPI_Waitall)
+    MPI_FN_SLOT(MPI_Barrier)
+    MPI_FN_SLOT(MPI_Bcast)
+    MPI_FN_SLOT(MPI_Allreduce)
+    MPI_FN_SLOT(MPI_Abort)
+#undef MPI_FN_SLOT
 };
 
 const MpiApi& mpi() {
@@ -60,25 +60,25 @@ const MpiApi& mpi() {
     const char* path = getenv("GOL_MPI_LIB");
     void* h = dlopen(path && *path ? path : GOL_MPI_LIB_PATH, RTLD_NOW | RTLD_GLOBAL);
     if (!h) throw Error(std::string("cannot load the MPI library: ") + dlerror());
-#define GOL_MPI_SYM(name)                                                     \
+#define MPI_SYM_SLOT(name)                                                     \
     api.name = reinterpret_cast<decltype(api.name)>(dlsym(h, #name));        \
     if (!api.name) throw Error("MPI library lacks " #name);
-    GOL_MPI_SYM(MPI_Init)
-    GOL_MPI_SYM(MPI_Initialized)
-    GOL_MPI_SYM(MPI_Finalized)
-    GOL_MPI_SYM(MPI_Finalize)
-    GOL_MPI_SYM(MPI_Comm_rank)
-    GOL_MPI_SYM(MPI_Comm_size)
-    GOL_MPI_SYM(MPI_Send)
-    GOL_MPI_SYM(MPI_Recv)
-    GOL_MPI_SYM(MPI_Isend)
-    GOL_MPI_SYM(MPI_Irecv)
-    GOL_MPI_SYM(MPI_Waitall)
-    GOL_MPI_SYM(MPI_Barrier)
-    GOL_MPI_SYM(MPI_Bcast)
-    GOL_MPI_SYM(MPI_Allreduce)
-    GOL_MPI_SYM(MPI_Abort)
-#undef GOL_MPI_SYM
+    MPI_SYM_SLOT(MPI_Init)
+    MPI_SYM_SLOT(MPI_Initialized)
+    MPI_SYM_SLOT(MPI_Finalized)
+    MPI_SYM_SLOT(MPI_Finalize)
+    MPI_SYM_SLOT(MPI_Comm_rank)
+    MPI_SYM_SLOT(MPI_Comm_size)
+    MPI_SYM_SLOT(MPI_Send)
+    MPI_SYM_SLOT(MPI_Recv)
+    MPI_SYM_SLOT(MPI_Isend)
+    MPI_SYM_SLOT(MPI_Irecv)
+    MPI_SYM_SLOT(MPI_Waitall)
+    MPI_SYM_SLOT(MPI_Barrier)
+    MPI_SYM_SLOT(MPI_Bcast)
+    MPI_SYM_SLOT(MPI_Allreduce)
+    MPI_SYM_SLOT(MPI_Abort)
+#undef MPI_SYM_SLOT
     loaded = true;
     return api;
 }

@@ -155,19 +155,17 @@ std::vector<LaneDesc> build_plan(const std::vector<Region>& regions, i64 nw, i64
     // XCD-aware order.  The full-width segments are sorted (narrow, packed waves stay last), then
     // whole workgroups are permuted so that XCD x — workgroup b is dispatched to XCD b % xcds — runs
     // a contiguous stretch of that order: neighbouring segments, which share halo rows and words,
-    // are hits in its own L2.  Row-major (default): the full-width segments of a row band are consecutive, so an XCD's
-    // stretch of the order is a band of whole rows and its stores cover whole rows of HBM.  The
-    // column-major order (GOL_PLAN_ORDER=col, round 1's choice for vertical halo reuse in L2, which
-    // a band of rows keeps too) left each XCD writing one 496-byte piece of every row: measured
-    // 32768^2 K=1 passes 71 -> 61 us, K=4 17.5 -> 16.1 us/gen, K=8 11.49 -> 11.20 (two halves on two
-    // streams), 16384^2 K=8 4.20 -> 4.11 (profiles/plan_order_ab.txt).
-    const bool row_major = !(getenv("GOL_PLAN_ORDER") && std::string(getenv("GOL_PLAN_ORDER")) == "col");
-    std::stable_sort(packed.begin(), packed.end(), [row_major, lw](const std::vector<Item>& a, const std::vector<Item>& b) {
+    // are hits in its own L2.  Row-major: the full-width segments of a row band are consecutive, so an
+    // XCD's stretch of the order is a band of whole rows and its stores cover whole rows of HBM.  (The
+    // column-major order, round 1's choice for vertical halo reuse in L2, which a band of rows keeps
+    // too, left each XCD writing one 496-byte piece of every row: measured 32768^2 K=1 passes 71 -> 61
+    // us, K=4 17.5 -> 16.1 us/gen, K=8 11.49 -> 11.20 (two halves on two streams), 16384^2 K=8 4.20 ->
+    // 4.11 with row-major, profiles/plan_order_ab.txt.)
+    std::stable_sort(packed.begin(), packed.end(), [lw](const std::vector<Item>& a, const std::vector<Item>& b) {
         const bool fa = a.size() == 1 && a[0].lanes() == lw, fb = b.size() == 1 && b[0].lanes() == lw;
         if (fa != fb) return fa;
         if (!fa) return false;
-        if (row_major) return a[0].r0 != b[0].r0 ? a[0].r0 < b[0].r0 : a[0].c0 < b[0].c0;
-        return a[0].c0 != b[0].c0 ? a[0].c0 < b[0].c0 : a[0].r0 < b[0].r0;
+        return a[0].r0 != b[0].r0 ? a[0].r0 < b[0].r0 : a[0].c0 < b[0].c0;
     });
     std::vector<std::vector<Item>> waves((size_t)nwaves);
     if (wg_waves < 1 || nwaves % wg_waves) wg_waves = 1;

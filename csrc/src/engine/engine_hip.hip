@@ -91,17 +91,16 @@ HipEngine::HipEngine(const Geometry& g, const EngineConfig& c, std::shared_ptr<T
     HIP_CHECK(hipDeviceGetStreamPriorityRange(&prio_least, &prio_greatest));
     HIP_CHECK(hipStreamCreateWithPriority(&s_comp_, hipStreamNonBlocking, 0));
     HIP_CHECK(hipStreamCreateWithPriority(&s_comm_, hipStreamNonBlocking,
-                                          env_int("GOL_COMM_PRIORITY", 1) ? prio_greatest : 0));
+                                          prio_greatest));
     events_needed_ = cfg_.force_split || !halo_items(L_.R).empty();
     // All device memory work is ordered on the engine's own streams.  (They are non-blocking:
     // null-stream calls such as hipMemset, or a pageable hipMemcpy whose DMA may still be in
     // flight when it returns, would NOT be ordered before their kernels.)
     for (int i = 0; i < 2; ++i) HIP_CHECK(hipMemsetAsync(buf_[i], 0, bytes, s_comp_));
     HIP_CHECK(hipStreamSynchronize(s_comp_));
-    // Stream-ordering events (never read by the host).  GOL_EVENT_SCOPE=device asks for a
-    // device-scope release instead of the default system-scope fence (measurement knob).
-    const unsigned evf = hipEventDisableTiming |
-                         (env_str("GOL_EVENT_SCOPE", "system") == "device" ? hipEventReleaseToDevice : 0u);
+    // Stream-ordering events (never read by the host).  (A device-scope release instead of the default
+    // system-scope fence measured no faster: docs/PERFORMANCE.md §5.)
+    const unsigned evf = hipEventDisableTiming;
     HIP_CHECK(hipEventCreateWithFlags(&ev_ready_, evf));
     HIP_CHECK(hipEventCreateWithFlags(&ev_halo_, evf));
     if (cfg_.profile) {
@@ -312,10 +311,8 @@ void HipEngine::do_init(const PatternSpec& p) {
         // The comm stream waits on the compute stream's ready event only in the split
         // schedule (and the forced-split measurement mode).  The full schedule
         // exchanges on the compute stream itself: recording the event there every superstep
-        // only idles the GPU (~15 us per record, a release fence).  GOL_READY_EVENTS=always
-        // restores the record (measurement knob).
-        events_needed_ = cfg_.force_split || (split_ && !halo_items(L_.R).empty()) ||
-                         env_str("GOL_READY_EVENTS", "") == "always";
+        // only idles the GPU (~15 us per record, a release fence).
+        events_needed_ = cfg_.force_split || (split_ && !halo_items(L_.R).empty());
     }
     stats_.kernel = split_ ? kern_[1] + "+boundary:" + kern_[2] : (dual_ ? std::string("temporal") : kern_[0]);
     if (!split_ && !dual_ && kern_[0] == "pipe")

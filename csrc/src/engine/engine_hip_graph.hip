@@ -62,9 +62,8 @@ void HipEngine::prewarm_graph() {
 
 // Replays, largest shape first (eager launches of a superstep cost ~15 us of GPU idle each;
 // graph replays none), every ladder shape captured at init.  The remainder no shape covers runs
-// eagerly.  (GOL_REMAINDER_GRAPHS=1, measurement knob, ranks without neighbours: the remainder as a
-// graph of that one short superstep, captured on first use — milliseconds inside that run; it did
-// not change the 8192^2 warmup anomaly, docs/PERFORMANCE.md §6.)
+// eagerly.  (A graph of that one short remainder, captured on first use, did not change the 8192^2
+// warmup anomaly, docs/PERFORMANCE.md §6, and was removed.)
 void HipEngine::run_graphed(u64& generations) {
     int k = 0, M = 0;
     if (!graph_shape(k, M)) return;
@@ -75,14 +74,6 @@ void HipEngine::run_graphed(u64& generations) {
             if (!exec) return;
             replay(exec, k, sh.m, sh.rem);
             generations -= per;
-        }
-    }
-    if (generations > 0 && generations < (u64)k && graph_ok_ && (cfg_.compat || halo_items(k).empty()) &&
-        env_int("GOL_REMAINDER_GRAPHS", 0) != 0) {
-        const int rem = (int)generations;
-        if (hipGraphExec_t exec = graph_for(k, 0, rem)) {
-            replay(exec, k, 0, rem);
-            generations = 0;
         }
     }
 }

@@ -60,8 +60,7 @@ const std::vector<int>& HipEngine::pass_depths(int k) {
                     pick[(size_t)x] = dc.first;
                 }
         for (int x = k; x > 0; x -= pick[(size_t)x]) ps.push_back(pick[(size_t)x]);
-        std::sort(ps.begin(), ps.end(), std::greater<int>());
-        if (env_int("GOL_PASS_ASCENDING", 0) != 0) std::reverse(ps.begin(), ps.end());  // measurement knob
+        std::sort(ps.begin(), ps.end(), std::greater<int>());  // deepest first (8 + 12 measured slower than 12 + 8)
         return passes_.emplace(key, ps).first->second;
     }
     const int n = (k + K - 1) / K;

@@ -6,8 +6,8 @@ namespace hipeng {
 
 void HipEngine::setup_dual() {
     if (sub_buf_[0][0]) return;
-    // GOL_SUB_SPLIT (per mille, measurement knob): rows of half 0 as a fraction of the tile
-    const i64 frac = std::max<i64>(100, std::min<i64>(900, env_int("GOL_SUB_SPLIT", 500)));
+    // equal halves (52/48 and 48/52 splits measured no better: docs/PERFORMANCE.md §6)
+    const i64 frac = 500;
     const i64 h0 = std::max<i64>(8 * (i64)L_.R, std::min<i64>(L_.h - 8 * (i64)L_.R, L_.h * frac / 1000));
     sub_r0_[0] = 0;
     sub_r0_[1] = h0;
@@ -157,7 +157,7 @@ void HipEngine::dual_superstep(int k) {
         const int np = (int)pass_depths(k).size();
         for (int j = 0; j < np; ++j)
             for (int i = 0; i < 2; ++i) {
-                const int s = sub_first_ ^ i;  // GOL_SUB_FIRST=1: half 1's pass first (measurement knob)
+                const int s = i;  // half 0's pass first (half 1 first measured no better: docs/PERFORMANCE.md §6)
                 if (!((ov && s == 0 && j == 0) || (ov2 && j == 0))) {
                     if (j == 0 && i == 0) trace::mark("gol.launch0");  // (GOL_ROCTX: host side of the launch latency)
                     launch_half(s, p, k, s ? s_comm_ : s_comp_, j);

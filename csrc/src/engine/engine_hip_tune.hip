@@ -14,22 +14,6 @@ void HipEngine::spin_up() {
     const bool big = (double)L_.h * (double)L_.w >= (double)(1 << 24);
     const double budget_ms = (double)env_int("GOL_SPINUP_MS", big ? 100 : 20);
     if (budget_ms <= 0 || cfg_.compat || kernel_ == "lds") return;
-    // GOL_SPINUP_DUAL=1 (measurement knob, sub-tile ranks without neighbours): spin up on the runs'
-    // own schedule, scratch sub-tile supersteps of the hinted run's length on both streams (the halves
-    // are reloaded from the board at the next run)
-    if (dual_ && env_int("GOL_SPINUP_DUAL", 0) != 0 && halo_items(L_.R).empty() && !xchg_self_) {
-        const std::vector<int> ks = init_depths();
-        const int k = ks.back();
-        const auto t0 = std::chrono::steady_clock::now();
-        for (int it = 0; it < 100000; ++it) {
-            for (int j = 0; j < 4; ++j) dual_superstep(k);
-            synchronize();
-            if (std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count() >= budget_ms) break;
-        }
-        sub_current_ = false;
-        stats_.graph_launches = 0;
-        return;
-    }
     const std::string saved = kern_[0];
     int k = 0;
     if (!dual_ && kern_[0] == "pipe" && pipe_k_ > 0) {

@@ -224,7 +224,7 @@ class HipEngine : public Engine {
         // ev_sub_a_ / ev_sub_b_ are recorded only where events_synced_ is cleared: after synchronize()
         // and before the next record they are complete, so the query (a runtime call before the
         // superstep's first launch) is skipped
-        if (events_synced_ && skip_synced_query_) return;
+        if (events_synced_) return;
         const hipError_t q = hipEventQuery(ev);
         if (q == hipSuccess) return;
         if (q != hipErrorNotReady) HIP_CHECK(q);
@@ -621,14 +621,12 @@ class HipEngine : public Engine {
     i64 sub_r0_[2] = {0, 0};
     u64* sub_buf_[2][3] = {{nullptr, nullptr, nullptr}, {nullptr, nullptr, nullptr}};
     int sub_cur_ = 0;  // buffer (0..2) holding both halves' current generation
-    int sub_first_ = (int)(env_int("GOL_SUB_FIRST", 0) != 0);  // half whose pass j is launched first
     bool sub_current_ = false;  // the halves hold the current board
     bool canon_stale_ = false;  // buf_[cur_] lags the halves (sync_canonical before reading it)
     std::map<int, DevPlan> sub_plans_;
     std::map<int, hipGraphExec_t> dual_graphs_;  // (half, start buffer, depth) -> launch_half graph
     hipEvent_t ev_sub_a_ = nullptr, ev_sub_b_ = nullptr;  // half 0 / half 1 done with its last superstep
     bool events_synced_ = false;  // both streams synchronised since ev_sub_a_ / ev_sub_b_ were last recorded
-    const bool skip_synced_query_ = env_int("GOL_SKIP_SYNCED_QUERY", 1) != 0;  // (measurement knob)
                                                            // (ev_sub_own_, or a progress marker's pair)
     hipEvent_t ev_sub_own_[2] = {nullptr, nullptr};
     hipEvent_t ev_sub_x_ = nullptr;                        // the rank's exchange (into both halves) done

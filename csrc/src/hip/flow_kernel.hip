@@ -90,7 +90,7 @@ __device__ __forceinline__ void flow_item(const u64* src, u64* dst, const LaneDe
 }
 
 // The depths one flow kernel instantiates (a superstep's cut uses any of them).
-#define GOL_FLOW_DEPTHS(X) X(1) X(2) X(3) X(4) X(5) X(6) X(7) X(8)
+#define FLOW_DEPTHS(X) X(1) X(2) X(3) X(4) X(5) X(6) X(7) X(8)
 
 // Three waves per SIMD, as step_temporal<8> (163 VGPRs): the persistent item loop around the
 // pipelines needs ~190 by default, and capping it spills 3-5 registers to scratch, reloaded once per
@@ -125,12 +125,12 @@ __global__ __launch_bounds__(64 * kWavesPerBlock) __attribute__((amdgpu_waves_pe
         u64* dst = odd ? a.a : a.b;
         if (nrows > 0) {
             switch (depth) {
-#define GOL_CASE(K)                                             \
+#define DEPTH_CASE(K)                                             \
     case K:                                                     \
         flow_item<K, ROWS>(src, dst, d, nrows, p, wave);        \
         break;
-                GOL_FLOW_DEPTHS(GOL_CASE)
-#undef GOL_CASE
+                FLOW_DEPTHS(DEPTH_CASE)
+#undef DEPTH_CASE
                 default:
                     break;
             }
@@ -160,11 +160,11 @@ const void* flow_kernel_for(u32 flags) {
 
 bool flow_depth_supported(int k) {
     switch (k) {
-#define GOL_CASE(K) \
+#define DEPTH_CASE(K) \
     case K:         \
         return true;
-        GOL_FLOW_DEPTHS(GOL_CASE)
-#undef GOL_CASE
+        FLOW_DEPTHS(DEPTH_CASE)
+#undef DEPTH_CASE
         default:
             return false;
     }

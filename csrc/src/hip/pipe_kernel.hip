@@ -41,26 +41,13 @@ namespace hipk {
 
 namespace {
 
-#ifndef GOL_PIPE_U
-#define GOL_PIPE_U 3
-#endif
-#ifndef GOL_PIPE_RING
-#define GOL_PIPE_RING 18
-#endif
-#ifndef GOL_PIPE_SYNC
-#define GOL_PIPE_SYNC 3
-#endif
-constexpr int kPipeSync = GOL_PIPE_SYNC;  // rows between counter updates (1 or 3)
-constexpr int kPipeU = GOL_PIPE_U;        // rows of every stage's register queue (its prefetch distance)
-constexpr int kPipeRing = GOL_PIPE_RING;  // rows per LDS ring between compute stages (>= kPipeU + 3, multiple of 6)
-#ifndef GOL_PIPE_LOADAHEAD
-#define GOL_PIPE_LOADAHEAD 12
-#endif
-constexpr int kPipeLoadAhead = GOL_PIPE_LOADAHEAD;  // rows the loader keeps in flight (2 DMAs per row, <= 31)
-#ifndef GOL_PIPE_RING0
-#define GOL_PIPE_RING0 18
-#endif
-constexpr int kPipeRing0 = GOL_PIPE_RING0;  // rows of the loader's ring (>= kPipeLoadAhead + kPipeU + 3)
+// Ring geometry (measured, docs/PERFORMANCE.md §13: a 3-row register queue with 18-row rings ran
+// 10.55 us/gen at 32768^2 where a 6-row queue or per-row counters were slower)
+constexpr int kPipeSync = 3;       // rows between counter updates
+constexpr int kPipeU = 3;          // rows of every stage's register queue (its prefetch distance)
+constexpr int kPipeRing = 18;      // rows per LDS ring between compute stages (>= kPipeU + 3, multiple of 6)
+constexpr int kPipeLoadAhead = 12; // rows the loader keeps in flight (2 DMAs per row, <= 31)
+constexpr int kPipeRing0 = 18;     // rows of the loader's ring (>= kPipeLoadAhead + kPipeU + 3)
 constexpr int kRowU32 = 128;    // one ring row: 64 lo words, then 64 hi words (LDS DMA writes planes)
 
 typedef __attribute__((address_space(3))) void lds_void_t;
@@ -70,10 +57,7 @@ typedef __attribute__((address_space(1))) void glb_void_t;
 // wave's DS operations in order, so ring rows written before a counter store are in LDS before the
 // store is, and a consumer's ring reads, issued after it saw the counter, come after it.  (Release /
 // acquire atomics would add s_waitcnt lgkmcnt(0) and, in the loader, vmcnt(0) — a wait for every DMA
-// in flight.)  GOL_PIPE_STRICT=1 adds the lgkmcnt(0) wait before every counter store anyway.
-#ifndef GOL_PIPE_STRICT
-#define GOL_PIPE_STRICT 0
-#endif
+// in flight.)
 // In the loader the counter accesses are inline asm: the compiler treats any LDS access after an LDS
 // DMA as possibly aliasing it and would wait for every DMA in flight (vmcnt(0)) before each of them.
 __device__ __forceinline__ u32 lds_addr(const void* p) {
@@ -92,7 +76,6 @@ __device__ __forceinline__ u32 ctr_load(const u32* c) {
 template <bool ASM = false>
 __device__ __forceinline__ void ctr_store(u32* c, u32 v) {
     asm volatile("" ::: "memory");
-    if (GOL_PIPE_STRICT) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     if constexpr (ASM) {
         asm volatile("ds_write_b32 %0, %1" ::"v"(lds_addr(c)), "v"(v) : "memory");
     } else {
@@ -282,7 +265,7 @@ __device__ __forceinline__ void stage(RingIn<RIN>& in, Out& out, int n) {
         q[j] = i0 + j < n ? in.template read<i0 + j>() : make_uint2(0, 0);
     });
     // U rows from row i (i - i0 a multiple of U, so every slot below is a constant); TAIL: stop at n
-    // Synchronisation every S rows (GOL_PIPE_SYNC): at a group's first row the output slots are
+    // Synchronisation every S rows (kPipeSync): at a group's first row the output slots are
     // reserved and both counters are read early (peek); at its last row the outputs are published, the
     // inputs released, and the queue registers of the group refilled kPipeU rows ahead.
     constexpr int S = kPipeSync;
@@ -322,9 +305,7 @@ __device__ __forceinline__ void stage(RingIn<RIN>& in, Out& out, int n) {
                         if (nx + j < n) q[(r - (S - 1) + j) % kPipeU] = in.template read<i0 + a + j>();
                     });
                 }
-#if !defined(GOL_PIPE_NOSB)
                 if (S == 3 || r % 3 == 2) __builtin_amdgcn_sched_barrier(0);
-#endif
             }
         });
     };
@@ -364,16 +345,6 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(5))) vo
         return;
     }
     const int st = wv - 1;                     // compute stage
-#if defined(GOL_PIPE_PRIO) && GOL_PIPE_PRIO == 1
-    // downstream stages first: a consumer runs as soon as its input is there
-    if (st * 4 >= 3 * (NW - 1)) __builtin_amdgcn_s_setprio(3);
-    else if (st * 4 >= 2 * (NW - 1)) __builtin_amdgcn_s_setprio(2);
-    else if (st * 4 >= (NW - 1)) __builtin_amdgcn_s_setprio(1);
-#elif defined(GOL_PIPE_PRIO) && GOL_PIPE_PRIO == 2
-    if (st * 4 < (NW - 1)) __builtin_amdgcn_s_setprio(3);
-    else if (st * 4 < 2 * (NW - 1)) __builtin_amdgcn_s_setprio(2);
-    else if (st * 4 < 3 * (NW - 1)) __builtin_amdgcn_s_setprio(1);
-#endif
     const int n = nrows + 2 * K - 2 * st * L;  // its input rows
     auto run = [&](auto in) {
         in.ring = ring_of(st) + lane;

@@ -43,15 +43,8 @@ namespace hipk {
 
 namespace {
 
-// GOL_TEMPORAL_WAVES_PER_EU (build-time experiment knob): minimum waves per SIMD the register
-// allocator must fit (e.g. 4 caps K=8 at 128 VGPRs instead of its natural 163).
-#ifdef GOL_TEMPORAL_WAVES_PER_EU
-#define GOL_TEMPORAL_OCC __attribute__((amdgpu_waves_per_eu(GOL_TEMPORAL_WAVES_PER_EU)))
-#else
-#define GOL_TEMPORAL_OCC
-#endif
 template <int K, int ROWS>
-__global__ __launch_bounds__(64 * kWavesPerBlock) GOL_TEMPORAL_OCC void step_temporal(const u64* __restrict__ src, u64* __restrict__ dst,
+__global__ __launch_bounds__(64 * kWavesPerBlock) void step_temporal(const u64* __restrict__ src, u64* __restrict__ dst,
                                                                       const LaneDesc* __restrict__ plan, StepParams p) {
     const int wv = threadIdx.x >> 6;
     const i64 wave = (i64)blockIdx.x * kWavesPerBlock + wv;
@@ -129,15 +122,10 @@ struct RowsSplit {
 };
 
 // Two register triples in the band loop for LDS passes of 4 levels (8192^2 tile@24: 1.457-1.494 ->
-// 1.437-1.453 us/gen; no gain at 2 levels, profiles/pingpong_loop_ab.txt).  GOL_TILE_PINGPONG=0/1
-// forces it off / on for every level count.
+// 1.437-1.453 us/gen; no gain at 2 levels, profiles/pingpong_loop_ab.txt).
 template <int LV>
 constexpr bool tile_pingpong() {
-#ifdef GOL_TILE_PINGPONG
-    return GOL_TILE_PINGPONG != 0;
-#else
     return LV >= 4;
-#endif
 }
 // Stream input rows 0 .. n-1 of `in` (n >= 2*LV+1) through an LV-level register window (LV
 // generations per LDS pass); outputs rows LV .. n-LV-1.
@@ -145,7 +133,7 @@ template <int LV, typename SRC, typename SINK>
 __device__ __forceinline__ void tile_band(const SRC& in, int n, SINK& out, int lane) {
     Pipe<LV> P;
     u32 lo, hi;
-#define GOL_TILE_ROW(PH, GUARD, IDX)                                   \
+#define TILE_ROW_STEP(PH, GUARD, IDX)                                   \
     lo = in.lo((IDX), lane);                                           \
     hi = in.hi((IDX), lane);                                           \
     if (advance<LV, PH, GUARD>(P, lo, hi, (IDX))) out.put(lo, hi);
@@ -153,13 +141,13 @@ __device__ __forceinline__ void tile_band(const SRC& in, int n, SINK& out, int l
     int i = 0;
     for (; i < i0; i += 3) {
         if (i < n) {
-            GOL_TILE_ROW(0, true, i)
+            TILE_ROW_STEP(0, true, i)
         }
         if (i + 1 < n) {
-            GOL_TILE_ROW(1, true, i + 1)
+            TILE_ROW_STEP(1, true, i + 1)
         }
         if (i + 2 < n) {
-            GOL_TILE_ROW(2, true, i + 2)
+            TILE_ROW_STEP(2, true, i + 2)
         }
     }
     // Steady state, software-pipelined: the next triple's LDS reads are issued before this triple's
@@ -218,7 +206,7 @@ __device__ __forceinline__ void tile_band(const SRC& in, int n, SINK& out, int l
         lo = l1, hi = h1;
         if (advance<LV, 1, false>(P, lo, hi, i + 1)) out.put(lo, hi);
     }
-#undef GOL_TILE_ROW
+#undef TILE_ROW_STEP
 }
 
 // Side rows per wave of the in-place tile: its 2*LV halo rows plus the band stream's over-read.
@@ -275,22 +263,6 @@ __device__ __forceinline__ void tile_pass(u32* A, u32* B, u32* side, u64* dst, c
     }
 }
 
-#ifdef GOL_TILE_STAMPS
-// Diagnostic build only (tools/kbench with -DGOL_TILE_STAMPS): s_memtime stamps per workgroup at
-// the kernel start, after the staging barrier and after every LDS pass, for a time breakdown.
-constexpr int kStampSlots = 48, kStampSlotsLast = kStampSlots - 1;
-__device__ unsigned long long g_tile_stamps[4096 * kStampSlots];
-__device__ __forceinline__ void tile_stamp(int wv, int lane, int slot) {
-    unsigned long long t;
-    __builtin_amdgcn_sched_barrier(0);
-    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
-    __builtin_amdgcn_sched_barrier(0);
-    if (wv == 0 && lane == 0 && blockIdx.x < 4096 && slot < kStampSlots) g_tile_stamps[blockIdx.x * kStampSlots + slot] = t;
-}
-#define GOL_STAMP(slot) tile_stamp(wv, lane, (slot))
-#else
-#define GOL_STAMP(slot) ((void)0)
-#endif
 
 template <int NW, bool WRAPY, int LV, bool IP>
 __global__ __launch_bounds__(64 * NW) void step_tile(const u64* __restrict__ src, u64* __restrict__ dst,
@@ -301,7 +273,6 @@ __global__ __launch_bounds__(64 * NW) void step_tile(const u64* __restrict__ src
     const LaneDesc d = plan[(i64)blockIdx.x * kWaveLanes + lane];
     const int nrows = __builtin_amdgcn_readfirstlane(d.nrows);
     if (nrows <= 0) return;  // padding tile (uniform over the workgroup)
-    GOL_STAMP(0);
     const int n_in = nrows + 2 * K;
     u32* A = tile_lds;
     u32* B = tile_lds + n_in * kTileRowU32;  // double-buffered: the second tile buffer
@@ -318,9 +289,6 @@ __global__ __launch_bounds__(64 * NW) void step_tile(const u64* __restrict__ src
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    GOL_STAMP(1);
-    int npass = 0;
-    (void)npass;
 
     // 2. K generations in LDS passes of up to LV levels (the last passes take what is left); the pass
     // starting at generation g with lv levels computes tile rows [g+lv, n_in-g-lv).  More levels per
@@ -339,10 +307,8 @@ __global__ __launch_bounds__(64 * NW) void step_tile(const u64* __restrict__ src
             tile_pass<NW, 1, IP>(A, B, side, dst, d, p, K, g, n_in, wv, lane);
         }
         g += lv;
-        ++npass;
         if (g < K) {
             __syncthreads();
-            GOL_STAMP(1 + npass);
             if constexpr (!IP) {
                 u32* t = A;
                 A = B;
@@ -350,7 +316,6 @@ __global__ __launch_bounds__(64 * NW) void step_tile(const u64* __restrict__ src
             }
         }
     }
-    GOL_STAMP(kStampSlotsLast);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -594,15 +559,15 @@ __global__ __launch_bounds__(256) void step_lds(const u64* __restrict__ src, u64
 
 // Instantiated depths.  Larger K amortises HBM traffic over more generations at the cost of
 // registers (10 VGPRs per level per lane) and 2K halo rows per segment.
-#define GOL_FOR_EACH_DEPTH(X) X(1) X(2) X(3) X(4) X(5) X(6) X(7) X(8) X(12) X(16)
+#define FOR_EACH_STEP_DEPTH(X) X(1) X(2) X(3) X(4) X(5) X(6) X(7) X(8) X(12) X(16)
 
 bool step_depth_supported(int k) {
     switch (k) {
-#define GOL_CASE(K) \
+#define DEPTH_CASE(K) \
     case K:         \
         return true;
-        GOL_FOR_EACH_DEPTH(GOL_CASE)
-#undef GOL_CASE
+        FOR_EACH_STEP_DEPTH(DEPTH_CASE)
+#undef DEPTH_CASE
         default:
             return false;
     }
@@ -612,11 +577,11 @@ int max_step_depth() { return 16; }
 
 static const void* kernel_of(int k, u32 flags) {
     switch (k) {
-#define GOL_CASE(K) \
+#define DEPTH_CASE(K) \
     case K:         \
         return kernel_for<K>(flags);
-        GOL_FOR_EACH_DEPTH(GOL_CASE)
-#undef GOL_CASE
+        FOR_EACH_STEP_DEPTH(DEPTH_CASE)
+#undef DEPTH_CASE
         default:
             return nullptr;
     }
@@ -723,11 +688,6 @@ void launch_step_tile(int nw_per_wg, int k, const u64* src, u64* dst, const Lane
     if (e != hipSuccess) throw Error(strprintf("step_tile launch failed: %s", hipGetErrorString(e)));
 }
 
-#ifdef GOL_TILE_STAMPS
-void read_tile_stamps(unsigned long long* out, size_t n) {
-    (void)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_tile_stamps), n * sizeof(unsigned long long));
-}
-#endif
 
 void launch_step_lds(const u64* src, u64* dst, const Layout& L, i64 r0, i64 r1, u32 flags, hipStream_t s) {
     if (r1 <= r0) return;

@@ -48,28 +48,21 @@ enum { ROWS_GHOST = 0, ROWS_WRAP = 1, ROWS_SEAM = 2 };
 // Prefetch depth in rows.  Deep passes (K >= 5) are VALU bound and keep one row-triple in flight
 // (registers are what limits their occupancy).  Shallow passes are memory bound: a whole-board pass
 // at K <= 4 costs ~70 us at 32768^2 whatever K is, i.e. ~3.8 TB/s, limited by the bytes each wave
-// keeps in flight, so they prefetch two row-triples ahead (GOL_SHALLOW_PF=0 at build time: one).
-#ifndef GOL_SHALLOW_PF
-#define GOL_SHALLOW_PF 1
-#endif
+// keeps in flight, so they prefetch two row-triples ahead.
 template <int K>
 constexpr int prefetch_rows() {
-    return (GOL_SHALLOW_PF && K <= 4) ? 6 : 3;
+    return K <= 4 ? 6 : 3;
 }
 // Deep passes whose one-triple steady loop the compiler schedules with a wait on the fresh prefetch
 // (see WaveRunner::run) use the two-triple loop: K = 6, 7 and 12.  Measured at 32768^2, two halves
 // (profiles/pingpong_loop_ab.txt): K=7 12.2 -> 10.9 us/gen, K=12 12.8 -> 10.6, K=6 12.0 -> 11.8;
-// K=5 and 8 do not gain.  GOL_PINGPONG_MASK (bit K) overrides the set at build time.
-#ifndef GOL_PINGPONG_MASK
-#define GOL_PINGPONG_MASK ((1 << 6) | (1 << 7) | (1 << 12))
-#endif
+// K=5 and 8 do not gain.
+constexpr unsigned kPingpongMask = (1u << 6) | (1u << 7) | (1u << 12);
 // ... and, for the ghost-row variant only (the sub-tile passes after the first), K = 5
-#ifndef GOL_PINGPONG_GHOST_MASK
-#define GOL_PINGPONG_GHOST_MASK (1 << 5)
-#endif
+constexpr unsigned kPingpongGhostMask = 1u << 5;
 template <int K, int ROWS>
 constexpr bool pingpong_loop() {
-    return K < 32 && (((GOL_PINGPONG_MASK >> K) & 1) != 0 || (ROWS == 0 && ((GOL_PINGPONG_GHOST_MASK >> K) & 1) != 0));
+    return K < 32 && (((kPingpongMask >> K) & 1) != 0 || (ROWS == 0 && ((kPingpongGhostMask >> K) & 1) != 0));
 }
 
 template <int K, int ROWS, bool COH = false>
@@ -176,15 +169,15 @@ struct WaveRunner {
             // the row six ahead, so six loads stay in flight per wave and no register copy has to
             // wait for an outstanding load (copying a prefetched register forces the wait: the
             // queue shift of the fill phase collapses the prefetch distance to one triple).
-#define GOL_ROW6(J)                                          \
+#define ROW6_STEP(J)                                          \
     compute_store<(J) % 3, false>(pf[J].x, pf[J].y, i + (J)); \
     pf[J] = load_row_word<COH>(ld);                                             \
     next_row();                                              \
     __builtin_amdgcn_sched_barrier(0);
             for (; i + 6 <= n; i += 6) {
-                GOL_ROW6(0) GOL_ROW6(1) GOL_ROW6(2) GOL_ROW6(3) GOL_ROW6(4) GOL_ROW6(5)
+                ROW6_STEP(0) ROW6_STEP(1) ROW6_STEP(2) ROW6_STEP(3) ROW6_STEP(4) ROW6_STEP(5)
             }
-#undef GOL_ROW6
+#undef ROW6_STEP
             // fewer than six rows left, in pf[0..] in order
             if (i < n) compute_store<0, false>(pf[0].x, pf[0].y, i);
             if (i + 1 < n) compute_store<1, false>(pf[1].x, pf[1].y, i + 1);

@@ -28,13 +28,6 @@ using namespace gol;
         }                                                                       \
     } while (0)
 
-#ifdef GOL_TILE_STAMPS
-namespace gol {
-namespace hipk {
-void read_tile_stamps(unsigned long long* out, size_t n);
-}
-}  // namespace gol
-#endif
 
 int main(int argc, char** argv) {
     const i64 N = argc > 1 ? atoll(argv[1]) : 32768;
@@ -173,28 +166,6 @@ int main(int argc, char** argv) {
         fprintf(stderr, "step_pipe: a ring wait timed out\n");
         return 3;
     }
-#ifdef GOL_TILE_STAMPS
-    if (tile_nw > 0) {  // time breakdown of the last launch: cycles from the kernel start, median over workgroups
-        const int slots = 48;
-        std::vector<unsigned long long> ts((size_t)4096 * slots);
-        gol::hipk::read_tile_stamps(ts.data(), ts.size());
-        const int nt = (int)std::min<i64>(st.waves, 4096);
-        std::vector<std::vector<double>> seg(slots);
-        for (int b = 0; b < nt; ++b) {
-            const unsigned long long* t = &ts[(size_t)b * slots];
-            if (!t[0]) continue;
-            for (int s = 1; s < slots; ++s)
-                if (t[s] >= t[0] && t[s] - t[0] < (1ull << 40)) seg[s].push_back((double)(t[s] - t[0]));
-        }
-        printf("stamps (median cycles since start):");
-        for (int s = 1; s < slots; ++s) {
-            if (seg[s].empty()) continue;
-            std::sort(seg[s].begin(), seg[s].end());
-            printf(" %d:%.0f", s, seg[s][seg[s].size() / 2]);
-        }
-        printf("\n");
-    }
-#endif
     if (getenv("KB_CHECK") && atoi(getenv("KB_CHECK")) && tile_nw > 0) {
         // K generations from the same random board: this tile kernel vs K single-generation passes of
         // the temporal kernel (its own one-round plan); every word of the board must match
