@@ -307,6 +307,7 @@ def main() -> int:
                 "transport": transport.name(),
                 "rccl_nranks": transport.data_plane_ranks() if rccl is not None else None,
                 "self_exchange": bool(args.self_exchange),
+                "rccl_registered": bool(st.get("registered", False)),
                 "halo_exchanges_rank0": st["exchanges"],
                 "halo_bytes_all_ranks": halo_bytes,
                 "watchdog_s": args.watchdog,

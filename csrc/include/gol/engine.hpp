@@ -95,6 +95,7 @@ struct EngineStats {
     std::string kernel;        // stencil kernel in use (HIP: temporal | tile | lds; CPU: cpu)
     std::string schedule;      // superstep schedule: local (no neighbours) | split | full
     std::string tuning;        // init-time measurements behind the auto choices (HIP)
+    bool registered = false;   // HIP + RCCL: the boards are registered with the communicator (zero-copy halos)
 };
 
 class Engine {

@@ -77,6 +77,16 @@ class Transport {
     // Whether exchange() may be captured into a hipGraph (RCCL: its kernels become graph nodes; the
     // thread-rank emulation rendezvous across streams of several threads and cannot be captured).
     virtual bool graph_capturable() const { return false; }
+    // Device transports: register a device buffer the exchanges send from / receive into (RCCL:
+    // ncclCommRegister, user-buffer registration for zero-copy peer transfers).  Returns a handle for
+    // deregister_buffer, or nullptr when the transport does not register (or registration failed:
+    // the exchanges then use the unregistered path).
+    virtual void* register_buffer(void* buf, size_t bytes) {
+        (void)buf;
+        (void)bytes;
+        return nullptr;
+    }
+    virtual void deregister_buffer(void* handle) { (void)handle; }
 };
 
 // P = 1.

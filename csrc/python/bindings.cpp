@@ -107,6 +107,7 @@ py::dict stats_dict(const EngineStats& s) {
     d["kernel_depth"] = s.kernel_depth;
     d["tile_waves"] = s.tile_waves;
     d["tuning"] = s.tuning;
+    d["registered"] = s.registered;
     return d;
 }
 

@@ -68,6 +68,14 @@ class RcclTransport : public Transport {
     void gatherv(const void* send, size_t n, std::vector<std::vector<u8>>* out, int root) override {
         ctl_->gatherv(send, n, out, root);
     }
+    void* register_buffer(void* buf, size_t bytes) override {
+        void* h = nullptr;
+        if (!comm_ || ncclCommRegister(comm_, buf, bytes, &h) != ncclSuccess) return nullptr;
+        return h;
+    }
+    void deregister_buffer(void* handle) override {
+        if (comm_ && handle) (void)ncclCommDeregister(comm_, handle);
+    }
     int data_plane_ranks() override {
         int n = -1;
         if (comm_ && ncclCommCount(comm_, &n) != ncclSuccess) return -1;

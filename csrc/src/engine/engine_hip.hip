@@ -76,6 +76,14 @@ HipEngine::HipEngine(const Geometry& g, const EngineConfig& c, std::shared_ptr<T
     for (int i = 0; i < 2; ++i) HIP_CHECK(hipMalloc(&buf_[i], bytes));
     alloc_bytes_ = bytes;
     device_transport_ = t_->device_buffers() && cfg_.transport != "host";
+    // Register both boards (their ghost and edge rows are what the one-tile exchanges send and receive)
+    // with the device transport: RCCL's user-buffer registration (ncclCommRegister) lets peer
+    // transfers read and write them directly instead of staging through its FIFOs.  Sub-tile halves
+    // and 2-D staging buffers stay unregistered.  GOL_RCCL_REGISTER=0 keeps every buffer unregistered.
+    if (device_transport_ && env_int("GOL_RCCL_REGISTER", 1) != 0 && !halo_items(L_.R).empty()) {
+        for (int i = 0; i < 2; ++i) reg_[i] = t_->register_buffer(buf_[i], bytes);
+        stats_registered_ = reg_[0] != nullptr && reg_[1] != nullptr;
+    }
     if (cfg_.transport == "device" && !t_->device_buffers())
         throw Error("GOL_TRANSPORT=device needs a device transport (RCCL)");
     for (auto& kk : kern_) kk = kernel_ == "resident" ? "auto" : kernel_;
@@ -188,6 +196,8 @@ HipEngine::~HipEngine() {
         for (u64* p : *v) hipFree(p);
     for (auto& v : {&hstage_s_, &hstage_r_, &xhs_, &xhr_})
         for (u64* p : *v) hipHostFree(p);
+    for (void* h : reg_)
+        if (h) t_->deregister_buffer(h);
     for (int i = 0; i < 2; ++i) hipFree(buf_[i]);
     for (auto& kv : flow_plans_)
         for (void* q : {(void*)kv.second.lanes, (void*)kv.second.items, (void*)kv.second.deps, (void*)kv.second.flags})
@@ -342,6 +352,7 @@ void HipEngine::do_init(const PatternSpec& p) {
                         (long long)p0.rows, (long long)p0.waves);
     }
     stats_.tuning = tn;
+    stats_.registered = stats_registered_;
     // Build the plans of the supersteps the runs will use now (the full superstep and the
     // remainder of the hinted run length), so neither graph capture nor a hinted timed loop
     // builds or uploads a plan.  Other remainders are built on first use.

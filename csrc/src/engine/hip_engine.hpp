@@ -645,6 +645,8 @@ class HipEngine : public Engine {
     u32* res_status_ = nullptr;
     u64* res_scratch_[2] = {nullptr, nullptr};  // timing / probe boards (the kernel rewrites its source)
     std::vector<u64*> xhs_, xhr_;  // sub-tile host staging (exchange_rows), xh_bytes_ each
+    void* reg_[2] = {nullptr, nullptr};  // RCCL user-buffer registrations of buf_[0], buf_[1]
+    bool stats_registered_ = false;
     size_t xh_bytes_ = 0;
 };
 
