@@ -109,11 +109,15 @@ void launch_step_pipe(int nw, int L, const u64* src, u64* dst, const LaneDesc* p
 // step_flow (flow_kernel.hip): a superstep of several step_temporal passes as ONE launch of a
 // persistent grid whose waves draw the items of a flow plan (plan.hpp build_flow_plan) in ticket
 // order and wait for each item's dependencies through per-item completion flags.
-struct FlowCtl {  // device memory, zero-initialised once; the kernel leaves next = done = 0
+struct FlowCtl {  // device memory, zero-initialised once; the kernel leaves next = done = exch = 0
     u32 next;     // ticket counter
     u32 done;     // waves that drew their last ticket
     u32 epoch;    // launches completed (flags of the running launch hold epoch + 1)
     u32 fault;    // a dependency wait timed out: the board is invalid
+    u32 exch;     // exchange-overlapped launches: set to 1 by the comm stream once the halo exchange of
+                  // this superstep is complete (hipStreamWriteValue32); the items marked FLOW_ITEM_EXCH
+                  // wait for it, the last wave out resets it
+    u32 pad[3];
 };
 struct FlowArgs {
     u64* a;                  // even passes read a and write b, odd passes the reverse

@@ -103,9 +103,12 @@ i64 round_balanced_rows(const std::vector<Region>& regions, i64 nw, i64 h, int k
 // pass j overwrites what pass j - 1 read).  Writes of pass j - 2 to the same buffer are ordered
 // transitively (every cell pass j writes was read, as a centre, by the pass j - 1 item that waited for
 // its pass j - 2 writer).  Every dependency has a smaller ticket than its dependant.
+enum : u32 {
+    FLOW_ITEM_EXCH = 1u << 31,  // FlowItem::pass bit: reads ghost cells the superstep's exchange writes
+};
 struct FlowItem {
     u32 depth;    // generations of the item's pass
-    u32 pass;     // pass index (even: reads buffer a, odd: buffer b)
+    u32 pass;     // pass index (even: reads buffer a, odd: buffer b), | FLOW_ITEM_EXCH
     u32 dep_off;  // dependencies: deps[dep_off .. dep_off + ndeps)
     u32 ndeps;
 };
@@ -126,7 +129,12 @@ struct FlowPlan {
 // neighbour (halo lanes stream the wrapped words); wrap_y: its own N/S neighbour (rows modulo h; each
 // pass then starts one band of the previous pass further down, so its first items depend on the
 // previous pass's first ones).  Returns an empty string or a description of an inconsistency.
-std::string build_flow_plan(const std::vector<FlowPass>& passes, i64 nw, i64 h, bool xwrap, bool wrap_y, FlowPlan& out);
+// mark_exch: the first pass's items that read a cell outside the tile (ghost rows / words the halo
+// exchange writes) get FLOW_ITEM_EXCH, and every pass orders its items from the middle of the tile
+// outwards, so the interior runs while the exchange is in flight and the bands next to the halos come
+// last (without it and without wrap_y, bands run top to bottom).
+std::string build_flow_plan(const std::vector<FlowPass>& passes, i64 nw, i64 h, bool xwrap, bool wrap_y, FlowPlan& out,
+                            bool mark_exch = false);
 
 // Neighbour tiles of a resident plan (hip_kernels.hpp step_resident: one plan wave = one tile, kept
 // by one workgroup for a whole run).  Tile t reads, for each of its lanes, rows [row0-k, row0+nrows+k)

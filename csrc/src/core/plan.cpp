@@ -247,7 +247,8 @@ std::string validate_plan(const std::vector<LaneDesc>& lanes, i64 nw, i64 h, int
     return "";
 }
 
-std::string build_flow_plan(const std::vector<FlowPass>& passes, i64 nw, i64 h, bool xwrap, bool wrap_y, FlowPlan& out) {
+std::string build_flow_plan(const std::vector<FlowPass>& passes, i64 nw, i64 h, bool xwrap, bool wrap_y, FlowPlan& out,
+                            bool mark_exch) {
     out = FlowPlan();
     if (passes.empty()) return "no passes";
     // per word column (col + 1 in [0, nw + 2)): the previous pass's written and read row intervals
@@ -297,13 +298,21 @@ std::string build_flow_plan(const std::vector<FlowPass>& passes, i64 nw, i64 h, 
         out.st.out_words += st.out_words;
         // ticket order inside the pass: row bands down the board (with the torus wrap starting at
         // `offset`, one band of the previous pass below its start); a wave holding several narrow
-        // segments sorts by its lowest band
+        // segments sorts by its lowest band.  mark_exch: bands from the middle of the tile outwards
+        // (the key is minus the distance to the nearer edge of the pass's rows)
         std::vector<std::pair<i64, size_t>> order;
+        i64 rlo = std::numeric_limits<i64>::max(), rhi = std::numeric_limits<i64>::min();
+        for (const Region& r : ps.regions)
+            if (r.r1 > r.r0 && r.c1 > r.c0) rlo = std::min(rlo, r.r0), rhi = std::max(rhi, r.r1);
         for (size_t w = 0; w < L.size() / kWaveLanes; ++w) {
             const LaneDesc* d = &L[w * kWaveLanes];
             if (d[0].nrows <= 0) continue;  // padding wave: no item
             i64 key = std::numeric_limits<i64>::min();
-            for (int l = 0; l < kWaveLanes; ++l) key = std::max<i64>(key, wrap_y ? pmod((i64)d[l].row0 - offset, h) : d[l].row0);
+            for (int l = 0; l < kWaveLanes; ++l) {
+                const i64 r0 = d[l].row0, r1 = r0 + d[l].nrows;
+                const i64 kk = mark_exch && !wrap_y ? -std::min(r0 - rlo, rhi - r1) : (wrap_y ? pmod(r0 - offset, h) : r0);
+                key = std::max<i64>(key, kk);
+            }
             order.push_back({key, w});
         }
         std::stable_sort(order.begin(), order.end(),
@@ -316,6 +325,16 @@ std::string build_flow_plan(const std::vector<FlowPass>& passes, i64 nw, i64 h, 
             const u32 id = (u32)out.items.size();
             const LaneDesc* d = &L[ow.second * kWaveLanes];
             FlowItem fi{(u32)ps.k, (u32)j, (u32)out.deps.size(), 0u};
+            if (mark_exch && j == 0) {
+                bool ghost = false;
+                for (int l = 0; l < kWaveLanes; ++l) {
+                    const LaneDesc& x = d[l];
+                    if (x.nrows <= 0) continue;
+                    ghost = ghost || x.col < 0 || x.col >= nw ||
+                            (!wrap_y && ((i64)x.row0 - ps.k < 0 || (i64)x.row0 + x.nrows + ps.k > h));
+                }
+                if (ghost) fi.pass |= FLOW_ITEM_EXCH;
+            }
             hit.clear();
             for (int l = 0; l < kWaveLanes; ++l) {
                 const LaneDesc& x = d[l];

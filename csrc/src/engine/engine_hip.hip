@@ -322,7 +322,8 @@ void HipEngine::do_init(const PatternSpec& p) {
         // schedule (and the forced-split measurement mode).  The full schedule
         // exchanges on the compute stream itself: recording the event there every superstep
         // only idles the GPU (~15 us per record, a release fence).
-        events_needed_ = cfg_.force_split || (split_ && !halo_items(L_.R).empty());
+        events_needed_ = cfg_.force_split || (split_ && !halo_items(L_.R).empty()) ||
+                         (flow_ && flow_ov_ && !halo_items(L_.R).empty());
     }
     stats_.kernel = split_ ? kern_[1] + "+boundary:" + kern_[2] : (dual_ ? std::string("temporal") : kern_[0]);
     if (!split_ && !dual_ && kern_[0] == "pipe")
@@ -334,7 +335,7 @@ void HipEngine::do_init(const PatternSpec& p) {
     stats_.schedule = split_ ? "split" : (halo_items(L_.R).empty() ? "local" : "full");
     if (dual_) stats_.schedule += sub_overlap_ == 2 ? "+subtiles2ov2" : (sub_overlap_ ? "+subtiles2ov" : "+subtiles2");
     if (flow_) {
-        stats_.schedule += flow_graph_ ? "+flow+graph" : "+flow";
+        stats_.schedule += flow_graph_ ? "+flow+graph" : (flow_ov_ ? "+flow+ov" : "+flow");
         stats_.kernel = strprintf("flow(temporal K<=%d)", hipk::flow_max_depth());
     }
     stats_.kernel_depth = dual_ ? tdepth_ : (flow_ ? hipk::flow_max_depth() : kdepth_);

@@ -36,7 +36,9 @@ std::vector<int> HipEngine::flow_cut(int k) const {
 }
 
 const HipEngine::FlowDev& HipEngine::flow_plan(int k) {
-    auto it = flow_plans_.find(k);
+    const bool ov = flow_ov_active(k);
+    const int key = k * 2 + (ov ? 1 : 0);
+    auto it = flow_plans_.find(key);
     if (it != flow_plans_.end()) return it->second;
     if (!flow_ctl_) {
         HIP_CHECK(hipMalloc(&flow_ctl_, sizeof(hipk::FlowCtl)));
@@ -58,7 +60,7 @@ const HipEngine::FlowDev& HipEngine::flow_plan(int k) {
         fps.push_back({ps[j], rg, rows});
     }
     FlowPlan fp;
-    const std::string err = build_flow_plan(fps, L_.nw, L_.h, xwrap_by_plan(), wrapy, fp);
+    const std::string err = build_flow_plan(fps, L_.nw, L_.h, xwrap_by_plan(), wrapy, fp, ov);
     if (!err.empty()) throw Error("flow plan: " + err);
     for (size_t j = 0; j < ps.size(); ++j) {
         const std::vector<LaneDesc> part(fp.lanes.begin() + (size_t)fp.pass_begin[j] * kWaveLanes,
@@ -82,7 +84,7 @@ const HipEngine::FlowDev& HipEngine::flow_plan(int k) {
     // flags start below every epoch a launch will wait for
     HIP_CHECK(hipMemsetAsync(fd.flags, 0, std::max<size_t>(1, fp.items.size()) * sizeof(u32), s_comp_));
     HIP_CHECK(hipStreamSynchronize(s_comp_));
-    return flow_plans_.emplace(k, fd).first->second;
+    return flow_plans_.emplace(key, fd).first->second;
 }
 
 void HipEngine::flow_launch(int k, const u64* src, u64* dst, hipStream_t s) {
@@ -103,11 +105,30 @@ void HipEngine::flow_launch(int k, const u64* src, u64* dst, hipStream_t s) {
     flow_used_ = true;
 }
 
-// One flow superstep: (with neighbours) the exchange of the k-deep halo on the compute stream, then
-// the single launch; the result lands in buf[cur ^ (passes & 1)].
+// One flow superstep: (with neighbours) the exchange of the k-deep halo, then the single launch; the
+// result lands in buf[cur ^ (passes & 1)].
+//   "flow":    the exchange on the compute stream, then the launch (its first pass reads the ghost rows).
+//   "flow+ov": the exchange on the comm stream (after the previous superstep's launch, ev_ready_),
+//              followed by a device flag (hipStreamWriteValue32); the launch goes to the compute stream
+//              at once, with no cross-queue event wait.  Its plan (build_flow_plan mark_exch) runs the
+//              items from the middle of the tile outwards and makes the first pass's items that read
+//              ghost cells wait for the flag, so the interior hides the exchange and only the bands next
+//              to the halos wait for it.  Pass 1 overwrites the edge rows the exchange sends; its items
+//              there depend on those flag-waiting items, so they start only after the exchange is done.
 void HipEngine::flow_superstep(int k) {
     const std::vector<int>& ps = pass_depths(k);
     const std::vector<HaloItem>& items = items_for(k);
+    if (flow_ov_active(k)) {
+        flow_plan(k);  // (allocates the control block the flag lives in)
+        prepare(k);
+        HIP_CHECK(hipStreamWaitEvent(s_comm_, ev_ready_, 0));
+        exchange_device(k, items, cur_, s_comm_);
+        HIP_CHECK(hipStreamWriteValue32(s_comm_, &flow_ctl_->exch, 1u, 0));
+        flow_launch(k, buf_[cur_], buf_[cur_ ^ 1], s_comp_);
+        if (ps.size() & 1) cur_ ^= 1;
+        HIP_CHECK(hipEventRecord(ev_ready_, s_comp_));  // the next exchange reads this launch's edge rows
+        return;
+    }
     if (!items.empty()) {
         prepare(k);
         if (device_transport_)

@@ -158,14 +158,17 @@ void HipEngine::choose_schedule() {
         if (t_->size() > 1) ok = t_->allreduce_min(ok);
         if (ok > 0) {
             cands.push_back("flow");
+            if (nbrs && device_transport_) cands.push_back("flow+ov");
             if (cfg_.graph && (!nbrs || (device_transport_ && t_->graph_capturable() && cfg_.graph_rccl != 0)))
                 cands.push_back("flow+graph");
         }
-        if (cfg_.sched == "flow") {  // GOL_SCHEDULE=flow: the only candidate
+        if (cfg_.sched == "flow" || cfg_.sched == "flow+ov") {  // GOL_SCHEDULE=flow[+ov]: the only candidate
             if (ok <= 0) throw Error("GOL_SCHEDULE=flow: no device memory for the flow timing scratch");
-            cands = {"flow"};
+            if (cfg_.sched == "flow+ov" && !(nbrs && device_transport_))
+                throw Error("GOL_SCHEDULE=flow+ov needs neighbours and a device transport (RCCL)");
+            cands = {cfg_.sched};
         }
-    } else if (cfg_.sched == "flow") {
+    } else if (cfg_.sched == "flow" || cfg_.sched == "flow+ov") {
         throw Error("GOL_SCHEDULE=flow: this tile cannot run flow supersteps (GOL_KERNEL / GOL_COMPAT / width)");
     }
     std::string pick = cands[0];
@@ -219,6 +222,7 @@ void HipEngine::choose_schedule() {
     sched_pick_ = pick;
     flow_ = pick.rfind("flow", 0) == 0;
     flow_graph_ = pick == "flow+graph";
+    flow_ov_ = pick == "flow+ov";
     split_ = pick == "split";
     dual_ = pick.rfind("subtiles", 0) == 0;
     sub_overlap_ = pick == "subtiles+ov" ? 1 : (pick == "subtiles+ov2" ? 2 : 0);
@@ -296,16 +300,27 @@ void HipEngine::time_schedule(const std::string& c, int k, int reps, bool eager)
             time_schedule(base, k, reps, true);  // the same exchanges as the peers' replays
         return;
     }
-    if (c == "flow") {
+    if (c == "flow" || c == "flow+ov") {
         // flow supersteps on scratch (a flow launch writes both of its buffers): the launches run between
         // flow_scratch_ and buf[cur ^ 1]; the exchange writes the board's ghost rows, as the other
         // candidates' do (the next real superstep rewrites them).  The kernel's run time does not depend
         // on the cell values, so the scratch's are never refreshed.
         if (!flow_timing_buffers()) throw Error("flow schedule timing: no scratch buffer");
-        const bool f = flow_;
+        const bool f = flow_, fo = flow_ov_;
         flow_ = true;
+        flow_ov_ = c == "flow+ov";
         const std::vector<HaloItem>& items = items_for(k);
         for (int i = 0; i < reps; ++i) {
+            if (flow_ov_active(k)) {  // as flow_superstep's overlapped path, on scratch
+                flow_plan(k);  // (allocates the control block the flag lives in)
+                prepare(k);
+                HIP_CHECK(hipStreamWaitEvent(s_comm_, ev_ready_, 0));
+                exchange_device(k, items, cur_, s_comm_);
+                HIP_CHECK(hipStreamWriteValue32(s_comm_, &flow_ctl_->exch, 1u, 0));
+                flow_launch(k, flow_scratch_, buf_[cur_ ^ 1], s_comp_);
+                HIP_CHECK(hipEventRecord(ev_ready_, s_comp_));
+                continue;
+            }
             if (!items.empty()) {
                 prepare(k);
                 if (device_transport_)
@@ -316,6 +331,7 @@ void HipEngine::time_schedule(const std::string& c, int k, int reps, bool eager)
             flow_launch(k, flow_scratch_, buf_[cur_ ^ 1], s_comp_);
         }
         flow_ = f;
+        flow_ov_ = fo;
         return;
     }
     split_ = c == "split";

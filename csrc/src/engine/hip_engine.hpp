@@ -596,6 +596,10 @@ class HipEngine : public Engine {
     }
     std::string sched_pick_;     // the schedule candidate choose_schedule picked (phase_probe times it)
     bool flow_graph_ = false;    // flow supersteps replay captured graphs ("flow+graph")
+    // flow supersteps with neighbours ("flow+ov"): the exchange runs on the comm stream while the
+    // launch's interior items run; the items reading ghost cells wait for its device flag
+    bool flow_ov_ = false;
+    bool flow_ov_active(int k) { return flow_ov_ && device_transport_ && !items_for(k).empty(); }
     u64* flow_scratch_ = nullptr;  // timing scratch of flow candidates (a flow launch writes both buffers)
     // Flow candidates are timed on scratch: the board copied to flow_scratch_, the launch between it and
     // buf[cur ^ 1].  False when there is no memory for one more board.
@@ -638,7 +642,7 @@ class HipEngine : public Engine {
     bool flow_used_ = false;                // a flow launch ran (fault check at readouts)
     hipk::FlowCtl* flow_ctl_ = nullptr;     // its ticket / epoch / fault words
     i64 flow_blocks_ = 0;                   // its persistent grid (workgroups)
-    std::map<int, FlowDev> flow_plans_;     // by superstep depth
+    std::map<int, FlowDev> flow_plans_;     // by superstep depth x 2 + exchange-overlapped
     bool res_ = false;  // supersteps run the resident kernel
     int res_kin_ = 0;   // its generations per in-kernel halo exchange
     std::map<int, ResPlan> res_plans_;

@@ -82,6 +82,29 @@ __device__ __forceinline__ void flow_wait(const FlowArgs& a, u32 dep_off, u32 nd
     asm volatile("" ::: "memory");  // the item's loads stay after the wait
 }
 
+// Exchange-overlapped launches: an item that reads ghost cells waits for the comm stream's flag
+// (hipStreamWriteValue32 after the RCCL group), then acquires at agent scope before its loads.  The
+// flag is a single word polled with system-scope loads (the write comes from another queue's packet
+// processor, not from a wave).
+__device__ __forceinline__ void flow_wait_exch(const FlowArgs& a) {
+    u64 t0 = 0;
+    for (int spin = 0;; ++spin) {
+        const u32 v = __builtin_amdgcn_readfirstlane(
+            __hip_atomic_load(&a.ctl->exch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
+        if (v != 0) break;
+        if (spin == 0) t0 = __builtin_amdgcn_s_memrealtime();
+        const u32 fault = __builtin_amdgcn_readfirstlane(
+            __hip_atomic_load(&a.ctl->fault, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+        if (__builtin_amdgcn_s_memrealtime() - t0 > kFlowWaitTicks || fault != 0) {
+            __hip_atomic_store(&a.ctl->fault, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // (all lanes, one word)
+            break;
+        }
+        __builtin_amdgcn_s_sleep(8);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
 template <int K, int ROWS>
 __device__ __forceinline__ void flow_item(const u64* src, u64* dst, const LaneDesc& d, int nrows, const StepParams& p,
                                           i64 wave) {
@@ -118,6 +141,7 @@ __global__ __launch_bounds__(64 * kWavesPerBlock) __attribute__((amdgpu_waves_pe
         const u32 dep_off = __builtin_amdgcn_readfirstlane(ip->dep_off);
         const u32 ndeps = __builtin_amdgcn_readfirstlane(ip->ndeps);
         flow_wait(a, dep_off, ndeps, target, lane);
+        if (pass & FLOW_ITEM_EXCH) flow_wait_exch(a);
         const LaneDesc d = a.lanes[(i64)t * kWaveLanes + lane];
         const int nrows = __builtin_amdgcn_readfirstlane(d.nrows);
         const bool odd = pass & 1u;
@@ -147,6 +171,7 @@ __global__ __launch_bounds__(64 * kWavesPerBlock) __attribute__((amdgpu_waves_pe
         if (left == n_waves - 1) {
             __hip_atomic_store(&a.ctl->next, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             __hip_atomic_store(&a.ctl->done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(&a.ctl->exch, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             __hip_atomic_store(&a.ctl->epoch, target, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
     }
@@ -192,13 +217,14 @@ void launch_step_flow(const FlowArgs& a, i64 n_blocks, const StepParams& p, hipS
 }
 
 bool flow_fault(FlowCtl* ctl, hipStream_t s) {
-    u32 v[4] = {0, 0, 0, 0};
-    if (hipMemcpyAsync(v, ctl, sizeof(v), hipMemcpyDeviceToHost, s) != hipSuccess || hipStreamSynchronize(s) != hipSuccess)
+    FlowCtl v{};
+    if (hipMemcpyAsync(&v, ctl, sizeof(v), hipMemcpyDeviceToHost, s) != hipSuccess || hipStreamSynchronize(s) != hipSuccess)
         throw Error("flow_fault: cannot read the control block");
-    if (v[3] == 0) return false;
-    // clear it, and the ticket state of the faulted launch (its waves all left)
-    const u32 z[4] = {0, 0, v[2], 0};
-    if (hipMemcpyAsync(ctl, z, sizeof(z), hipMemcpyHostToDevice, s) != hipSuccess || hipStreamSynchronize(s) != hipSuccess)
+    if (v.fault == 0) return false;
+    // clear it, and the ticket / exchange state of the faulted launch (its waves all left)
+    FlowCtl z{};
+    z.epoch = v.epoch;
+    if (hipMemcpyAsync(ctl, &z, sizeof(z), hipMemcpyHostToDevice, s) != hipSuccess || hipStreamSynchronize(s) != hipSuccess)
         throw Error("flow_fault: cannot reset the control block");
     return true;
 }

@@ -183,8 +183,8 @@ EngineConfig engine_config(const Options& o, const std::string& backend, int dev
     c.graph_rccl = tri("GOL_GRAPH_RCCL");
     c.plan_xcds = (int)env_int("GOL_PLAN_XCDS", 8);
     c.sched = env_str("GOL_SCHEDULE", "auto");
-    if (c.sched != "auto" && c.sched != "split" && c.sched != "full" && c.sched != "flow")
-        throw Error("GOL_SCHEDULE must be auto, split, full or flow (got " + c.sched + ")");
+    if (c.sched != "auto" && c.sched != "split" && c.sched != "full" && c.sched != "flow" && c.sched != "flow+ov")
+        throw Error("GOL_SCHEDULE must be auto, split, full, flow or flow+ov (got " + c.sched + ")");
     return c;
 }
 

@@ -588,7 +588,8 @@ static void test_flow_plan() {
             ps.push_back({k, {{-e, cs.h + e, 0, cs.nw}}, cs.rows});
         }
         FlowPlan fp;
-        const std::string err = build_flow_plan(ps, cs.nw, cs.h, cs.xwrap, cs.wrap_y, fp);
+        const bool mark = cs.ext != 0;  // ranks with neighbours: the exchange-overlapped variant's plan
+        const std::string err = build_flow_plan(ps, cs.nw, cs.h, cs.xwrap, cs.wrap_y, fp, mark);
         CHECK(err.empty());
         if (!err.empty()) {
             fprintf(stderr, "  build_flow_plan: %s\n", err.c_str());
@@ -601,7 +602,7 @@ static void test_flow_plan() {
         for (size_t j = 0; j < cs.cut.size(); ++j) {
             std::vector<int> cov((size_t)(rows_all * cols_all), 0);
             for (u32 t = fp.pass_begin[j]; t < fp.pass_begin[j + 1]; ++t) {
-                CHECK(fp.items[t].pass == j && fp.items[t].depth == (u32)cs.cut[j]);
+                CHECK((fp.items[t].pass & ~FLOW_ITEM_EXCH) == j && fp.items[t].depth == (u32)cs.cut[j]);
                 for (int l = 0; l < 64; ++l) {
                     const LaneDesc& d = fp.lanes[(size_t)t * 64 + l];
                     if (!(d.flags & LANE_STORE)) continue;
@@ -622,7 +623,7 @@ static void test_flow_plan() {
         for (u32 t = 0; t < n; ++t)
             for (u32 q = 0; q < fp.items[t].ndeps; ++q) {
                 const u32 d = fp.deps[fp.items[t].dep_off + q];
-                order_ok = order_ok && d < t && fp.items[d].pass + 1 == fp.items[t].pass;
+                order_ok = order_ok && d < t && (fp.items[d].pass & ~FLOW_ITEM_EXCH) + 1 == (fp.items[t].pass & ~FLOW_ITEM_EXCH);
             }
         CHECK(order_ok);
         // ancestors (transitive closure; deps point backwards, so one forward sweep)
@@ -672,6 +673,21 @@ static void test_flow_plan() {
                 if (meet(wr[t], wr[m]) || meet(wr[t], rd[m]) || meet(rd[t], wr[m])) ++races;
             }
         CHECK(races == 0);
+        // exchange marks: exactly the first pass's items that read a cell outside the tile
+        bool marks_ok = true;
+        for (u32 t = 0; t < n; ++t) {
+            const FlowItem& f = fp.items[t];
+            bool ghost = false;
+            for (int l = 0; l < 64; ++l) {
+                const LaneDesc& d = fp.lanes[(size_t)t * 64 + l];
+                if (d.nrows <= 0) continue;
+                ghost = ghost || d.col < 0 || d.col >= cs.nw ||
+                        (!cs.wrap_y && (d.row0 - (i64)f.depth < 0 || d.row0 + d.nrows + (i64)f.depth > cs.h));
+            }
+            const bool want = mark && (f.pass & ~FLOW_ITEM_EXCH) == 0 && ghost;
+            marks_ok = marks_ok && ((f.pass & FLOW_ITEM_EXCH) != 0) == want;
+        }
+        CHECK(marks_ok);
         if (races) fprintf(stderr, "  flow plan nw %lld h %lld: %d racing item pairs\n", (long long)cs.nw, (long long)cs.h, races);
         // the first item of every later pass waits only for items in the first half of the pass before
         // (plans without packed narrow segments: a wave packing segments of several bands depends on

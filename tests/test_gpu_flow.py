@@ -66,22 +66,25 @@ def test_flow_headline_vs_torch(gol, monkeypatch):
         assert np.array_equal(got, want), f"after +{g}: {int((got != want).sum())} cells differ"
 
 
+@pytest.mark.parametrize("sched", ["flow", "flow+ov"])
 @pytest.mark.parametrize("P,R", [(2, 32), (3, 32), (2, 128)])
-def test_flow_thread_ranks_ghost_rows(gol, monkeypatch, P, R):
+def test_flow_thread_ranks_ghost_rows(gol, monkeypatch, P, R, sched):
     """Ranks with neighbours: the exchange fills the ghost rows, then one flow launch runs the superstep
-    (its earlier passes also computing the ghost rows the later ones read)."""
+    (its earlier passes also computing the ghost rows the later ones read).  flow+ov: the exchange runs
+    on the comm stream while the launch's interior items run; the band items wait for its device flag
+    (RCCL-semantics transport: device buffers, stream-ordered)."""
     N = 384 if R == 32 else 768
     gens = R * 3 + 11
-    monkeypatch.setenv("GOL_SCHEDULE", "flow")
+    monkeypatch.setenv("GOL_SCHEDULE", sched)
     ts = gol.parallel.p2p_thread_transports(P)
     out, errs = [None] * P, []
 
     def rank_main(r):
         try:
             s = gol.Simulation(N, ts[r], backend="hip", device=0, global_mode=True, halo_depth=R, overlap=False,
-                               subtiles=0, schedule="flow")
+                               subtiles=0, schedule=sched)
             s.init(5, seed=21)
-            assert "+flow" in s.stats()["schedule"], s.stats()
+            assert s.stats()["schedule"].endswith("+" + sched), s.stats()
             s.step(gens)
             out[r] = (s.geometry.row0, s.board())
         except Exception as e:  # pragma: no cover - reported below

@@ -105,14 +105,15 @@ def test_rccl_self_auto_depth_rectangular(gol, rccl, H, W, decomp):
     assert np.array_equal(got, numpy_step(random_board(H, W, 6), gens))
 
 
+@pytest.mark.parametrize("sched", ["flow", "flow+ov"])
 @pytest.mark.parametrize("R", [8, 32])
-def test_rccl_self_flow(gol, rccl, monkeypatch, R):
+def test_rccl_self_flow(gol, rccl, monkeypatch, R, sched):
     """Flow supersteps (one step_flow launch each) whose halos go through RCCL first: the launch's first
     pass reads the ghost rows the exchange wrote, the later passes the extended rows."""
-    monkeypatch.setenv("GOL_SCHEDULE", "flow")
+    monkeypatch.setenv("GOL_SCHEDULE", sched)
     N, gens = 1024, 3 * R + 5
-    got, st = _run(gol, rccl, N, gens, R, halo_depth=R, schedule="flow", subtiles=0)
-    assert "+flow" in st["schedule"] and st["exchanges"] >= 3, st
+    got, st = _run(gol, rccl, N, gens, R, halo_depth=R, schedule=sched, subtiles=0)
+    assert st["schedule"].endswith("+" + sched) and st["exchanges"] >= 3, st
     assert np.array_equal(got, numpy_step(initial_board(5, N, 1, True, R), gens))
 
 
