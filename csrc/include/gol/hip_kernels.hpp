@@ -134,6 +134,16 @@ int flow_max_depth();
 // Resident 256-thread workgroups per CU of the flow kernel (its persistent grid is this x CUs).
 int flow_blocks_per_cu(u32 flags);
 void launch_step_flow(const FlowArgs& a, i64 n_blocks, const StepParams& p, hipStream_t s);
+// The same with LDS tile items (step_tile / step_tile_fold's device code, one workgroup of `nw_per_wg`
+// waves per item; `rows` the largest chunk height and `kmax` the deepest pass of the plan, which size
+// the dynamic LDS).  p.flags carries the tile variant (STEP_TILE_FOLD, _INPLACE, _L2/_L4); supported:
+// nw_per_wg 8, double-buffered with 4 generations per LDS pass or in place with 2.
+bool flow_tile_supported(int nw_per_wg, u32 flags);
+// Most rows a flow tile item may hold at depth k (the tile kernel's capacity less the ticket slot).
+i64 flow_tile_max_rows(int k, int nw_per_wg, u32 flags);
+int flow_tile_blocks_per_cu(int nw_per_wg, i64 rows, int kmax, u32 flags);
+void launch_step_flow_tile(int nw_per_wg, const FlowArgs& a, i64 n_blocks, i64 rows, int kmax, const StepParams& p,
+                           hipStream_t s);
 // True (and cleared) when a wait of a flow launch timed out since the last call (synchronises s).
 bool flow_fault(FlowCtl* ctl, hipStream_t s);
 // Single-generation LDS-tiled kernel over output rows [r0, r1) (all words).

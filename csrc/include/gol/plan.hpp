@@ -116,6 +116,7 @@ struct FlowPass {
     int k;                        // generations
     std::vector<Region> regions;  // output regions (tile coordinates, ghost rows/words allowed)
     i64 rows;                     // segment height of its plan
+    bool fold = false;            // LDS tile items with folded 32-lane tiles (build_plan fold)
 };
 struct FlowPlan {
     std::vector<LaneDesc> lanes;  // items x 64, in ticket order

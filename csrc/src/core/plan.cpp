@@ -291,7 +291,7 @@ std::string build_flow_plan(const std::vector<FlowPass>& passes, i64 nw, i64 h, 
         const FlowPass& ps = passes[j];
         if (ps.k < 1) return strprintf("pass %zu: depth %d", j, ps.k);
         PlanStats st;
-        const std::vector<LaneDesc> L = build_plan(ps.regions, nw, h, ps.rows, ps.k, xwrap, &st, 1, 1);
+        const std::vector<LaneDesc> L = build_plan(ps.regions, nw, h, ps.rows, ps.k, xwrap, &st, 1, 1, ps.fold);
         out.st.waves += st.waves;
         out.st.active_lanes += st.active_lanes;
         out.st.lane_rows += st.lane_rows;

@@ -15,12 +15,16 @@
 namespace gol {
 namespace hipeng {
 
-bool HipEngine::flow_eligible() const {
+bool HipEngine::flow_eligible() {
     // one tile; every pass is a step_temporal pass (no LDS-tile / pipe / LDS kernels, no split bands);
     // ghost words of a non-aligned self-wrapping width are refreshed by a kernel after every pass,
     // which a single launch cannot do
     if (cfg_.compat || cfg_.profile || cfg_.force_split || kernel_ == "lds" || res_) return false;
-    if (cfg_.kernel == "tile" || cfg_.kernel == "pipe" || cfg_.kernel == "resident") return false;
+    if (cfg_.kernel == "pipe" || cfg_.kernel == "resident") return false;
+    if (flow_tiles()) {  // the tile variant the full-tile plans use must have a flow twin
+        const u32 f = step_flags() | plan(0, kdepth_, 0).tflags;
+        if (!hipk::flow_tile_supported(cfg_.tile_waves, f)) return false;
+    }
     if (self_x() && !L_.aligned()) return false;
     return env_int("GOL_FLOW", 1) != 0;
 }
@@ -28,7 +32,9 @@ bool HipEngine::flow_eligible() const {
 // Passes of a flow superstep: as few as the flow kernel's deepest depth allows, as equal as
 // possible (20 = 7 + 7 + 6).  GOL_FLOW_KMAX lowers the deepest depth (measurement knob).
 std::vector<int> HipEngine::flow_cut(int k) const {
-    const int kmax = std::max(1, std::min<int>(hipk::flow_max_depth(), (int)env_int("GOL_FLOW_KMAX", hipk::flow_max_depth())));
+    // tile items: passes of the tuned tile depth (any depth runs); waves: the flow kernel's deepest
+    const int deepest = flow_tiles() ? std::max(1, kdepth_) : hipk::flow_max_depth();
+    const int kmax = std::max(1, std::min<int>(deepest, (int)env_int("GOL_FLOW_KMAX", deepest)));
     const int n = (k + kmax - 1) / kmax;
     std::vector<int> ps;
     for (int j = 0; j < n; ++j) ps.push_back(k / n + (j < k % n ? 1 : 0));
@@ -46,18 +52,36 @@ const HipEngine::FlowDev& HipEngine::flow_plan(int k) {
     }
     const std::vector<int> ps = flow_cut(k);
     const bool wrapy = (step_flags() & hipk::STEP_WRAP_Y) != 0;
-    if (flow_blocks_ <= 0) flow_blocks_ = (i64)hipk::flow_blocks_per_cu(step_flags()) * cus_;
-    const i64 resident = flow_blocks_ * kWavesPerBlock;
-    // items per pass: one round of the persistent grid (GOL_FLOW_ROUNDS in percent scales it; big
-    // tiles take several rounds of ~45K-row segments, as the pass kernels' plans)
-    const double scale = (double)env_int("GOL_FLOW_ROUNDS", 100) / 100.0;
+    FlowDev fd;
     std::vector<FlowPass> fps;
-    for (size_t j = 0; j < ps.size(); ++j) {
-        const std::vector<Region> rg = regions(0, ps[j], ext_after(ps, j));
-        const i64 target = std::max<i64>(1, (i64)(scale * (double)resident));
-        const i64 rows = round_balanced_rows(rg, L_.nw, L_.h, ps[j], target, 2 * (i64)ps[j], xwrap_by_plan(),
-                                             round_rows(ps[j]));
-        fps.push_back({ps[j], rg, rows});
+    if (flow_tiles()) {
+        // LDS tile items: every pass uses the tile variant and chunk height of the deepest pass's plan
+        // (a shallower pass needs less LDS), capped at the flow variant's capacity (its ticket slot)
+        const int kmax = *std::max_element(ps.begin(), ps.end());
+        const DevPlan& p0 = plan(0, kmax, ext_after(ps, 0));
+        fd.tile = true;
+        fd.kmax = kmax;
+        fd.tflags = p0.tflags;
+        const u32 f = step_flags() | p0.tflags;
+        fd.rows = std::min<i64>(p0.rows, hipk::flow_tile_max_rows(kmax, cfg_.tile_waves, f));
+        if (p0.fold && fd.rows < hipk::kFoldMinRows) throw Error("flow plan: folded tiles do not fit with the ticket slot");
+        fd.blocks = (i64)hipk::flow_tile_blocks_per_cu(cfg_.tile_waves, fd.rows, kmax, f) * cus_;
+        for (size_t j = 0; j < ps.size(); ++j)
+            fps.push_back({ps[j], regions(0, ps[j], ext_after(ps, j)), fd.rows, p0.fold});
+    } else {
+        if (flow_blocks_ <= 0) flow_blocks_ = (i64)hipk::flow_blocks_per_cu(step_flags()) * cus_;
+        fd.blocks = flow_blocks_;
+        const i64 resident = flow_blocks_ * kWavesPerBlock;
+        // items per pass: one round of the persistent grid (GOL_FLOW_ROUNDS in percent scales it; big
+        // tiles take several rounds of ~45K-row segments, as the pass kernels' plans)
+        const double scale = (double)env_int("GOL_FLOW_ROUNDS", 100) / 100.0;
+        for (size_t j = 0; j < ps.size(); ++j) {
+            const std::vector<Region> rg = regions(0, ps[j], ext_after(ps, j));
+            const i64 target = std::max<i64>(1, (i64)(scale * (double)resident));
+            const i64 rows = round_balanced_rows(rg, L_.nw, L_.h, ps[j], target, 2 * (i64)ps[j], xwrap_by_plan(),
+                                                 round_rows(ps[j]));
+            fps.push_back({ps[j], rg, rows});
+        }
     }
     FlowPlan fp;
     const std::string err = build_flow_plan(fps, L_.nw, L_.h, xwrap_by_plan(), wrapy, fp, ov);
@@ -69,7 +93,6 @@ const HipEngine::FlowDev& HipEngine::flow_plan(int k) {
         if (!bad.empty())
             throw Error(strprintf("refusing to launch an unsafe flow plan (k %d, pass %zu): %s", k, j, bad.c_str()));
     }
-    FlowDev fd;
     fd.cut = ps;
     fd.n_items = (u32)fp.items.size();
     fd.st = fp.st;
@@ -99,8 +122,11 @@ void HipEngine::flow_launch(int k, const u64* src, u64* dst, hipStream_t s) {
     a.flags = fd.flags;
     a.ctl = flow_ctl_;
     a.n_items = fd.n_items;
-    hipk::StepParams sp{L_.pitch, (i32)L_.h, (i32)L_.nw, L_.R, step_flags()};
-    hipk::launch_step_flow(a, flow_blocks_, sp, s);
+    hipk::StepParams sp{L_.pitch, (i32)L_.h, (i32)L_.nw, L_.R, step_flags() | fd.tflags};
+    if (fd.tile)
+        hipk::launch_step_flow_tile(cfg_.tile_waves, a, fd.blocks, fd.rows, fd.kmax, sp, s);
+    else
+        hipk::launch_step_flow(a, fd.blocks, sp, s);
     HIP_CHECK(hipGetLastError());
     flow_used_ = true;
 }

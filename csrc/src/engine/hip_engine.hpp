@@ -262,7 +262,8 @@ class HipEngine : public Engine {
     // generation).  With neighbours every rank keeps R: the exchanges must match.
     int superstep_depth() const override {
         if (res_) return std::max(L_.R, res_run_depth());
-        if (dual_ || flow_ || !tuned_ || cfg_.compat || kdepth_ <= 0 || kdepth_ >= L_.R || !halo_items(L_.R).empty())
+        if (flow_) return flow_superstep_depth();
+        if (dual_ || !tuned_ || cfg_.compat || kdepth_ <= 0 || kdepth_ >= L_.R || !halo_items(L_.R).empty())
             return L_.R;
         return (L_.R / kdepth_) * kdepth_;
     }
@@ -497,8 +498,24 @@ class HipEngine : public Engine {
         u32 n_items = 0, max_deps = 0;
         std::vector<int> cut;
         PlanStats st;
+        bool tile = false;  // LDS tile items (the tuned full-tile kernel is step_tile)
+        i64 rows = 0;       // tile items: chunk height of the plans
+        int kmax = 0;       // tile items: deepest pass
+        u32 tflags = 0;     // tile items: variant bits (STEP_TILE_*)
+        i64 blocks = 0;     // persistent grid (workgroups)
     };
-    bool flow_eligible() const;
+    bool flow_eligible();
+    // Flow items are LDS tiles when the tuned full-tile kernel is the tile kernel and a flow tile variant
+    // exists for its workgroup size and variant bits; otherwise step_temporal waves.
+    bool flow_tiles() const { return kern_[0] == "tile"; }
+    // Generations per flow superstep: the halo depth R with neighbours (the exchanges must match); on a
+    // rank without neighbours the hinted run length (at least R, at most 1024), so a whole run is one
+    // launch of passes that flow into each other (8192^2 x 1000: 32 tile passes, no kernel boundary).
+    // (Wave items keep R: a superstep's plan holds ~3000 items of 1 KiB of lane descriptors per pass.)
+    int flow_superstep_depth() const {
+        if (!flow_tiles() || !halo_items(L_.R).empty() || cfg_.run_hint == 0) return L_.R;
+        return (int)std::max<u64>((u64)L_.R, std::min<u64>(cfg_.run_hint, 1024));
+    }
     std::vector<int> flow_cut(int k) const;
     const FlowDev& flow_plan(int k);
     void flow_launch(int k, const u64* src, u64* dst, hipStream_t s);

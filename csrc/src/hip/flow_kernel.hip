@@ -42,10 +42,13 @@
 // Reference: the generation loop gol-main.c:93-116 and its per-generation launch + device sync,
 // gol-with-cuda.cu:264-284.
 #include <mutex>
+#include <set>
+#include <utility>
 
 #include "gol/hip_kernels.hpp"
 #include "stencil_device.hpp"
 #include "wave_runner.hpp"
+#include "tile_device.hpp"
 
 namespace gol {
 namespace hipk {
@@ -177,6 +180,81 @@ __global__ __launch_bounds__(64 * kWavesPerBlock) __attribute__((amdgpu_waves_pe
     }
 }
 
+// ---- tile items: one workgroup of NW waves per item (step_tile / step_tile_fold's device code) ----
+// The ticket is drawn by wave 0 and broadcast through an LDS word past the tile buffers; wave 0 also
+// waits for the item's dependencies, then a barrier releases the workgroup.  Every branch is on a
+// workgroup-uniform value (barrier-published LDS word, readfirstlane), and only wave-granular code is
+// conditional (wv == 0).  The deadlock argument is the wave kernel's with workgroups for waves.
+template <int NW, bool WRAPY, int LV, bool IP, bool FOLD>
+__global__ __launch_bounds__(64 * NW) void step_flow_tile(FlowArgs a, StepParams p, u32 ticket_slot) {
+    extern __shared__ __attribute__((aligned(16))) u32 tile_lds[];
+    const int lane = threadIdx.x & 63;
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    u32* s_ticket = tile_lds + ticket_slot;
+    const u32 n_groups = gridDim.x;
+    const u32 target = __builtin_amdgcn_readfirstlane(
+                           __hip_atomic_load(&a.ctl->epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) + 1u;
+    for (;;) {
+        if (wv == 0) {
+            const u32 t = __builtin_amdgcn_readfirstlane(
+                __hip_atomic_fetch_add(&a.ctl->next, lane == 0 ? 1u : 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+            if (t < a.n_items) {
+                const FlowItem* ip = a.items + t;
+                flow_wait(a, __builtin_amdgcn_readfirstlane(ip->dep_off), __builtin_amdgcn_readfirstlane(ip->ndeps),
+                          target, lane);
+                if (__builtin_amdgcn_readfirstlane(ip->pass) & FLOW_ITEM_EXCH) flow_wait_exch(a);
+            }
+            *s_ticket = t;  // (every lane, the same word)
+        }
+        __syncthreads();
+        const u32 t = __builtin_amdgcn_readfirstlane(*s_ticket);
+        __syncthreads();  // every wave has read the slot before wave 0 may rewrite it
+        if (t >= a.n_items) break;
+        const FlowItem* ip = a.items + t;
+        const int K = (int)__builtin_amdgcn_readfirstlane(ip->depth);
+        const u32 pass = __builtin_amdgcn_readfirstlane(ip->pass);
+        const LaneDesc d = a.lanes[(i64)t * kWaveLanes + lane];
+        const int nrows = __builtin_amdgcn_readfirstlane(d.nrows);
+        const bool odd = pass & 1u;
+        const u64* src = odd ? a.b : a.a;
+        u64* dst = odd ? a.a : a.b;
+        if (nrows > 0) {
+            if constexpr (FOLD)
+                fold_item<NW, WRAPY, LV, IP, true>(src, dst, d, nrows, p, K, tile_lds, wv, lane, blockIdx.x);
+            else
+                tile_item<NW, WRAPY, LV, IP, true>(src, dst, d, nrows, p, K, tile_lds, wv, lane, blockIdx.x);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's output rows have left it
+        __syncthreads();                                   // ... and every other wave's
+        if (wv == 0) __hip_atomic_store(&a.flags[t], target, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (wv == 0) {
+        const u32 left = __builtin_amdgcn_readfirstlane(
+            __hip_atomic_fetch_add(&a.ctl->done, lane == 0 ? 1u : 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+        if (left == n_groups - 1) {
+            __hip_atomic_store(&a.ctl->next, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(&a.ctl->done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(&a.ctl->exch, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(&a.ctl->epoch, target, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+}
+
+// tile variants of the flow kernel: double-buffered tiles with 4 generations per LDS pass, or in place
+// with 2 (the engine's defaults for 8 waves, step_kernels.hip tile_bits), folded or plain
+template <bool WRAPY, bool FOLD>
+const void* flow_tile_variant(u32 flags) {
+    if (flags & STEP_TILE_INPLACE)
+        return (flags & STEP_TILE_L2) ? (const void*)step_flow_tile<8, WRAPY, 2, true, FOLD> : nullptr;
+    return (flags & STEP_TILE_L4) ? (const void*)step_flow_tile<8, WRAPY, 4, false, FOLD> : nullptr;
+}
+const void* flow_tile_kernel_for(int nw_per_wg, u32 flags) {
+    if (nw_per_wg != 8) return nullptr;
+    const bool fold = flags & STEP_TILE_FOLD;
+    if (flags & STEP_WRAP_Y) return fold ? flow_tile_variant<true, true>(flags) : flow_tile_variant<true, false>(flags);
+    return fold ? flow_tile_variant<false, true>(flags) : flow_tile_variant<false, false>(flags);
+}
+
 const void* flow_kernel_for(u32 flags) {
     return (flags & STEP_WRAP_Y) ? (const void*)step_flow<ROWS_WRAP> : (const void*)step_flow<ROWS_GHOST>;
 }
@@ -214,6 +292,65 @@ void launch_step_flow(const FlowArgs& a, i64 n_blocks, const StepParams& p, hipS
     void* args[] = {(void*)&aa, (void*)&pp};
     hipError_t e = hipLaunchKernel(flow_kernel_for(p.flags), dim3((unsigned)n_blocks), dim3(64 * kWavesPerBlock), args, 0, s);
     if (e != hipSuccess) throw Error(strprintf("step_flow launch failed: %s", hipGetErrorString(e)));
+}
+
+bool flow_tile_supported(int nw_per_wg, u32 flags) { return flow_tile_kernel_for(nw_per_wg, flags) != nullptr; }
+
+// LDS of a flow tile item: the tile kernel's (tile_lds_bytes), then the 16-byte ticket slot
+static size_t flow_tile_lds_bytes(i64 rows, int k, int nw, u32 flags) { return tile_lds_bytes(rows, k, nw, flags) + 16; }
+
+i64 flow_tile_max_rows(int k, int nw_per_wg, u32 flags) {
+    // the largest rows whose tile plus the ticket slot fit the 160 KiB
+    i64 r = tile_max_rows(k, nw_per_wg, flags);
+    while (r > 0 && flow_tile_lds_bytes(r, k, nw_per_wg, flags) > kMaxLdsBytes) --r;
+    return r;
+}
+
+static const void* flow_tile_checked(int nw_per_wg, u32 flags) {
+    const void* f = flow_tile_kernel_for(nw_per_wg, flags);
+    if (!f) throw Error(strprintf("step_flow: no tile variant for %d waves per workgroup, flags 0x%x", nw_per_wg, flags));
+    static std::mutex mu;
+    static std::set<std::pair<int, const void*>> attr_set;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) throw Error("step_flow: no current HIP device");
+    std::lock_guard<std::mutex> lk(mu);
+    if (attr_set.insert({dev, f}).second) {
+        const hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kMaxLdsBytes);
+        if (e != hipSuccess) {
+            attr_set.erase({dev, f});
+            throw Error(strprintf("step_flow: hipFuncSetAttribute: %s", hipGetErrorString(e)));
+        }
+    }
+    return f;
+}
+
+int flow_tile_blocks_per_cu(int nw_per_wg, i64 rows, int kmax, u32 flags) {
+    const void* f = flow_tile_checked(nw_per_wg, flags);
+    int nb = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, f, 64 * nw_per_wg, flow_tile_lds_bytes(rows, kmax, nw_per_wg, flags)) !=
+            hipSuccess ||
+        nb < 1)
+        return 1;
+    return std::min(nb, 8);
+}
+
+void launch_step_flow_tile(int nw_per_wg, const FlowArgs& a, i64 n_blocks, i64 rows, int kmax, const StepParams& p,
+                           hipStream_t s) {
+    if (n_blocks < 1) throw Error("step_flow: empty grid");
+    if (kmax < 1 || kmax > 64) throw Error(strprintf("step_flow: tile depth %d outside 1..64", kmax));
+    const size_t bytes = flow_tile_lds_bytes(rows, kmax, nw_per_wg, p.flags);
+    if (rows < 1 || bytes > kMaxLdsBytes)
+        throw Error(strprintf("step_flow: %lld-row tiles at depth %d exceed the LDS", (long long)rows, kmax));
+    if ((p.flags & STEP_TILE_FOLD) && rows < kFoldMinRows)
+        throw Error(strprintf("step_flow: a folded tile plan needs at least %d rows", kFoldMinRows));
+    const void* f = flow_tile_checked(nw_per_wg, p.flags);
+    StepParams pp = p;
+    if (!pp.trash) pp.trash = trash_of_current_device();
+    FlowArgs aa = a;
+    u32 slot = (u32)(tile_lds_bytes(rows, kmax, nw_per_wg, p.flags) / 4);
+    void* args[] = {(void*)&aa, (void*)&pp, (void*)&slot};
+    const hipError_t e = hipLaunchKernel(f, dim3((unsigned)n_blocks), dim3(64 * nw_per_wg), args, bytes, s);
+    if (e != hipSuccess) throw Error(strprintf("step_flow (tiles) launch failed: %s", hipGetErrorString(e)));
 }
 
 bool flow_fault(FlowCtl* ctl, hipStream_t s) {

@@ -130,3 +130,33 @@ def test_flow_2d_thread_ranks(gol, monkeypatch):
     for r0, c0, b in out:
         board[r0 : r0 + b.shape[0], c0 : c0 + b.shape[1]] = b
     assert np.array_equal(board, numpy_step(initial_board(5, N, 1, True, 5), gens))
+
+
+@pytest.mark.parametrize("N,gens,hint,env", [(1024, 200, 200, {}), (1024, 137, 137, {"GOL_TILE_FOLD": "1"}),
+                                            (2048, 96, 96, {"GOL_TILE_INPLACE": "1", "GOL_TILE_FOLD": "0"}),
+                                            (768, 75, 0, {})])
+def test_flow_tiles_vs_numpy(gol, monkeypatch, N, gens, hint, env):
+    """Flow supersteps of LDS tile items (the tile kernel's device code, one workgroup per item): the
+    hinted run is one launch of tile passes (folded, double-buffered or in place)."""
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    s = _sim(gol, N, monkeypatch, kernel="tile", run_hint=hint).init(5, seed=N + gens)
+    st = s.stats()
+    assert "+flow" in st["schedule"] and st["kernel"].startswith("flow"), st
+    s.step(gens)
+    assert np.array_equal(s.board(), numpy_step(initial_board(5, N, 1, True, N + gens), gens))
+
+
+def test_flow_config2_vs_torch(gol, monkeypatch):
+    """BASELINE config 2 on the flow schedule (auto kernel: tile items at 8192^2), 1000-generation hint."""
+    import torch
+
+    N, seed = 8192, 0x5EED
+    s = _sim(gol, N, monkeypatch, run_hint=1000).init(5, seed=seed)
+    ref = torch.as_tensor(initial_board(5, N, 1, True, seed), device="cuda:0")
+    for g in (100, 37, 1000):
+        s.step(g)
+        ref = torch_step(ref, g, device="cuda:0")
+        got = s.board()
+        want = ref.cpu().numpy()
+        assert np.array_equal(got, want), f"after +{g}: {int((got != want).sum())} cells differ"
