@@ -128,6 +128,8 @@ struct FlowArgs {
     u32* flags;              // n_items completion flags (zero-initialised once per plan)
     FlowCtl* ctl;
     u32 n_items;
+    u32 variant;             // host-side kernel choice: bit 0 draws each wave's next ticket at the start
+                             // of its current item (wave items only)
 };
 bool flow_depth_supported(int k);
 int flow_max_depth();

@@ -121,7 +121,10 @@ __device__ __forceinline__ void flow_item(const u64* src, u64* dst, const LaneDe
 // Three waves per SIMD, as step_temporal<8> (163 VGPRs): the persistent item loop around the
 // pipelines needs ~190 by default, and capping it spills 3-5 registers to scratch, reloaded once per
 // item (outside the row loops).
-template <int ROWS>
+// PF: a wave draws its NEXT ticket when it starts an item, so the draw's latency (a contended atomic,
+// ~1 us under load) hides behind the item instead of preceding the next one.  The deadlock argument
+// holds: a wave holding a drawn-but-unstarted ticket is working on a smaller one.
+template <int ROWS, bool PF>
 __global__ __launch_bounds__(64 * kWavesPerBlock) __attribute__((amdgpu_waves_per_eu(3))) void step_flow(FlowArgs a,
                                                                                                     StepParams p) {
     const int lane = threadIdx.x & 63;
@@ -133,10 +136,13 @@ __global__ __launch_bounds__(64 * kWavesPerBlock) __attribute__((amdgpu_waves_pe
     // store let the compiler thread that condition across the loop's back edge, and lanes 1-63 went on
     // re-running ticket 0 — the first version hung.  The draw is an all-lane atomic adding 1 from lane
     // 0 and 0 from the others; the flag is stored by every lane to the same word.)
+    u32 t = __builtin_amdgcn_readfirstlane(
+        __hip_atomic_fetch_add(&a.ctl->next, lane == 0 ? 1u : 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
     for (;;) {
-        const u32 t = __builtin_amdgcn_readfirstlane(
-            __hip_atomic_fetch_add(&a.ctl->next, lane == 0 ? 1u : 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
         if (t >= a.n_items) break;
+        u32 t_next = 0;  // (PF: a per-lane register until the item's end, so no wait is forced here)
+        if constexpr (PF)
+            t_next = __hip_atomic_fetch_add(&a.ctl->next, lane == 0 ? 1u : 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         // the item's fields as wave-uniform values (they steer every branch below)
         const FlowItem* ip = a.items + t;
         const u32 depth = __builtin_amdgcn_readfirstlane(ip->depth);
@@ -165,6 +171,11 @@ __global__ __launch_bounds__(64 * kWavesPerBlock) __attribute__((amdgpu_waves_pe
         // every store of the item has left the wave (write-through) before its flag does
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __hip_atomic_store(&a.flags[t], target, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if constexpr (PF)
+            t = __builtin_amdgcn_readfirstlane(t_next);
+        else
+            t = __builtin_amdgcn_readfirstlane(
+                __hip_atomic_fetch_add(&a.ctl->next, lane == 0 ? 1u : 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
     }
     // The last wave out resets the tickets and advances the epoch for the next launch (every other
     // wave has drawn its last ticket before its `done` increment).
@@ -255,8 +266,10 @@ const void* flow_tile_kernel_for(int nw_per_wg, u32 flags) {
     return fold ? flow_tile_variant<false, true>(flags) : flow_tile_variant<false, false>(flags);
 }
 
-const void* flow_kernel_for(u32 flags) {
-    return (flags & STEP_WRAP_Y) ? (const void*)step_flow<ROWS_WRAP> : (const void*)step_flow<ROWS_GHOST>;
+const void* flow_kernel_for(u32 flags, u32 variant = 0) {
+    if (variant & 1u)
+        return (flags & STEP_WRAP_Y) ? (const void*)step_flow<ROWS_WRAP, true> : (const void*)step_flow<ROWS_GHOST, true>;
+    return (flags & STEP_WRAP_Y) ? (const void*)step_flow<ROWS_WRAP, false> : (const void*)step_flow<ROWS_GHOST, false>;
 }
 
 }  // namespace
@@ -290,7 +303,8 @@ void launch_step_flow(const FlowArgs& a, i64 n_blocks, const StepParams& p, hipS
     if (!pp.trash) pp.trash = trash_of_current_device();
     FlowArgs aa = a;
     void* args[] = {(void*)&aa, (void*)&pp};
-    hipError_t e = hipLaunchKernel(flow_kernel_for(p.flags), dim3((unsigned)n_blocks), dim3(64 * kWavesPerBlock), args, 0, s);
+    hipError_t e = hipLaunchKernel(flow_kernel_for(p.flags, a.variant), dim3((unsigned)n_blocks), dim3(64 * kWavesPerBlock),
+                                   args, 0, s);
     if (e != hipSuccess) throw Error(strprintf("step_flow launch failed: %s", hipGetErrorString(e)));
 }
 

@@ -121,6 +121,7 @@ int main(int argc, char** argv) {
     fa.flags = upload(std::vector<u32>(fp.items.size(), 0u));
     fa.ctl = upload(std::vector<hipk::FlowCtl>(1, hipk::FlowCtl{0, 0, 0, 0}));
     fa.n_items = (u32)fp.items.size();
+    fa.variant = getenv("KB_FLOW_PF") ? (u32)atoi(getenv("KB_FLOW_PF")) : 0u;  // 1: ticket prefetch
     double avg_deps = fp.items.empty() ? 0 : (double)fp.deps.size() / (double)fp.items.size();
     printf("flow plan: %zu items, %u..%zu deps (max %u, avg %.1f), rows/pass:", fp.items.size(), 0u, fp.deps.size(),
            fp.max_deps, avg_deps);

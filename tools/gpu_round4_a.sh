@@ -17,5 +17,6 @@ bash tools/flow_sweep.sh gpurun_out/flow_sweep.txt || exit 1
 step bench-ab
 bash tools/flow_bench_ab.sh gpurun_out/flow_bench_ab.jsonl 5 > gpurun_out/flow_bench_ab.txt 2>&1 || { cat gpurun_out/flow_bench_ab.txt; exit 1; }
 step trace
-GOL_SCHEDULE=flow timeout -k 10 240 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_flow -o flow -- python3 bench.py --gpus 1 --steps 20 --warmup 5 > gpurun_out/prof_flow_bench.txt 2>&1 || { echo "trace rc=$?"; tail -20 gpurun_out/prof_flow_bench.txt; exit 1; }
+GOL_SCHEDULE=flow GOL_ROCTX=1 timeout -k 10 240 rocprofv3 --kernel-trace --marker-trace --stats -d gpurun_out/prof_flow -o flow -- python3 bench.py --gpus 1 --steps 20 --warmup 5 --no-phases > gpurun_out/prof_flow_bench.txt 2>&1 || { echo "trace rc=$?"; tail -20 gpurun_out/prof_flow_bench.txt; exit 1; }
+python3 tools/timed_trace.py gpurun_out/prof_flow > gpurun_out/prof_flow_timed.txt 2>&1 || true
 step done
