@@ -571,12 +571,15 @@ static void test_flow_plan() {
         i64 rows;
         bool xwrap, wrap_y;
         int ext;  // ghost-row extension per remaining generation (1: y neighbours, multi-pass)
+        bool fold = false;  // folded 32-lane tile items (step_flow_tile)
     };
     const std::vector<Case> cases = {
         {3, 48, {2, 2, 1}, 8, true, true, 0},   {5, 40, {3, 3}, 7, true, true, 0},
         {1, 30, {1, 2, 3}, 6, true, true, 0},   {130, 24, {2, 2}, 5, true, true, 0},
         {4, 40, {3, 2, 2}, 9, false, false, 1}, {2, 36, {2, 2, 2, 2}, 6, true, false, 1},
         {64, 64, {4, 4}, 16, true, true, 0},
+        // folded tile items (plans of 32-lane tiles, lanes 32-63 repeating 0-31), torus and ghost rows
+        {64, 120, {6, 5, 6}, 30, true, true, 0, true}, {70, 96, {4, 4}, 28, false, false, 1, true},
     };
     for (const Case& cs : cases) {
         std::vector<FlowPass> ps;
@@ -585,7 +588,7 @@ static void test_flow_plan() {
         for (int k : cs.cut) {
             left -= k;
             const i64 e = cs.ext ? left : 0;
-            ps.push_back({k, {{-e, cs.h + e, 0, cs.nw}}, cs.rows});
+            ps.push_back({k, {{-e, cs.h + e, 0, cs.nw}}, cs.rows, cs.fold});
         }
         FlowPlan fp;
         const bool mark = cs.ext != 0;  // ranks with neighbours: the exchange-overlapped variant's plan
@@ -603,7 +606,7 @@ static void test_flow_plan() {
             std::vector<int> cov((size_t)(rows_all * cols_all), 0);
             for (u32 t = fp.pass_begin[j]; t < fp.pass_begin[j + 1]; ++t) {
                 CHECK((fp.items[t].pass & ~FLOW_ITEM_EXCH) == j && fp.items[t].depth == (u32)cs.cut[j]);
-                for (int l = 0; l < 64; ++l) {
+                for (int l = 0; l < (cs.fold ? 32 : 64); ++l) {  // (folded tiles: lanes 32-63 repeat 0-31)
                     const LaneDesc& d = fp.lanes[(size_t)t * 64 + l];
                     if (!(d.flags & LANE_STORE)) continue;
                     for (i64 r = d.row0; r < d.row0 + d.nrows; ++r) cov[(size_t)((r + R) * cols_all + d.col + 1)]++;
