@@ -93,8 +93,12 @@ int main(int argc, char** argv) {
     if (bpc <= 0) bpc = hipk::flow_blocks_per_cu(flags);
     const i64 resident = (i64)bpc * kWavesPerBlock * cus;
     std::vector<FlowPass> fps;
-    for (int k : cut) {
-        const i64 target = std::max<i64>(1, (i64)(per_round * (double)resident));
+    // KB_LAST_PR: items per round of the LAST pass (finer items there shorten the superstep's drain)
+    const double last_pr = getenv("KB_LAST_PR") ? atof(getenv("KB_LAST_PR")) : per_round;
+    for (size_t j = 0; j < cut.size(); ++j) {
+        const int k = cut[j];
+        const double pr = j + 1 == cut.size() ? last_pr : per_round;
+        const i64 target = std::max<i64>(1, (i64)(pr * (double)resident));
         fps.push_back({k, rg, balanced_rows_per_chunk(rg, L.nw, N, k, target, 2 * k, true)});
     }
     FlowPlan fp;
