@@ -66,6 +66,18 @@ def parse_args(argv=None):
     return ap.parse_args(argv)
 
 
+def rank_problems(ranks, P, rccl_ranks):
+    """Why a multi-rank record is not a valid measurement: the ranks ran different schedules / kernels /
+    depths, or the RCCL communicator does not span every rank (rccl_ranks None: no RCCL data plane)."""
+    problems = []
+    if len({(r["schedule"], r["kernel"], r["depth"]) for r in ranks}) > 1:
+        problems.append("ranks disagree on the schedule: " +
+                        ", ".join(f"{i}:{r['schedule']}/{r['kernel']}/{r['depth']}" for i, r in enumerate(ranks)))
+    if rccl_ranks is not None and P > 1 and rccl_ranks != P:
+        problems.append(f"the RCCL communicator spans {rccl_ranks} of {P} ranks")
+    return problems
+
+
 def _free_port() -> int:
     with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
         s.bind(("127.0.0.1", 0))
@@ -243,12 +255,7 @@ def main() -> int:
             "exchange_us": round(ph["exchange_us"], 2) if phases is not None and "exchange_us" in ph else None,
             "superstep_us": round(ph["superstep_us"], 2) if phases is not None and "superstep_us" in ph else None}
     ranks = gather(mine)
-    problems = []
-    if len({(r["schedule"], r["kernel"], r["depth"]) for r in ranks}) > 1:
-        problems.append("ranks disagree on the schedule: " +
-                        ", ".join(f"{i}:{r['schedule']}/{r['kernel']}/{r['depth']}" for i, r in enumerate(ranks)))
-    if rccl is not None and P > 1 and transport.data_plane_ranks() != P:
-        problems.append(f"the RCCL communicator spans {transport.data_plane_ranks()} of {P} ranks")
+    problems = rank_problems(ranks, P, transport.data_plane_ranks() if rccl is not None else None)
     per_rank_block = {
         "per_rank_elapsed_us": [r["elapsed_us"] for r in per_rank],
         "per_rank_t0_offset_us": [r["t0_offset_us"] for r in per_rank],

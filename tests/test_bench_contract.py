@@ -97,3 +97,18 @@ def test_bench_hung_rank_ends_the_job():
     assert r.returncode != 0
     assert "watchdog" in r.stderr
     assert dt < 120, dt
+
+
+def test_bench_rank_problems():
+    """The checks that turn a multi-rank record into an error record (non-zero exit, value null)."""
+    sys.path.insert(0, REPO)
+    import bench
+
+    same = [{"schedule": "full+flow", "kernel": "flow", "depth": 128}] * 4
+    assert bench.rank_problems(same, 4, 4) == []
+    assert bench.rank_problems(same, 4, None) == []  # host transport: no communicator to check
+    diff = same[:3] + [{"schedule": "full+subtiles2", "kernel": "temporal", "depth": 128}]
+    (p,) = bench.rank_problems(diff, 4, 4)
+    assert "disagree" in p and "3:full+subtiles2/temporal/128" in p
+    (p,) = bench.rank_problems(same, 4, 2)
+    assert "spans 2 of 4" in p
