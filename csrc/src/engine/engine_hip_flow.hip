@@ -54,10 +54,12 @@ const HipEngine::FlowDev& HipEngine::flow_plan(int k) {
     const bool wrapy = (step_flags() & hipk::STEP_WRAP_Y) != 0;
     FlowDev fd;
     std::vector<FlowPass> fps;
-    if (flow_tiles()) {
+    const int kmax = *std::max_element(ps.begin(), ps.end());
+    // (tile items need a flow twin of the variant the deepest pass's tile plan uses; a superstep whose
+    // cut lands on another variant runs wave items)
+    if (flow_tiles() && hipk::flow_tile_supported(cfg_.tile_waves, step_flags() | plan(0, kmax, ext_after(ps, 0)).tflags)) {
         // LDS tile items: every pass uses the tile variant and chunk height of the deepest pass's plan
         // (a shallower pass needs less LDS), capped at the flow variant's capacity (its ticket slot)
-        const int kmax = *std::max_element(ps.begin(), ps.end());
         const DevPlan& p0 = plan(0, kmax, ext_after(ps, 0));
         fd.tile = true;
         fd.kmax = kmax;
