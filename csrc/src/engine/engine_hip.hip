@@ -100,6 +100,8 @@ HipEngine::HipEngine(const Geometry& g, const EngineConfig& c, std::shared_ptr<T
     HIP_CHECK(hipStreamCreateWithPriority(&s_comp_, hipStreamNonBlocking, 0));
     HIP_CHECK(hipStreamCreateWithPriority(&s_comm_, hipStreamNonBlocking,
                                           prio_greatest));
+    s_base_ = s_comp_;
+    engines_on_device(dev_, this, +1);
     events_needed_ = cfg_.force_split || !halo_items(L_.R).empty();
     // All device memory work is ordered on the engine's own streams.  (They are non-blocking:
     // null-stream calls such as hipMemset, or a pageable hipMemcpy whose DMA may still be in
@@ -218,8 +220,10 @@ HipEngine::~HipEngine() {
             if (e) hipEventDestroy(e);
     if (cfg_.profile)
         for (auto e : {ev_t0_, ev_t1_, ev_t2_, ev_t3_}) hipEventDestroy(e);
-    hipStreamDestroy(s_comp_);
+    if (s_ov_) hipStreamDestroy(s_ov_);
+    hipStreamDestroy(s_base_);
     hipStreamDestroy(s_comm_);
+    engines_on_device(dev_, this, -1);
 }
 
 std::vector<u64> HipEngine::tile_words() {
@@ -386,7 +390,7 @@ void HipEngine::do_init(const PatternSpec& p) {
         stats_.lane_efficiency = 0;
     } else if (flow_) {
         const FlowDev& fd = flow_plan(superstep_depth());
-        stats_.plan_waves = flow_blocks_ * kWavesPerBlock;  // the persistent grid
+        stats_.plan_waves = fd.blocks * (fd.tile ? cfg_.tile_waves : kWavesPerBlock);  // the persistent grid
         stats_.lane_efficiency = fd.st.lane_rows ? (double)fd.st.out_words / (double)fd.st.lane_rows : 0.0;
     } else {
         const DevPlan& fp = full_plan_stats();

@@ -10,10 +10,50 @@
 // measured rate decides whether a run uses it.
 // Reference: the generation loop gol-main.c:93-116, one launch + device sync per generation in
 // gol-with-cuda.cu:264-284.
+#include <algorithm>
+#include <map>
+#include <mutex>
+
 #include "hip_engine.hpp"
 
 namespace gol {
 namespace hipeng {
+
+namespace {
+std::mutex g_dev_mu;
+std::map<int, std::vector<const HipEngine*>> g_dev_engines;
+}  // namespace
+
+std::pair<int, int> HipEngine::engines_on_device(int dev, const HipEngine* e, int op) {
+    std::lock_guard<std::mutex> lk(g_dev_mu);
+    std::vector<const HipEngine*>& v = g_dev_engines[dev];
+    auto it = std::find(v.begin(), v.end(), e);
+    if (op > 0 && it == v.end()) v.push_back(e);
+    if (op < 0 && it != v.end()) v.erase(it);
+    it = std::find(v.begin(), v.end(), e);
+    return {it == v.end() ? -1 : (int)(it - v.begin()), (int)v.size()};
+}
+
+// The CU-restricted compute stream of flow+ov (hip_engine.hpp kOvReservedCus): CUs [0, cus - reserved)
+// split evenly over the engines of this device, so the top kOvReservedCus stay free for the exchange's
+// kernels on the (unrestricted) comm stream.
+bool HipEngine::ov_stream() {
+    if (s_ov_) return true;
+    const std::pair<int, int> sn = engines_on_device(dev_, this, 0);
+    const int usable = cus_ - kOvReservedCus;
+    if (sn.first < 0 || usable < sn.second) return false;
+    const int lo = (int)((i64)sn.first * usable / sn.second), hi = (int)((i64)(sn.first + 1) * usable / sn.second);
+    std::vector<u32> mask((size_t)(cus_ + 31) / 32, 0u);
+    for (int c = lo; c < hi; ++c) mask[(size_t)c / 32] |= 1u << (c % 32);
+    hipStream_t s = nullptr;
+    if (hipExtStreamCreateWithCUMask(&s, (u32)mask.size(), mask.data()) != hipSuccess || !s) {
+        (void)hipGetLastError();
+        return false;
+    }
+    s_ov_ = s;
+    ov_cus_ = hi - lo;
+    return true;
+}
 
 bool HipEngine::flow_eligible() {
     // one tile; every pass is a step_temporal pass (no LDS-tile / pipe / LDS kernels, no split bands);
@@ -46,6 +86,8 @@ const HipEngine::FlowDev& HipEngine::flow_plan(int k) {
     const int key = k * 2 + (ov ? 1 : 0);
     auto it = flow_plans_.find(key);
     if (it != flow_plans_.end()) return it->second;
+    if (ov && !ov_stream()) throw Error("flow plan: no CU-restricted stream for the exchange-overlapped launch");
+    const i64 cus = flow_cus(ov);
     if (!flow_ctl_) {
         HIP_CHECK(hipMalloc(&flow_ctl_, sizeof(hipk::FlowCtl)));
         HIP_CHECK(hipMemsetAsync(flow_ctl_, 0, sizeof(hipk::FlowCtl), s_comp_));
@@ -67,13 +109,12 @@ const HipEngine::FlowDev& HipEngine::flow_plan(int k) {
         const u32 f = step_flags() | p0.tflags;
         fd.rows = std::min<i64>(p0.rows, hipk::flow_tile_max_rows(kmax, cfg_.tile_waves, f));
         if (p0.fold && fd.rows < hipk::kFoldMinRows) throw Error("flow plan: folded tiles do not fit with the ticket slot");
-        fd.blocks = (i64)hipk::flow_tile_blocks_per_cu(cfg_.tile_waves, fd.rows, kmax, f) * cus_;
+        fd.blocks = (i64)hipk::flow_tile_blocks_per_cu(cfg_.tile_waves, fd.rows, kmax, f) * cus;
         for (size_t j = 0; j < ps.size(); ++j)
             fps.push_back({ps[j], regions(0, ps[j], ext_after(ps, j)), fd.rows, p0.fold});
     } else {
-        if (flow_blocks_ <= 0) flow_blocks_ = (i64)hipk::flow_blocks_per_cu(step_flags()) * cus_;
-        fd.blocks = flow_blocks_;
-        const i64 resident = flow_blocks_ * kWavesPerBlock;
+        fd.blocks = (i64)hipk::flow_blocks_per_cu(step_flags()) * cus;
+        const i64 resident = fd.blocks * kWavesPerBlock;
         // items per pass: one round of the persistent grid (GOL_FLOW_ROUNDS in percent scales it; big
         // tiles take several rounds of ~45K-row segments, as the pass kernels' plans)
         const double scale = (double)env_int("GOL_FLOW_ROUNDS", 100) / 100.0;
@@ -147,6 +188,7 @@ void HipEngine::flow_superstep(int k) {
     const std::vector<int>& ps = pass_depths(k);
     const std::vector<HaloItem>& items = items_for(k);
     if (flow_ov_active(k)) {
+        if (s_comp_ != s_ov_) throw Error("flow+ov superstep outside the CU-restricted compute stream");
         flow_plan(k);  // (allocates the control block the flag lives in)
         prepare(k);
         HIP_CHECK(hipStreamWaitEvent(s_comm_, ev_ready_, 0));

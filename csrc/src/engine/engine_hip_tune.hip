@@ -156,9 +156,12 @@ void HipEngine::choose_schedule() {
     if (cands[0] != "split" && flow_eligible()) {
         double ok = flow_timing_buffers() ? 1.0 : 0.0;
         if (t_->size() > 1) ok = t_->allreduce_min(ok);
+        // flow+ov also needs its CU-restricted stream (hip_engine.hpp kOvReservedCus) on every rank
+        double ov_ok = nbrs && device_transport_ && ov_stream() ? 1.0 : 0.0;
+        if (t_->size() > 1) ov_ok = t_->allreduce_min(ov_ok);
         if (ok > 0) {
             cands.push_back("flow");
-            if (nbrs && device_transport_) cands.push_back("flow+ov");
+            if (ov_ok > 0) cands.push_back("flow+ov");
             if (cfg_.graph && (!nbrs || (device_transport_ && t_->graph_capturable() && cfg_.graph_rccl != 0)))
                 cands.push_back("flow+graph");
         }
@@ -166,6 +169,8 @@ void HipEngine::choose_schedule() {
             if (ok <= 0) throw Error("GOL_SCHEDULE=flow: no device memory for the flow timing scratch");
             if (cfg_.sched == "flow+ov" && !(nbrs && device_transport_))
                 throw Error("GOL_SCHEDULE=flow+ov needs neighbours and a device transport (RCCL)");
+            if (cfg_.sched == "flow+ov" && ov_ok <= 0)
+                throw Error("GOL_SCHEDULE=flow+ov: no CU-restricted compute stream (hipExtStreamCreateWithCUMask)");
             cands = {cfg_.sched};
         }
     } else if (cfg_.sched == "flow" || cfg_.sched == "flow+ov") {
@@ -227,6 +232,13 @@ void HipEngine::choose_schedule() {
     flow_ = pick.rfind("flow", 0) == 0;
     flow_graph_ = pick == "flow+graph";
     flow_ov_ = pick == "flow+ov";
+    // flow+ov runs on the CU-restricted compute stream from here on (every later launch of the engine
+    // is ordered on it)
+    hipStream_t sc = flow_ov_ ? s_ov_ : s_base_;
+    if (s_comp_ != sc) {
+        HIP_CHECK(hipStreamSynchronize(s_comp_));
+        s_comp_ = sc;
+    }
     split_ = pick == "split";
     dual_ = pick.rfind("subtiles", 0) == 0;
     sub_overlap_ = pick == "subtiles+ov" ? 1 : (pick == "subtiles+ov2" ? 2 : 0);
@@ -314,6 +326,13 @@ void HipEngine::time_schedule(const std::string& c, int k, int reps, bool eager)
         flow_ = true;
         flow_ov_ = c == "flow+ov";
         const std::vector<HaloItem>& items = items_for(k);
+        // (flow+ov on its CU-restricted stream, as the runs)
+        const hipStream_t keep = s_comp_;
+        if (flow_ov_active(k) && s_comp_ != s_ov_) {
+            if (!ov_stream()) throw Error("flow+ov timing: no CU-restricted compute stream");
+            HIP_CHECK(hipStreamSynchronize(s_comp_));
+            s_comp_ = s_ov_;
+        }
         for (int i = 0; i < reps; ++i) {
             if (flow_ov_active(k)) {  // as flow_superstep's overlapped path, on scratch
                 flow_plan(k);  // (allocates the control block the flag lives in)
@@ -333,6 +352,10 @@ void HipEngine::time_schedule(const std::string& c, int k, int reps, bool eager)
                     exchange_staged(k, items, cur_, s_comp_);
             }
             flow_launch(k, flow_scratch_, buf_[cur_ ^ 1], s_comp_);
+        }
+        if (s_comp_ != keep) {
+            HIP_CHECK(hipStreamSynchronize(s_comp_));
+            s_comp_ = keep;
         }
         flow_ = f;
         flow_ov_ = fo;

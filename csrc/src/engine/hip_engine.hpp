@@ -617,6 +617,23 @@ class HipEngine : public Engine {
     // launch's interior items run; the items reading ghost cells wait for its device flag
     bool flow_ov_ = false;
     bool flow_ov_active(int k) { return flow_ov_ && device_transport_ && !items_for(k).empty(); }
+    // The flow+ov launch holds every wave slot it is given until its band items have seen the exchange
+    // flag, so the exchange's own kernels (RCCL's send/recv kernel: 248-256 VGPRs and 37.6 KB of LDS per
+    // 256-512-thread workgroup on gfx950, read from librccl's code-object notes; HIP's copy kernels)
+    // must find CUs the persistent grid does not occupy: a wave flow grid at 3 waves/SIMD leaves 8 of
+    // the 512 VGPRs per SIMD lane, a tile flow grid the LDS of its CU.  flow+ov launches therefore go
+    // to a compute stream restricted (hipExtStreamCreateWithCUMask) to all CUs but kOvReservedCus, and
+    // their grid is sized to the CUs it may use.  Engines sharing a device (thread ranks) split those
+    // CUs, so no engine's launch can take the CUs another's exchange waits for.
+    static constexpr int kOvReservedCus = 8;
+    hipStream_t s_base_ = nullptr;  // the engine's unrestricted compute stream
+    hipStream_t s_ov_ = nullptr;    // the CU-restricted one (s_comp_ while flow+ov is the schedule)
+    int ov_cus_ = 0;                // CUs of s_ov_
+    bool ov_stream();               // create s_ov_ (false: not possible here)
+    // The live engines of a device in this process: op +1 registers e, -1 removes it, 0 queries;
+    // returns {e's slot among them, their count}.
+    static std::pair<int, int> engines_on_device(int dev, const HipEngine* e, int op);
+    i64 flow_cus(bool ov) const { return ov ? (i64)ov_cus_ : (i64)cus_; }
     u64* flow_scratch_ = nullptr;  // timing scratch of flow candidates (a flow launch writes both buffers)
     // Flow candidates are timed on scratch: the board copied to flow_scratch_, the launch between it and
     // buf[cur ^ 1].  False when there is no memory for one more board.
@@ -658,7 +675,6 @@ class HipEngine : public Engine {
     bool flow_ = false;                     // supersteps run as one step_flow launch (schedule "+flow")
     bool flow_used_ = false;                // a flow launch ran (fault check at readouts)
     hipk::FlowCtl* flow_ctl_ = nullptr;     // its ticket / epoch / fault words
-    i64 flow_blocks_ = 0;                   // its persistent grid (workgroups)
     std::map<int, FlowDev> flow_plans_;     // by superstep depth x 2 + exchange-overlapped
     bool res_ = false;  // supersteps run the resident kernel
     int res_kin_ = 0;   // its generations per in-kernel halo exchange
