@@ -203,11 +203,18 @@ void HipEngine::choose_schedule() {
                 synchronize();
                 const double dt = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
                 best[c] = std::min(best[c], t_->allreduce_max(dt) * 1e6 / (rc * kc));
+                // a flow launch whose wait timed out (clears the fault word): the candidate is dropped
+                if (fl && flow_ctl_ && hipk::flow_fault(flow_ctl_, s_comp_)) {
+                    fprintf(stderr, "[gol] rank %d: schedule candidate %s: a flow wait timed out (dropped)\n", g_.rank,
+                            cands[c].c_str());
+                    sched_graph_failed_.insert(cands[c]);
+                }
                 init_step("init: schedule timing", cands[c].c_str(), kc, (float)best[c]);
             }
         size_t bi = 0;
         for (size_t c = 0; c < cands.size(); ++c) {
-            // a candidate whose timing graph could not be captured on some rank is dropped
+            // a candidate whose timing graph could not be captured (or whose flow launch faulted) on some
+            // rank is dropped
             if (t_->allreduce_max(sched_graph_failed_.count(cands[c]) ? 1.0 : 0.0) > 0) best[c] = 1e30;
             sched_us_[cands[c]] = best[c];
             if (best[c] < best[bi]) bi = c;
