@@ -109,15 +109,19 @@ void launch_step_pipe(int nw, int L, const u64* src, u64* dst, const LaneDesc* p
 // step_flow (flow_kernel.hip): a superstep of several step_temporal passes as ONE launch of a
 // persistent grid whose waves draw the items of a flow plan (plan.hpp build_flow_plan) in ticket
 // order and wait for each item's dependencies through per-item completion flags.
-struct FlowCtl {  // device memory, zero-initialised once; the kernel leaves next = done = exch = 0
-    u32 next;     // ticket counter
-    u32 done;     // waves that drew their last ticket
-    u32 epoch;    // launches completed (flags of the running launch hold epoch + 1)
-    u32 fault;    // a dependency wait timed out: the board is invalid
-    u32 exch;     // exchange-overlapped launches: set to 1 by the comm stream once the halo exchange of
-                  // this superstep is complete (hipStreamWriteValue32); the items marked FLOW_ITEM_EXCH
-                  // wait for it, the last wave out resets it
-    u32 pad[3];
+// Every word the kernel's waves contend for sits in a 128-byte line of its own (a same-line poll
+// doubles the cost of the atomics: tools/ticket_probe.hip, profiles/ticket_probe.txt).
+constexpr int kFlowSeqs = 8;  // ticket sequences: one per XCD
+struct FlowCtl {  // device memory, zero-initialised once
+    // Ticket counters: launch e (FlowArgs::epoch = e) draws from next[e & 1][its sequence] and zeroes
+    // next[(e + 1) & 1] for launch e + 1 (launch e - 1, which used them, has completed: stream order).
+    u32 next[2][kFlowSeqs][32];
+    u32 fault;  // a dependency wait timed out: the board is invalid
+    u32 pad0[31];
+    u32 exch;   // exchange-overlapped launches: set to the launch's epoch by the comm stream once the
+                // halo exchange of its superstep is complete (hipStreamWriteValue32); the items marked
+                // FLOW_ITEM_EXCH wait for it
+    u32 pad1[31];
 };
 struct FlowArgs {
     u64* a;                  // even passes read a and write b, odd passes the reverse
@@ -125,9 +129,13 @@ struct FlowArgs {
     const LaneDesc* lanes;   // n_items x 64
     const FlowItem* items;
     const u32* deps;
-    u32* flags;              // n_items completion flags (zero-initialised once per plan)
+    u32* flags;              // n_items completion flags (zero-initialised once per plan); an item's flag
+                             // holds the epoch of the launch that completed it last
     FlowCtl* ctl;
     u32 n_items;
+    u32 epoch;               // this launch's number (host-counted per control block, from 1; never 0)
+    u32 nseq;                // ticket sequences: kFlowSeqs (item t belongs to sequence t % nseq, drawn by
+                             // the waves of XCD t % nseq) or 1 (one global sequence, any residency)
     u32 variant;             // host-side kernel choice: bit 0 draws each wave's next ticket at the start
                              // of its current item (wave items only)
 };
@@ -146,7 +154,8 @@ i64 flow_tile_max_rows(int k, int nw_per_wg, u32 flags);
 int flow_tile_blocks_per_cu(int nw_per_wg, i64 rows, int kmax, u32 flags);
 void launch_step_flow_tile(int nw_per_wg, const FlowArgs& a, i64 n_blocks, i64 rows, int kmax, const StepParams& p,
                            hipStream_t s);
-// True (and cleared) when a wait of a flow launch timed out since the last call (synchronises s).
+// True (and cleared, with every ticket counter) when a wait of a flow launch timed out since the last
+// call (synchronises s).
 bool flow_fault(FlowCtl* ctl, hipStream_t s);
 // Single-generation LDS-tiled kernel over output rows [r0, r1) (all words).
 void launch_step_lds(const u64* src, u64* dst, const Layout& L, i64 r0, i64 r1, u32 flags, hipStream_t s);

@@ -339,11 +339,14 @@ void HipEngine::do_init(const PatternSpec& p) {
     stats_.schedule = split_ ? "split" : (halo_items(L_.R).empty() ? "local" : "full");
     if (dual_) stats_.schedule += sub_overlap_ == 2 ? "+subtiles2ov2" : (sub_overlap_ ? "+subtiles2ov" : "+subtiles2");
     if (flow_) {
-        stats_.schedule += flow_graph_ ? "+flow+graph" : (flow_ov_ ? "+flow+ov" : "+flow");
-        stats_.kernel = flow_tiles() ? strprintf("flow(tile@%d x %dw)", kdepth_, cfg_.tile_waves)
-                                     : strprintf("flow(temporal K<=%d)", hipk::flow_max_depth());
+        stats_.schedule += flow_ov_ ? "+flow+ov" : "+flow";
+        const FlowDev& fd = flow_plan(superstep_depth());
+        stats_.kernel = fd.tile ? strprintf("flow(tile@%d x %dw)", fd.kmax, cfg_.tile_waves)
+                                : strprintf("flow(temporal K<=%d)", hipk::flow_max_depth());
     }
-    stats_.kernel_depth = dual_ ? tdepth_ : (flow_ && !flow_tiles() ? hipk::flow_max_depth() : kdepth_);
+    stats_.kernel_depth = dual_ ? tdepth_ : (flow_ ? *std::max_element(pass_depths(superstep_depth()).begin(),
+                                                                       pass_depths(superstep_depth()).end())
+                                                   : kdepth_);
     stats_.tile_waves = cfg_.tile_waves;
     std::string tn;
     for (const auto& kv : tune_ms_) tn += strprintf("%s%s=%.3fus/gen", tn.empty() ? "" : " ", kv.first.c_str(), kv.second * 1e3);

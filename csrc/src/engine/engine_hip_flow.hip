@@ -61,24 +61,33 @@ bool HipEngine::flow_eligible() {
     // which a single launch cannot do
     if (cfg_.compat || cfg_.profile || cfg_.force_split || kernel_ == "lds" || res_) return false;
     if (cfg_.kernel == "pipe" || cfg_.kernel == "resident") return false;
-    if (flow_tiles()) {  // the tile variant the full-tile plans use must have a flow twin
-        const u32 f = step_flags() | plan(0, kdepth_, 0).tflags;
-        if (!hipk::flow_tile_supported(cfg_.tile_waves, f)) return false;
-    }
     if (self_x() && !L_.aligned()) return false;
     return env_int("GOL_FLOW", 1) != 0;
 }
 
-// Passes of a flow superstep: as few as the flow kernel's deepest depth allows, as equal as
-// possible (20 = 7 + 7 + 6).  GOL_FLOW_KMAX lowers the deepest depth (measurement knob).
-std::vector<int> HipEngine::flow_cut(int k) const {
-    // tile items: passes of the tuned tile depth (any depth runs); waves: the flow kernel's deepest
-    const int deepest = flow_tiles() ? std::max(1, kdepth_) : hipk::flow_max_depth();
-    const int kmax = std::max(1, std::min<int>(deepest, (int)env_int("GOL_FLOW_KMAX", deepest)));
-    const int n = (k + kmax - 1) / kmax;
-    std::vector<int> ps;
-    for (int j = 0; j < n; ++j) ps.push_back(k / n + (j < k % n ? 1 : 0));
-    return ps;
+// Passes of a flow superstep: as few as the items' deepest depth allows, as equal as possible
+// (20 = 7 + 7 + 6).  GOL_FLOW_KMAX lowers the deepest depth (measurement knob).
+std::vector<int> HipEngine::flow_cut(int k) {
+    auto cut = [&](int deepest) {
+        const int kmax = std::max(1, std::min<int>(deepest, (int)env_int("GOL_FLOW_KMAX", deepest)));
+        const int n = (k + kmax - 1) / kmax;
+        std::vector<int> ps;
+        for (int j = 0; j < n; ++j) ps.push_back(k / n + (j < k % n ? 1 : 0));
+        return ps;
+    };
+    // tile items: passes of the tuned tile depth (any depth runs), when their variant has a flow twin;
+    // waves: the flow kernel's deepest
+    if (flow_tiles()) {
+        std::vector<int> ps = cut(std::max(1, kdepth_));
+        if (flow_tile_cut_ok(ps)) return ps;
+    }
+    return cut(hipk::flow_max_depth());
+}
+
+bool HipEngine::flow_tile_cut_ok(const std::vector<int>& ps) {
+    if (!flow_tiles() || ps.empty()) return false;
+    const int kmax = *std::max_element(ps.begin(), ps.end());
+    return hipk::flow_tile_supported(cfg_.tile_waves, step_flags() | plan(0, kmax, ext_after(ps, 0)).tflags);
 }
 
 const HipEngine::FlowDev& HipEngine::flow_plan(int k) {
@@ -97,9 +106,7 @@ const HipEngine::FlowDev& HipEngine::flow_plan(int k) {
     FlowDev fd;
     std::vector<FlowPass> fps;
     const int kmax = *std::max_element(ps.begin(), ps.end());
-    // (tile items need a flow twin of the variant the deepest pass's tile plan uses; a superstep whose
-    // cut lands on another variant runs wave items)
-    if (flow_tiles() && hipk::flow_tile_supported(cfg_.tile_waves, step_flags() | plan(0, kmax, ext_after(ps, 0)).tflags)) {
+    if (flow_tile_cut_ok(ps)) {
         // LDS tile items: every pass uses the tile variant and chunk height of the deepest pass's plan
         // (a shallower pass needs less LDS), capped at the flow variant's capacity (its ticket slot)
         const DevPlan& p0 = plan(0, kmax, ext_after(ps, 0));
@@ -165,12 +172,22 @@ void HipEngine::flow_launch(int k, const u64* src, u64* dst, hipStream_t s) {
     a.flags = fd.flags;
     a.ctl = flow_ctl_;
     a.n_items = fd.n_items;
+    a.epoch = next_flow_epoch();
+    // one ticket sequence per XCD, or one for all while another engine shares the device (its grid may
+    // hold a whole XCD: flow_kernel.hip, deadlock freedom)
+    if (flow_nseq_ <= 0) {
+        int x = 1;
+        if (hipDeviceGetAttribute(&x, hipDeviceAttributeNumberOfXccs, dev_) != hipSuccess || x < 1) x = 1;
+        flow_nseq_ = std::min(x, hipk::kFlowSeqs);
+    }
+    a.nseq = engines_on_device(dev_, this, 0).second > 1 ? 1u : (u32)flow_nseq_;
     hipk::StepParams sp{L_.pitch, (i32)L_.h, (i32)L_.nw, L_.R, step_flags() | fd.tflags};
     if (fd.tile)
         hipk::launch_step_flow_tile(cfg_.tile_waves, a, fd.blocks, fd.rows, fd.kmax, sp, s);
     else
         hipk::launch_step_flow(a, fd.blocks, sp, s);
     HIP_CHECK(hipGetLastError());
+    flow_epoch_ = a.epoch;
     flow_used_ = true;
 }
 
@@ -178,7 +195,8 @@ void HipEngine::flow_launch(int k, const u64* src, u64* dst, hipStream_t s) {
 // result lands in buf[cur ^ (passes & 1)].
 //   "flow":    the exchange on the compute stream, then the launch (its first pass reads the ghost rows).
 //   "flow+ov": the exchange on the comm stream (after the previous superstep's launch, ev_ready_),
-//              followed by a device flag (hipStreamWriteValue32); the launch goes to the compute stream
+//              followed by a device flag (hipStreamWriteValue32 of the launch's epoch); the launch goes
+//              to the compute stream
 //              at once, with no cross-queue event wait.  Its plan (build_flow_plan mark_exch) runs the
 //              items from the middle of the tile outwards and makes the first pass's items that read
 //              ghost cells wait for the flag, so the interior hides the exchange and only the bands next
@@ -193,7 +211,7 @@ void HipEngine::flow_superstep(int k) {
         prepare(k);
         HIP_CHECK(hipStreamWaitEvent(s_comm_, ev_ready_, 0));
         exchange_device(k, items, cur_, s_comm_);
-        HIP_CHECK(hipStreamWriteValue32(s_comm_, &flow_ctl_->exch, 1u, 0));
+        HIP_CHECK(hipStreamWriteValue32(s_comm_, &flow_ctl_->exch, next_flow_epoch(), 0));
         flow_launch(k, buf_[cur_], buf_[cur_ ^ 1], s_comp_);
         if (ps.size() & 1) cur_ ^= 1;
         HIP_CHECK(hipEventRecord(ev_ready_, s_comp_));  // the next exchange reads this launch's edge rows

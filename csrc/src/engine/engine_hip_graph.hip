@@ -12,7 +12,7 @@ bool HipEngine::graph_shape(int& k, int& m) {
     // 12.8 us/gen over 20 generations, 13.0 vs 10.4 over 256; profiles/short_run_probe.txt).
     // A single-stream graph per half and superstep is available (GOL_SUBTILE_GRAPHS=1), also slower.
     if (dual_) return false;
-    if (flow_ && !flow_graph_) return false;  // flow supersteps launch eagerly unless "flow+graph" won
+    if (flow_) return false;  // a flow superstep is one launch (its epoch is an argument: never replayed)
     k = cfg_.compat ? 1 : superstep_depth();
     m = cfg_.graph_supersteps;
     if (m <= 0) m = k >= 8 ? 16 : 32;

@@ -162,8 +162,8 @@ void HipEngine::choose_schedule() {
         if (ok > 0) {
             cands.push_back("flow");
             if (ov_ok > 0) cands.push_back("flow+ov");
-            if (cfg_.graph && (!nbrs || (device_transport_ && t_->graph_capturable() && cfg_.graph_rccl != 0)))
-                cands.push_back("flow+graph");
+            // (no graphed flow candidate: a superstep is one launch whose epoch is an argument, and a
+            // graph replay costs more than a direct launch)
         }
         if (cfg_.sched == "flow" || cfg_.sched == "flow+ov") {  // GOL_SCHEDULE=flow[+ov]: the only candidate
             if (ok <= 0) throw Error("GOL_SCHEDULE=flow: no device memory for the flow timing scratch");
@@ -237,7 +237,6 @@ void HipEngine::choose_schedule() {
     free_flow_scratch();
     sched_pick_ = pick;
     flow_ = pick.rfind("flow", 0) == 0;
-    flow_graph_ = pick == "flow+graph";
     flow_ov_ = pick == "flow+ov";
     // flow+ov runs on the CU-restricted compute stream from here on (every later launch of the engine
     // is ordered on it)
@@ -281,13 +280,13 @@ void HipEngine::time_schedule(const std::string& c, int k, int reps, bool eager)
         sub_graphs_on_ = sg;
         return;
     }
-    // One-tile supersteps as the runs replay them (graphs: "local" always, "full+graph" and
-    // "flow+graph" candidates): `reps` supersteps captured once per candidate (round 0's warm-up call,
+    // One-tile supersteps as the runs replay them (graphs: "local" always, the "full+graph"
+    // candidate): `reps` supersteps captured once per candidate (round 0's warm-up call,
     // after one eager superstep that loads every kernel variant), one replay per call.
-    const bool graphed = !eager && (c == "full+graph" || c == "flow+graph" ||
+    const bool graphed = !eager && (c == "full+graph" ||
                                     (c == "local" && cfg_.graph && !cfg_.profile && !cfg_.compat && graph_ok_));
     if (graphed) {
-        const std::string base = c == "local" ? "local" : (c == "flow+graph" ? "flow" : "full");
+        const std::string base = c == "local" ? "local" : "full";
         SchedGraph& sg = sched_graphs_[c];
         if (sg.exec && sg.reps != reps) {
             HIP_CHECK(hipStreamSynchronize(s_comp_));
@@ -346,7 +345,7 @@ void HipEngine::time_schedule(const std::string& c, int k, int reps, bool eager)
                 prepare(k);
                 HIP_CHECK(hipStreamWaitEvent(s_comm_, ev_ready_, 0));
                 exchange_device(k, items, cur_, s_comm_);
-                HIP_CHECK(hipStreamWriteValue32(s_comm_, &flow_ctl_->exch, 1u, 0));
+                HIP_CHECK(hipStreamWriteValue32(s_comm_, &flow_ctl_->exch, next_flow_epoch(), 0));
                 flow_launch(k, flow_scratch_, buf_[cur_ ^ 1], s_comp_);
                 HIP_CHECK(hipEventRecord(ev_ready_, s_comp_));
                 continue;
@@ -541,8 +540,10 @@ void HipEngine::autotune_kernel() {
     pipe_used_ = false;  // (the candidates ran on scratch; faults were checked above)
     // The resident kernel (small boards without neighbours): one launch per run, halos exchanged
     // between tiles inside the kernel every kin generations.  Timed on launches of the hinted run's
-    // length (at most 256 generations) against the best pass kernel above.
-    if (resident_eligible() && !split_used()) {
+    // length (at most 256 generations) against the best pass kernel above.  (GOL_SCHEDULE=flow asks
+    // for flow supersteps of the pass kernels: no resident candidate.)
+    const bool flow_forced = cfg_.sched == "flow" || cfg_.sched == "flow+ov";
+    if (resident_eligible() && !split_used() && (!flow_forced || cfg_.kernel == "resident")) {
         const int G = std::min(res_run_depth(), 256);
         float rbest = 1e30f;
         int rk = 0;

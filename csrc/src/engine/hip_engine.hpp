@@ -262,7 +262,8 @@ class HipEngine : public Engine {
     // generation).  With neighbours every rank keeps R: the exchanges must match.
     int superstep_depth() const override {
         if (res_) return std::max(L_.R, res_run_depth());
-        if (flow_) return flow_superstep_depth();
+        // (flow_superstep_depth builds and caches tile plans: logically const)
+        if (flow_) return const_cast<HipEngine*>(this)->flow_superstep_depth();
         if (dual_ || !tuned_ || cfg_.compat || kdepth_ <= 0 || kdepth_ >= L_.R || !halo_items(L_.R).empty())
             return L_.R;
         return (L_.R / kdepth_) * kdepth_;
@@ -506,17 +507,20 @@ class HipEngine : public Engine {
     };
     bool flow_eligible();
     // Flow items are LDS tiles when the tuned full-tile kernel is the tile kernel and a flow tile variant
-    // exists for its workgroup size and variant bits; otherwise step_temporal waves.
+    // exists for its workgroup size and the variant bits of the cut's deepest pass (flow_cut,
+    // flow_tile_cut_ok); otherwise step_temporal waves.
     bool flow_tiles() const { return kern_[0] == "tile"; }
+    bool flow_tile_cut_ok(const std::vector<int>& ps);
     // Generations per flow superstep: the halo depth R with neighbours (the exchanges must match); on a
     // rank without neighbours the hinted run length (at least R, at most 1024), so a whole run is one
     // launch of passes that flow into each other (8192^2 x 1000: 32 tile passes, no kernel boundary).
     // (Wave items keep R: a superstep's plan holds ~3000 items of 1 KiB of lane descriptors per pass.)
-    int flow_superstep_depth() const {
+    int flow_superstep_depth() {
         if (!flow_tiles() || !halo_items(L_.R).empty() || cfg_.run_hint == 0) return L_.R;
-        return (int)std::max<u64>((u64)L_.R, std::min<u64>(cfg_.run_hint, 1024));
+        const int d = (int)std::max<u64>((u64)L_.R, std::min<u64>(cfg_.run_hint, 1024));
+        return flow_tile_cut_ok(flow_cut(d)) ? d : L_.R;
     }
-    std::vector<int> flow_cut(int k) const;
+    std::vector<int> flow_cut(int k);
     const FlowDev& flow_plan(int k);
     void flow_launch(int k, const u64* src, u64* dst, hipStream_t s);
     void flow_superstep(int k);
@@ -597,7 +601,7 @@ class HipEngine : public Engine {
     bool graph_ok_ = true;
     bool graph_rccl_on_ = false;  // one-tile supersteps with an RCCL exchange are captured (choose_schedule)
     bool sub_graphs_on_ = false;  // sub-tile passes replay per-half graphs (choose_schedule)
-    // timing graphs of the graphed schedule candidates ("local", "full+graph", "flow+graph"), by name
+    // timing graphs of the graphed schedule candidates ("local", "full+graph"), by name
     struct SchedGraph {
         hipGraphExec_t exec = nullptr;
         int reps = 0;
@@ -612,7 +616,6 @@ class HipEngine : public Engine {
         sched_graphs_.clear();
     }
     std::string sched_pick_;     // the schedule candidate choose_schedule picked (phase_probe times it)
-    bool flow_graph_ = false;    // flow supersteps replay captured graphs ("flow+graph")
     // flow supersteps with neighbours ("flow+ov"): the exchange runs on the comm stream while the
     // launch's interior items run; the items reading ghost cells wait for its device flag
     bool flow_ov_ = false;
@@ -674,7 +677,10 @@ class HipEngine : public Engine {
     std::vector<u64*> dstage_s_, dstage_r_, hstage_s_, hstage_r_;
     bool flow_ = false;                     // supersteps run as one step_flow launch (schedule "+flow")
     bool flow_used_ = false;                // a flow launch ran (fault check at readouts)
-    hipk::FlowCtl* flow_ctl_ = nullptr;     // its ticket / epoch / fault words
+    hipk::FlowCtl* flow_ctl_ = nullptr;     // its ticket / fault / exchange words
+    u32 flow_epoch_ = 0;                    // flow launches made on flow_ctl_ (FlowArgs::epoch of the last)
+    u32 next_flow_epoch() const { return flow_epoch_ + 1u == 0u ? 1u : flow_epoch_ + 1u; }
+    int flow_nseq_ = 0;                     // the device's XCDs (ticket sequences; 1 when the device is shared)
     std::map<int, FlowDev> flow_plans_;     // by superstep depth x 2 + exchange-overlapped
     bool res_ = false;  // supersteps run the resident kernel
     int res_kin_ = 0;   // its generations per in-kernel halo exchange

@@ -13,31 +13,42 @@
 //    global ticket order: every item of pass j comes before any item of pass j + 1, and inside a pass
 //    the items run down the board in row bands (with the torus wrap, pass j starts one band further
 //    down than pass j - 1, so its first items read only the rows pass j - 1 finished first).
-//  * A persistent grid of waves (one full round of resident slots) takes tickets from a device
-//    counter; a wave that draws item t waits for the items t depends on (host-computed: the items of
+//  * A persistent grid of waves (one full round of resident slots) takes tickets from device
+//    counters; a wave that draws item t waits for the items t depends on (host-computed: the items of
 //    pass j - 1 that WRITE rows it reads, and those that READ rows it overwrites — two buffers
 //    alternate, so pass j + 1 writes the buffer pass j reads), streams the item with the
 //    step_temporal wave (wave_runner.hpp), and publishes its completion flag.  So an early-finishing
 //    wave starts on pass j + 1 as soon as its neighbourhood of pass j is done, instead of idling at a
 //    kernel boundary; only the superstep's end drains.
-//  * Deadlock freedom (no residency assumption, no cooperative launch): tickets are issued in a total
-//    order and an item depends only on items with SMALLER tickets.  A ticket is only ever drawn by a
-//    running wave, which then works on it without waiting for anything but its dependencies.  The
-//    unfinished item with the smallest ticket therefore has all its dependencies finished, so it
-//    progresses; by induction every item finishes.  Every wait is also bounded (2 s of s_memrealtime),
-//    after which the wave records a fault (FlowCtl::fault, read by the engine at every board readout)
-//    and goes on, so a bug cannot hang the GPU.
+//  * Ticket sequences.  One device-wide counter costs ~12 ns per draw, serialised (same-address
+//    atomics: tools/ticket_probe.hip, profiles/ticket_probe.txt), and a superstep draws ~15000 tickets
+//    (items plus each wave's final draw): ~180 us, the whole budget.  So item t belongs to sequence
+//    t % nseq, and sequence s is drawn only by the waves running on XCD s (HW_REG_XCC_ID; nseq = the
+//    device's XCDs): eight counters in parallel, ~2.5 ns per draw device-wide.
+//  * Deadlock freedom (no residency assumption, no cooperative launch): an item depends only on items
+//    with SMALLER tickets, and each sequence is drawn in increasing order by running waves, which work
+//    on a drawn item without waiting for anything but its dependencies.  Let t be the smallest
+//    unfinished item and s its sequence; its dependencies are finished.  If t is drawn, its wave runs it
+//    (with PF, the item the wave is still on is an earlier one of sequence s: finished).  If not, every
+//    drawn item of sequence s is smaller, hence finished, so the waves of XCD s are free and the next
+//    draw on s is t: XCD s has a wave of the launch (the hardware deals workgroups to every XCD, none
+//    exits before its sequence is drawn out, and nothing else holds its CUs for ever).  By induction
+//    every item finishes.  Engines sharing a device (thread ranks) use one sequence (nseq = 1): then the
+//    argument needs no XCD at all (another engine's grid may hold an XCD).  Every wait is also bounded
+//    (2 s of s_memrealtime), after which the wave records a fault (FlowCtl::fault, read by the engine
+//    at every board readout) and goes on, so a bug cannot hang the GPU.
 //  * Cross-CU visibility (MI355X_MICROARCH.md, "inter-workgroup visibility", valid hand-off forms):
 //    every board-row load and store of an item is an agent-scope relaxed atomic, `global_load/store
 //    ... sc1` (write-through stores, loads that bypass the CU's L1); a wave's stores are complete at
 //    its `s_waitcnt vmcnt(0)`, after which ONE lane stores the item's flag (`sc1`); a consumer polls
-//    flags with `sc1` loads and issues its row loads only after every flag matched.  Flags hold an
-//    epoch (FlowCtl::epoch + 1 of the running launch), so they are never reset between launches: the
-//    last wave to leave a launch resets the ticket counters and advances the epoch, and the stream
-//    order puts that before the next launch.  (No scalar-cache stores or atomics anywhere: every
-//    store and atomic here is a vector memory instruction.)
-//  * Kernel boundaries still order supersteps (exchanges, graph replays and readouts see finished
-//    boards), and the launch is replayable from a captured graph: nothing in its arguments changes.
+//    flags with `sc1` loads and issues its row loads only after every flag matched.  Flags hold the
+//    launch's epoch (host-counted, FlowArgs::epoch), so they are never reset between launches, and the
+//    ticket counters are double-buffered by epoch parity: launch e zeroes the ones launch e + 1 draws
+//    from (no completion count, no last-wave-out reset).  (No scalar-cache stores or atomics anywhere:
+//    every store and atomic here is a vector memory instruction.)
+//  * Kernel boundaries still order supersteps (exchanges and readouts see finished boards).  The epoch
+//    is a launch argument, so a flow launch is not replayed from a captured graph (it is one launch per
+//    superstep: a graph replay costs more than a direct launch, MI355X_MICROARCH.md graph-replay-floor).
 //
 // Reference: the generation loop gol-main.c:93-116 and its per-generation launch + device sync,
 // gol-with-cuda.cu:264-284.
@@ -72,12 +83,15 @@ __device__ __forceinline__ void flow_wait(const FlowArgs& a, u32 dep_off, u32 nd
             const u32 v = act ? __hip_atomic_load(&a.flags[dep], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : target;
             const bool ready = (int)(v - target) >= 0;
             if (__builtin_amdgcn_ballot_w64(!ready) == 0) break;
-            if (spin == 0) t0 = __builtin_amdgcn_s_memrealtime();
-            const u32 fault = __builtin_amdgcn_readfirstlane(
-                __hip_atomic_load(&a.ctl->fault, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-            if (__builtin_amdgcn_s_memrealtime() - t0 > kFlowWaitTicks || fault != 0) {
-                __hip_atomic_store(&a.ctl->fault, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // (all lanes, one word)
-                break;
+            if (spin == 0) {
+                t0 = __builtin_amdgcn_s_memrealtime();
+            } else if ((spin & 15) == 0) {  // (the time limit, or a fault elsewhere: every 16th poll)
+                const u32 fault = __builtin_amdgcn_readfirstlane(
+                    __hip_atomic_load(&a.ctl->fault, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+                if (__builtin_amdgcn_s_memrealtime() - t0 > kFlowWaitTicks || fault != 0) {
+                    __hip_atomic_store(&a.ctl->fault, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // (all lanes, one word)
+                    break;
+                }
             }
             __builtin_amdgcn_s_sleep(4);
         }
@@ -86,15 +100,15 @@ __device__ __forceinline__ void flow_wait(const FlowArgs& a, u32 dep_off, u32 nd
 }
 
 // Exchange-overlapped launches: an item that reads ghost cells waits for the comm stream's flag
-// (hipStreamWriteValue32 after the RCCL group), then acquires at agent scope before its loads.  The
-// flag is a single word polled with system-scope loads (the write comes from another queue's packet
-// processor, not from a wave).
+// (hipStreamWriteValue32 of the launch's epoch after the RCCL group), then acquires at agent scope
+// before its loads.  The flag is a single word polled with system-scope loads (the write comes from
+// another queue's packet processor, not from a wave).
 __device__ __forceinline__ void flow_wait_exch(const FlowArgs& a) {
     u64 t0 = 0;
     for (int spin = 0;; ++spin) {
         const u32 v = __builtin_amdgcn_readfirstlane(
             __hip_atomic_load(&a.ctl->exch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
-        if (v != 0) break;
+        if ((int)(v - a.epoch) >= 0) break;
         if (spin == 0) t0 = __builtin_amdgcn_s_memrealtime();
         const u32 fault = __builtin_amdgcn_readfirstlane(
             __hip_atomic_load(&a.ctl->fault, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
@@ -106,6 +120,28 @@ __device__ __forceinline__ void flow_wait_exch(const FlowArgs& a) {
     }
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+// The ticket sequence of the calling wave (kFlowSeqs = one per XCD, or one for all) and its counter for
+// this launch; block 0's first wave zeroes the counters of the next launch (double-buffered by epoch).
+__device__ __forceinline__ u32* flow_sequence(const FlowArgs& a, u32& seq, int lane) {
+    seq = 0;
+    if (a.nseq > 1) {
+        u32 xcc = 0;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID, 0, 4)" : "=s"(xcc));
+        seq = xcc % a.nseq;
+    }
+    if (blockIdx.x == 0 && threadIdx.x < 64)  // (wave 0 of block 0: lanes 0-7 one counter each, the rest repeat them)
+        __hip_atomic_store(&a.ctl->next[(a.epoch + 1u) & 1u][lane & (kFlowSeqs - 1)][0], 0u, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+    return &a.ctl->next[a.epoch & 1u][seq][0];
+}
+
+// Draw the next item of the wave's sequence: item seq + nseq x (draw number); >= n_items when the
+// sequence is drawn out.  An all-lane atomic adding 1 from lane 0 and 0 from the others.
+__device__ __forceinline__ u32 flow_draw(const FlowArgs& a, u32* ctr, u32 seq, int lane) {
+    const u32 i = __hip_atomic_fetch_add(ctr, lane == 0 ? 1u : 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return __builtin_amdgcn_readfirstlane(i) * a.nseq + seq;
 }
 
 template <int K, int ROWS>
@@ -129,20 +165,19 @@ __global__ __launch_bounds__(64 * kWavesPerBlock) __attribute__((amdgpu_waves_pe
                                                                                                     StepParams p) {
     const int lane = threadIdx.x & 63;
     const i64 wave = (i64)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
-    const u32 n_waves = gridDim.x * (u32)kWavesPerBlock;
-    const u32 target = __builtin_amdgcn_readfirstlane(
-                           __hip_atomic_load(&a.ctl->epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) + 1u;
+    const u32 target = a.epoch;
     // (No lane-conditional code in this loop: a `lane == 0` branch around the ticket draw or the flag
     // store let the compiler thread that condition across the loop's back edge, and lanes 1-63 went on
     // re-running ticket 0 — the first version hung.  The draw is an all-lane atomic adding 1 from lane
     // 0 and 0 from the others; the flag is stored by every lane to the same word.)
-    u32 t = __builtin_amdgcn_readfirstlane(
-        __hip_atomic_fetch_add(&a.ctl->next, lane == 0 ? 1u : 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    u32 seq = 0;
+    u32* ctr = flow_sequence(a, seq, lane);
+    u32 t = flow_draw(a, ctr, seq, lane);
     for (;;) {
         if (t >= a.n_items) break;
         u32 t_next = 0;  // (PF: a per-lane register until the item's end, so no wait is forced here)
         if constexpr (PF)
-            t_next = __hip_atomic_fetch_add(&a.ctl->next, lane == 0 ? 1u : 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            t_next = __hip_atomic_fetch_add(ctr, lane == 0 ? 1u : 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         // the item's fields as wave-uniform values (they steer every branch below)
         const FlowItem* ip = a.items + t;
         const u32 depth = __builtin_amdgcn_readfirstlane(ip->depth);
@@ -172,22 +207,9 @@ __global__ __launch_bounds__(64 * kWavesPerBlock) __attribute__((amdgpu_waves_pe
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __hip_atomic_store(&a.flags[t], target, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if constexpr (PF)
-            t = __builtin_amdgcn_readfirstlane(t_next);
+            t = __builtin_amdgcn_readfirstlane(t_next) * a.nseq + seq;
         else
-            t = __builtin_amdgcn_readfirstlane(
-                __hip_atomic_fetch_add(&a.ctl->next, lane == 0 ? 1u : 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-    }
-    // The last wave out resets the tickets and advances the epoch for the next launch (every other
-    // wave has drawn its last ticket before its `done` increment).
-    {
-        const u32 left = __builtin_amdgcn_readfirstlane(
-            __hip_atomic_fetch_add(&a.ctl->done, lane == 0 ? 1u : 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-        if (left == n_waves - 1) {
-            __hip_atomic_store(&a.ctl->next, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(&a.ctl->done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(&a.ctl->exch, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(&a.ctl->epoch, target, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
+            t = flow_draw(a, ctr, seq, lane);
     }
 }
 
@@ -202,13 +224,12 @@ __global__ __launch_bounds__(64 * NW) void step_flow_tile(FlowArgs a, StepParams
     const int lane = threadIdx.x & 63;
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     u32* s_ticket = tile_lds + ticket_slot;
-    const u32 n_groups = gridDim.x;
-    const u32 target = __builtin_amdgcn_readfirstlane(
-                           __hip_atomic_load(&a.ctl->epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) + 1u;
+    const u32 target = a.epoch;
+    u32 seq = 0;
+    u32* ctr = flow_sequence(a, seq, lane);
     for (;;) {
         if (wv == 0) {
-            const u32 t = __builtin_amdgcn_readfirstlane(
-                __hip_atomic_fetch_add(&a.ctl->next, lane == 0 ? 1u : 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+            const u32 t = flow_draw(a, ctr, seq, lane);
             if (t < a.n_items) {
                 const FlowItem* ip = a.items + t;
                 flow_wait(a, __builtin_amdgcn_readfirstlane(ip->dep_off), __builtin_amdgcn_readfirstlane(ip->ndeps),
@@ -238,16 +259,6 @@ __global__ __launch_bounds__(64 * NW) void step_flow_tile(FlowArgs a, StepParams
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's output rows have left it
         __syncthreads();                                   // ... and every other wave's
         if (wv == 0) __hip_atomic_store(&a.flags[t], target, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    if (wv == 0) {
-        const u32 left = __builtin_amdgcn_readfirstlane(
-            __hip_atomic_fetch_add(&a.ctl->done, lane == 0 ? 1u : 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-        if (left == n_groups - 1) {
-            __hip_atomic_store(&a.ctl->next, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(&a.ctl->done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(&a.ctl->exch, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(&a.ctl->epoch, target, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
     }
 }
 
@@ -368,14 +379,15 @@ void launch_step_flow_tile(int nw_per_wg, const FlowArgs& a, i64 n_blocks, i64 r
 }
 
 bool flow_fault(FlowCtl* ctl, hipStream_t s) {
-    FlowCtl v{};
-    if (hipMemcpyAsync(&v, ctl, sizeof(v), hipMemcpyDeviceToHost, s) != hipSuccess || hipStreamSynchronize(s) != hipSuccess)
+    u32 v = 0;
+    if (hipMemcpyAsync(&v, &ctl->fault, sizeof(v), hipMemcpyDeviceToHost, s) != hipSuccess ||
+        hipStreamSynchronize(s) != hipSuccess)
         throw Error("flow_fault: cannot read the control block");
-    if (v.fault == 0) return false;
-    // clear it, and the ticket / exchange state of the faulted launch (its waves all left)
-    FlowCtl z{};
-    z.epoch = v.epoch;
-    if (hipMemcpyAsync(ctl, &z, sizeof(z), hipMemcpyHostToDevice, s) != hipSuccess || hipStreamSynchronize(s) != hipSuccess)
+    if (v == 0) return false;
+    // clear it, and the ticket counters of the faulted launch (its waves all left); the exchange flag
+    // holds an epoch and stays
+    if (hipMemsetAsync(ctl->next, 0, sizeof(ctl->next), s) != hipSuccess ||
+        hipMemsetAsync(&ctl->fault, 0, sizeof(u32), s) != hipSuccess || hipStreamSynchronize(s) != hipSuccess)
         throw Error("flow_fault: cannot reset the control block");
     return true;
 }

@@ -123,17 +123,23 @@ int main(int argc, char** argv) {
     fa.items = upload(fp.items);
     fa.deps = upload(fp.deps);
     fa.flags = upload(std::vector<u32>(fp.items.size(), 0u));
-    fa.ctl = upload(std::vector<hipk::FlowCtl>(1, hipk::FlowCtl{0, 0, 0, 0}));
+    fa.ctl = upload(std::vector<hipk::FlowCtl>(1, hipk::FlowCtl{}));
     fa.n_items = (u32)fp.items.size();
+    // ticket sequences: KB_FLOW_SEQS (default: the device's XCDs)
+    int xccs = 1;
+    CK(hipDeviceGetAttribute(&xccs, hipDeviceAttributeNumberOfXccs, 0));
+    fa.nseq = (u32)std::max(1, std::min(getenv("KB_FLOW_SEQS") ? atoi(getenv("KB_FLOW_SEQS")) : xccs, hipk::kFlowSeqs));
     fa.variant = getenv("KB_FLOW_PF") ? (u32)atoi(getenv("KB_FLOW_PF")) : 0u;  // 1: ticket prefetch
     double avg_deps = fp.items.empty() ? 0 : (double)fp.deps.size() / (double)fp.items.size();
     printf("flow plan: %zu items, %u..%zu deps (max %u, avg %.1f), rows/pass:", fp.items.size(), 0u, fp.deps.size(),
            fp.max_deps, avg_deps);
     for (const FlowPass& p : fps) printf(" %lld", (long long)p.rows);
-    printf(", grid %d blocks/CU (%lld waves), host build %.1f ms\n", bpc, (long long)resident, build_ms);
+    printf(", grid %d blocks/CU (%lld waves), %u ticket sequences, host build %.1f ms\n", bpc, (long long)resident,
+           fa.nseq, build_ms);
     auto run_flow = [&](u64*& x, u64*& y) {
         fa.a = x;
         fa.b = y;
+        ++fa.epoch;
         hipk::launch_step_flow(fa, (i64)bpc * cus, sp, 0);
         if (cut.size() & 1) std::swap(x, y);
     };
