@@ -60,9 +60,15 @@ struct PlanStats {
 // With `fold` (the tile kernel's STEP_TILE_FOLD) segments are packed into 32-lane tiles of <= 30
 // output words, and each tile's 64 lanes are its 32 lanes twice: the kernel folds the tile's rows so
 // lanes 0-31 stream the top half and lanes 32-63 (bottom up) the bottom half.
+// With `age_weights` (C > 1 values; a single region, not folded) the plan's row bands get heights
+// proportional to the weight of the dispatch class their full-width segments land in: workgroup b of
+// nwg is in class b * C / nwg.  On MI355X the co-resident waves of a SIMD are issued by age, and in a
+// one-round plan of 3 workgroups per CU the first-dispatched third of the grid finished a pass in ~half
+// the time of the last third (tools/stamp_probe.hip, profiles/stamp_probe.txt): weights (w0 > w1 > w2)
+// give the older waves taller segments so that a SIMD's waves finish together.
 std::vector<LaneDesc> build_plan(const std::vector<Region>& regions, i64 nw, i64 h, i64 rows_per_chunk, int k,
                                  bool xwrap, PlanStats* stats = nullptr, int wg_waves = kWavesPerBlock,
-                                 int xcds = 8, bool fold = false);
+                                 int xcds = 8, bool fold = false, const std::vector<double>* age_weights = nullptr);
 
 // Bounds check of a plan before it is uploaded (a bad plan would fault the GPU): every lane's word
 // column lies in [-1, nw]; without y-wrap its input rows [row0-k, row0+nrows+k) lie in the

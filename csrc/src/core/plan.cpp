@@ -89,8 +89,9 @@ namespace {
 
 // Cut the regions into segments of <= rows_per_chunk rows x <= 62 words and pack them into waves:
 // full-width segments get a wave each; narrow ones (same height) are packed first-fit-decreasing.
+// `bands` (one region only): its row bands' heights, top to bottom, instead of equal ones.
 std::vector<std::vector<Item>> pack_waves(const std::vector<Region>& regions, i64 nw, i64 h, i64 rows_per_chunk,
-                                          bool fold) {
+                                          bool fold, const std::vector<i64>* bands = nullptr) {
     if (rows_per_chunk < 1) rows_per_chunk = 1;
     const int lw = pack_lanes(fold), sw = lw - 2;
     std::map<i64, std::vector<Item>> by_rows;
@@ -100,11 +101,11 @@ std::vector<std::vector<Item>> pack_waves(const std::vector<Region>& regions, i6
         // rows may extend into the ghost rows and columns into the ghost words (multi-pass
         // supersteps: at most the 64-row halo and the one-word column halo)
         if (rg.r0 < -128 || rg.r1 > h + 128 || rg.c0 < -1 || rg.c1 > nw + 1) throw Error("plan region outside the tile");
-        i64 nch = ceil_div(rows, rows_per_chunk);
+        i64 nch = bands ? (i64)bands->size() : ceil_div(rows, rows_per_chunk);
         i64 base = rows / nch, extra = rows % nch;
         i64 r = rg.r0;
         for (i64 ch = 0; ch < nch; ++ch) {
-            i64 nr = base + (ch < extra ? 1 : 0);
+            i64 nr = bands ? (*bands)[(size_t)ch] : base + (ch < extra ? 1 : 0);
             for (i64 c = rg.c0; c < rg.c1; c += sw) by_rows[nr].push_back({r, nr, c, std::min<i64>(sw, rg.c1 - c)});
             r += nr;
         }
@@ -147,9 +148,63 @@ i64 plan_waves(const std::vector<Region>& regions, i64 nw, i64 h, i64 rows_per_c
     return round_up(std::max<i64>(1, (i64)pack_waves(regions, nw, h, rows_per_chunk, fold).size()), kWavesPerBlock);
 }
 
+namespace {
+
+// The permutation of whole workgroups that gives XCD x (workgroup b runs on XCD b % xcds) a
+// contiguous stretch of the plan order: order[s] = the launch index of plan-order workgroup s.
+std::vector<i64> xcd_order(i64 nwg, int xcds) {
+    std::vector<i64> order((size_t)nwg);
+    for (i64 b = 0; b < nwg; ++b) order[(size_t)b] = b;
+    if (xcds > 1)
+        std::stable_sort(order.begin(), order.end(), [xcds](i64 a, i64 b) {
+            return a % xcds != b % xcds ? a % xcds < b % xcds : a / xcds < b / xcds;
+        });
+    return order;
+}
+
+// Row-band heights of a single-region plan weighted by dispatch class (build_plan age_weights): the
+// band count of the equal-height plan, band i's class from the launch index of its first full-width
+// segment, heights proportional to the class weights (>= 1 row, summing to the region's rows).
+std::vector<i64> age_bands(const Region& rg, i64 rows_per_chunk, int wg_waves, int xcds, const std::vector<double>& w) {
+    const i64 rows = rg.r1 - rg.r0, words = rg.c1 - rg.c0;
+    const i64 nb = ceil_div(rows, std::max<i64>(1, rows_per_chunk));
+    const i64 full = words / kSegWords, narrow = words % kSegWords ? words % kSegWords + 2 : 0;
+    if (nb < 2 || full < 1) return {};
+    const i64 per_wave = narrow ? kWaveLanes / narrow : 1;  // narrow segments per packed wave
+    const i64 nwaves = round_up(nb * full + (narrow ? ceil_div(nb, per_wave) : 0), kWavesPerBlock);
+    const i64 nwg = nwaves / std::max(1, wg_waves);
+    const std::vector<i64> order = xcd_order(nwg, xcds);
+    const i64 C = (i64)w.size();
+    std::vector<double> wt((size_t)nb);
+    double sum = 0;
+    for (i64 i = 0; i < nb; ++i) {
+        const i64 s = std::min(nwg - 1, i * full / std::max(1, wg_waves));
+        const i64 cls = std::min(C - 1, order[(size_t)s] * C / nwg);
+        wt[(size_t)i] = std::max(0.05, w[(size_t)cls]);
+        sum += wt[(size_t)i];
+    }
+    std::vector<i64> bands((size_t)nb);
+    i64 used = 0;
+    double acc = 0;
+    for (i64 i = 0; i < nb; ++i) {  // cumulative rounding: every band >= 1 row, the total exact
+        acc += wt[(size_t)i] * (double)rows / sum;
+        const i64 end = std::min(rows - (nb - 1 - i), std::max(used + 1, (i64)(acc + 0.5)));
+        bands[(size_t)i] = end - used;
+        used = end;
+    }
+    bands.back() += rows - used;
+    return bands;
+}
+
+}  // namespace
+
 std::vector<LaneDesc> build_plan(const std::vector<Region>& regions, i64 nw, i64 h, i64 rows_per_chunk, int k,
-                                 bool xwrap, PlanStats* stats, int wg_waves, int xcds, bool fold) {
-    std::vector<std::vector<Item>> packed = pack_waves(regions, nw, h, rows_per_chunk, fold);
+                                 bool xwrap, PlanStats* stats, int wg_waves, int xcds, bool fold,
+                                 const std::vector<double>* age_weights) {
+    std::vector<i64> bands;
+    if (age_weights && age_weights->size() > 1 && regions.size() == 1 && !fold)
+        bands = age_bands(regions[0], rows_per_chunk, wg_waves < 1 ? 1 : wg_waves, xcds, *age_weights);
+    std::vector<std::vector<Item>> packed = pack_waves(regions, nw, h, rows_per_chunk, fold, bands.empty() ? nullptr : &bands);
     const int lw = pack_lanes(fold);
     i64 nwaves = round_up(std::max<i64>(1, (i64)packed.size()), kWavesPerBlock);
     // XCD-aware order.  The full-width segments are sorted (narrow, packed waves stay last), then
@@ -170,12 +225,7 @@ std::vector<LaneDesc> build_plan(const std::vector<Region>& regions, i64 nw, i64
     std::vector<std::vector<Item>> waves((size_t)nwaves);
     if (wg_waves < 1 || nwaves % wg_waves) wg_waves = 1;
     const i64 nwg = nwaves / wg_waves;
-    std::vector<i64> order((size_t)nwg);
-    for (i64 b = 0; b < nwg; ++b) order[(size_t)b] = b;
-    if (xcds > 1)
-        std::stable_sort(order.begin(), order.end(), [xcds](i64 a, i64 b) {
-            return a % xcds != b % xcds ? a % xcds < b % xcds : a / xcds < b / xcds;
-        });
+    const std::vector<i64> order = xcd_order(nwg, xcds);
     for (i64 s = 0; s < nwg; ++s)
         for (int i = 0; i < wg_waves; ++i) {
             const size_t src = (size_t)(s * wg_waves + i);

@@ -559,6 +559,50 @@ static void test_plan_rounds() {
     }
 }
 
+// Age-weighted plans (build_plan age_weights): the plan still covers every output word exactly once,
+// fits the same waves, and the first-dispatched third of the grid gets the tallest segments.
+static void test_plan_age_weights() {
+    const std::vector<double> w = {1.6, 1.15, 0.75};
+    for (const auto& c : std::vector<std::pair<i64, i64>>{{32768, 512}, {16384, 256}, {8192, 512}, {4000, 100}}) {
+        const i64 h = c.first, nw = c.second;
+        std::vector<Region> rg = {{0, h, 0, nw}};
+        const i64 resident = 3 * 4 * 256;
+        const i64 rows = balanced_rows_per_chunk(rg, nw, h, 8, resident, 16, true);
+        PlanStats s0, s1;
+        const std::vector<LaneDesc> eq = build_plan(rg, nw, h, rows, 8, true, &s0, 4, 8);
+        const std::vector<LaneDesc> aw = build_plan(rg, nw, h, rows, 8, true, &s1, 4, 8, false, &w);
+        CHECK(validate_plan(aw, nw, h, 8, 8, true).empty());
+        CHECK(s1.out_words == h * nw);
+        const i64 waves = (i64)aw.size() / kWaveLanes, nwg = waves / 4;
+        CHECK(waves <= (i64)eq.size() / kWaveLanes + 8);
+        // every output word exactly once
+        std::vector<int> cover((size_t)(h * nw), 0);
+        for (i64 wv = 0; wv < waves; ++wv)
+            for (int l = 0; l < kWaveLanes; ++l) {
+                const LaneDesc& d = aw[(size_t)(wv * kWaveLanes + l)];
+                if (!(d.flags & LANE_STORE)) continue;
+                for (i64 r = d.row0; r < d.row0 + d.nrows; ++r) ++cover[(size_t)(r * nw + d.col)];
+            }
+        bool once = true;
+        for (int v : cover) once = once && v == 1;
+        CHECK(once);
+        // mean full-segment height by dispatch third: decreasing, in about the weights' ratios
+        double sum[3] = {0, 0, 0}, n[3] = {0, 0, 0};
+        for (i64 wv = 0; wv < waves; ++wv) {
+            const LaneDesc& d = aw[(size_t)(wv * kWaveLanes)];
+            if (d.nrows <= 0 || !(aw[(size_t)(wv * kWaveLanes + 62)].flags & LANE_STORE)) continue;  // full segments
+            const int cls = (int)std::min<i64>(2, (wv / 4) * 3 / std::max<i64>(1, nwg));
+            sum[cls] += d.nrows;
+            n[cls] += 1;
+        }
+        if (n[0] > 0 && n[1] > 0 && n[2] > 0) {
+            const double m0 = sum[0] / n[0], m1 = sum[1] / n[1], m2 = sum[2] / n[2];
+            CHECK(m0 > m1 && m1 > m2);
+            CHECK(std::fabs(m0 / m2 - w[0] / w[2]) < 0.35 * w[0] / w[2]);
+        }
+    }
+}
+
 // Flow plans (plan.hpp build_flow_plan, flow_kernel.hip): race freedom checked exhaustively.  Two items
 // may run concurrently unless one is an ancestor of the other in the dependency graph; for every such
 // pair, no cell of a buffer may be written by one and read or written by the other.  Also: every
@@ -713,6 +757,7 @@ static void test_flow_plan() {
 }
 
 int main() {
+    test_plan_age_weights();
     test_flow_plan();
     test_watchdog();
     test_plan_rounds();

@@ -4,7 +4,8 @@
 // plan, run through the production wave code (wave_runner.hpp), each wave stamping s_memrealtime at
 // its start and end with its hardware slot (HW_ID: SE, CU, SIMD, wave; XCC_ID).  Prints the finish
 // times by the wave's age rank on its SIMD (0 = dispatched first) and by dispatch third of the grid.
-//   build/stamp_probe [N=32768] [heights=1,1,1: relative segment heights of the grid's thirds]
+//   build/stamp_probe [N=32768] [weights=1,1,1: build_plan age_weights, segment heights of the grid's
+//                      dispatch thirds] [reps=3]
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -75,10 +76,12 @@ int main(int argc, char** argv) {
     std::vector<Region> rg = {{0, N, 0, L.nw}};
     const i64 rows = balanced_rows_per_chunk(rg, L.nw, N, 8, resident, 16, true);
     PlanStats st;
-    std::vector<LaneDesc> lanes = build_plan(rg, L.nw, N, rows, 8, true, &st);
+    const bool weighted = !(hts[0] == hts[1] && hts[1] == hts[2]);
+    std::vector<LaneDesc> lanes = build_plan(rg, L.nw, N, rows, 8, true, &st, kWavesPerBlock, 8, false, weighted ? &hts : nullptr);
     const i64 waves = (i64)lanes.size() / kWaveLanes;
-    printf("stamp_probe: %lld^2, K 8, %d blocks/CU, plan %lld waves of %lld rows (resident %lld)\n", (long long)N, bpc,
-           (long long)waves, (long long)rows, (long long)resident);
+    printf("stamp_probe: %lld^2, K 8, %d blocks/CU, plan %lld waves of %lld rows (resident %lld), weights %.2f,%.2f,%.2f\n",
+           (long long)N, bpc, (long long)waves, (long long)rows, (long long)resident, hts[0], hts[1], hts[2]);
+    if (waves > resident) printf("  (more waves than resident slots: not one round)\n");
     LaneDesc* dplan = nullptr;
     CK(hipMalloc(&dplan, lanes.size() * sizeof(LaneDesc)));
     CK(hipMemcpy(dplan, lanes.data(), lanes.size() * sizeof(LaneDesc), hipMemcpyHostToDevice));
@@ -88,7 +91,9 @@ int main(int argc, char** argv) {
     const int blocks = (int)(waves / kWavesPerBlock);
     for (int i = 0; i < 20; ++i) hipLaunchKernelGGL(stamped, dim3(blocks), dim3(64 * kWavesPerBlock), 0, 0, a, b, dplan, p, stamps);
     CK(hipDeviceSynchronize());
-    for (int rep = 0; rep < 3; ++rep) {
+    const int nrep = argc > 3 ? atoi(argv[3]) : 3;
+    std::vector<double> spans;
+    for (int rep = 0; rep < nrep; ++rep) {
         hipLaunchKernelGGL(stamped, dim3(blocks), dim3(64 * kWavesPerBlock), 0, 0, a, b, dplan, p, stamps);
         CK(hipDeviceSynchronize());
         std::vector<u64> s((size_t)waves * 4);
@@ -115,6 +120,7 @@ int main(int argc, char** argv) {
             max_per_simd = std::max(max_per_simd, kv.second.size());
         }
         const double span = (double)(t_max - t_min) * 1e-2;  // us (100 MHz)
+        spans.push_back(span);
         printf("rep %d: pass %.1f us, %zu SIMDs (<= %zu waves each), slot busy %.0f%%\n", rep, span, simd.size(),
                max_per_simd, 100.0 * busy * 1e-2 / (span * (double)waves));
         auto stats = [&](const char* what, auto&& key, int nkeys) {
@@ -135,7 +141,35 @@ int main(int argc, char** argv) {
         };
         stats("age rank", [&](i64 w) { return rank[(size_t)w]; }, (int)max_per_simd);
         stats("grid third", [&](i64 w) { return (int)(3 * (w / kWavesPerBlock) / blocks); }, 3);
+        // segment heights by grid third
+        for (int c = 0; c < 3; ++c) {
+            double sr = 0;
+            i64 n = 0;
+            for (i64 w = 0; w < waves; ++w)
+                if ((int)(3 * (w / kWavesPerBlock) / blocks) == c && lanes[(size_t)w * kWaveLanes].nrows > 0) {
+                    sr += lanes[(size_t)w * kWaveLanes].nrows;
+                    ++n;
+                }
+            printf("  grid third %d: mean segment %.1f rows\n", c, n ? sr / (double)n : 0.0);
+        }
     }
-    (void)hts;
+    // back-to-back passes (event timed): the rate a superstep of such passes runs at
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    float best = 1e30f;
+    for (int r = 0; r < 5; ++r) {
+        CK(hipEventRecord(e0, 0));
+        for (int i = 0; i < 20; ++i)
+            hipLaunchKernelGGL(stamped, dim3(blocks), dim3(64 * kWavesPerBlock), 0, 0, (i & 1) ? b : a, (i & 1) ? a : b, dplan, p, stamps);
+        CK(hipEventRecord(e1, 0));
+        CK(hipEventSynchronize(e1));
+        float ms = 0;
+        CK(hipEventElapsedTime(&ms, e0, e1));
+        best = std::min(best, ms);
+    }
+    std::sort(spans.begin(), spans.end());
+    printf("weights %.2f,%.2f,%.2f: stamped pass span median %.1f us; 20 back-to-back passes %.1f us/pass = %.3f us/gen\n",
+           hts[0], hts[1], hts[2], spans.empty() ? 0.0 : spans[spans.size() / 2], best * 1e3 / 20, best * 1e3 / 160);
     return 0;
 }
