@@ -177,8 +177,11 @@ std::vector<i64> age_bands(const Region& rg, i64 rows_per_chunk, int wg_waves, i
     const i64 C = (i64)w.size();
     std::vector<double> wt((size_t)nb);
     double sum = 0;
+    // (the weighted plan orders every wave by its first segment's rows, the packed narrow ones among
+    // the full-width ones of their bands: band i starts at wave i x (full + 1 / per_wave))
+    const double per_band = (double)full + (narrow ? 1.0 / (double)per_wave : 0.0);
     for (i64 i = 0; i < nb; ++i) {
-        const i64 s = std::min(nwg - 1, i * full / std::max(1, wg_waves));
+        const i64 s = std::min(nwg - 1, (i64)((double)i * per_band) / std::max(1, wg_waves));
         const i64 cls = std::min(C - 1, order[(size_t)s] * C / nwg);
         wt[(size_t)i] = std::max(0.05, w[(size_t)cls]);
         sum += wt[(size_t)i];
@@ -216,10 +219,17 @@ std::vector<LaneDesc> build_plan(const std::vector<Region>& regions, i64 nw, i64
     // too, left each XCD writing one 496-byte piece of every row: measured 32768^2 K=1 passes 71 -> 61
     // us, K=4 17.5 -> 16.1 us/gen, K=8 11.49 -> 11.20 (two halves on two streams), 16384^2 K=8 4.20 ->
     // 4.11 with row-major, profiles/plan_order_ab.txt.)
-    std::stable_sort(packed.begin(), packed.end(), [lw](const std::vector<Item>& a, const std::vector<Item>& b) {
+    // (Age-weighted plans order the packed narrow waves among the full-width ones, by their first
+    // segment: a narrow wave holds segments of its bands' height, so it must land in their dispatch
+    // class — placed last, the narrow segments of the tallest bands ran in the youngest class and
+    // finished a pass ~30 us after the rest, profiles/stamp_probe.txt.)
+    const bool mixed = !bands.empty();
+    std::stable_sort(packed.begin(), packed.end(), [lw, mixed](const std::vector<Item>& a, const std::vector<Item>& b) {
         const bool fa = a.size() == 1 && a[0].lanes() == lw, fb = b.size() == 1 && b[0].lanes() == lw;
-        if (fa != fb) return fa;
-        if (!fa) return false;
+        if (!mixed) {
+            if (fa != fb) return fa;
+            if (!fa) return false;
+        }
         return a[0].r0 != b[0].r0 ? a[0].r0 < b[0].r0 : a[0].c0 < b[0].c0;
     });
     std::vector<std::vector<Item>> waves((size_t)nwaves);

@@ -144,10 +144,10 @@ __device__ __forceinline__ u32 flow_draw(const FlowArgs& a, u32* ctr, u32 seq, i
     return __builtin_amdgcn_readfirstlane(i) * a.nseq + seq;
 }
 
-template <int K, int ROWS>
+template <int K, int ROWS, bool COH = true>
 __device__ __forceinline__ void flow_item(const u64* src, u64* dst, const LaneDesc& d, int nrows, const StepParams& p,
                                           i64 wave) {
-    WaveRunner<K, ROWS, true> w(src, dst, d, nrows, p, wave);
+    WaveRunner<K, ROWS, COH> w(src, dst, d, nrows, p, wave);
     w.run();
 }
 
@@ -160,7 +160,9 @@ __device__ __forceinline__ void flow_item(const u64* src, u64* dst, const LaneDe
 // PF: a wave draws its NEXT ticket when it starts an item, so the draw's latency (a contended atomic,
 // ~1 us under load) hides behind the item instead of preceding the next one.  The deadlock argument
 // holds: a wave holding a drawn-but-unstarted ticket is working on a smaller one.
-template <int ROWS, bool PF>
+// (KONLY, COH: measurement variants of the GOL_FLOW_EXPERIMENTS build only — one depth instantiated,
+// plain row loads and stores; the production kernel is KONLY = 0, COH = true.)
+template <int ROWS, bool PF, int KONLY = 0, bool COH = true>
 __global__ __launch_bounds__(64 * kWavesPerBlock) __attribute__((amdgpu_waves_per_eu(3))) void step_flow(FlowArgs a,
                                                                                                     StepParams p) {
     const int lane = threadIdx.x & 63;
@@ -192,15 +194,19 @@ __global__ __launch_bounds__(64 * kWavesPerBlock) __attribute__((amdgpu_waves_pe
         const u64* src = odd ? a.b : a.a;
         u64* dst = odd ? a.a : a.b;
         if (nrows > 0) {
-            switch (depth) {
+            if constexpr (KONLY > 0) {
+                if (depth == KONLY) flow_item<KONLY, ROWS, COH>(src, dst, d, nrows, p, wave);
+            } else {
+                switch (depth) {
 #define DEPTH_CASE(K)                                             \
     case K:                                                     \
         flow_item<K, ROWS>(src, dst, d, nrows, p, wave);        \
         break;
-                FLOW_DEPTHS(DEPTH_CASE)
+                    FLOW_DEPTHS(DEPTH_CASE)
 #undef DEPTH_CASE
-                default:
-                    break;
+                    default:
+                        break;
+                }
             }
         }
         // every store of the item has left the wave (write-through) before its flag does
@@ -278,6 +284,11 @@ const void* flow_tile_kernel_for(int nw_per_wg, u32 flags) {
 }
 
 const void* flow_kernel_for(u32 flags, u32 variant = 0) {
+#ifdef GOL_FLOW_EXPERIMENTS
+    // bit 1: only depth 8 instantiated; bit 2 (with bit 1): plain loads and stores (y-wrapped tiles only)
+    if ((variant & 6u) == 2u) return (const void*)step_flow<ROWS_WRAP, false, 8, true>;
+    if ((variant & 6u) == 6u) return (const void*)step_flow<ROWS_WRAP, false, 8, false>;
+#endif
     if (variant & 1u)
         return (flags & STEP_WRAP_Y) ? (const void*)step_flow<ROWS_WRAP, true> : (const void*)step_flow<ROWS_GHOST, true>;
     return (flags & STEP_WRAP_Y) ? (const void*)step_flow<ROWS_WRAP, false> : (const void*)step_flow<ROWS_GHOST, false>;

@@ -8,7 +8,7 @@ for s in $SRCS csrc/src/core/plan.cpp csrc/src/core/geometry.cpp csrc/src/core/c
   o=build/fb/$(basename $s).o
   objs+=($o)
   if [ ! -f $o ] || [ $s -nt $o ] || [ csrc/src/hip/wave_runner.hpp -nt $o ] || [ csrc/include/gol/hip_kernels.hpp -nt $o ] || [ csrc/include/gol/plan.hpp -nt $o ]; then
-    ( hipcc --offload-arch=gfx950 -O3 -std=c++17 -Icsrc/include -Wno-unused-result -Wno-unused-value $FLAGS -x hip -c $s -o $o || echo "FAILED $s" ) &
+    ( hipcc --offload-arch=gfx950 -O3 -std=c++17 -Icsrc/include -Wno-unused-result -Wno-unused-value -DGOL_FLOW_EXPERIMENTS $FLAGS -x hip -c $s -o $o || echo "FAILED $s" ) &
   fi
 done
 wait

@@ -4,8 +4,8 @@
 // plan, run through the production wave code (wave_runner.hpp), each wave stamping s_memrealtime at
 // its start and end with its hardware slot (HW_ID: SE, CU, SIMD, wave; XCC_ID).  Prints the finish
 // times by the wave's age rank on its SIMD (0 = dispatched first) and by dispatch third of the grid.
-//   build/stamp_probe [N=32768] [weights=1,1,1: build_plan age_weights, segment heights of the grid's
-//                      dispatch thirds] [reps=3]
+//   build/stamp_probe [N=32768] [weights=1: build_plan age_weights, one per dispatch class of the grid]
+//                     [reps=3] [blocks_per_cu=0: the occupancy limit]
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -59,8 +59,16 @@ __global__ __launch_bounds__(64 * kWavesPerBlock) void stamped(const u64* __rest
 
 int main(int argc, char** argv) {
     const i64 N = argc > 1 ? atoll(argv[1]) : 32768;
-    std::vector<double> hts = {1, 1, 1};
-    if (argc > 2) sscanf(argv[2], "%lf,%lf,%lf", &hts[0], &hts[1], &hts[2]);
+    std::vector<double> hts;
+    {
+        const std::string s = argc > 2 ? argv[2] : "1";
+        for (size_t q = 0; q < s.size();) {
+            size_t e = s.find(',', q);
+            if (e == std::string::npos) e = s.size();
+            hts.push_back(atof(s.substr(q, e - q).c_str()));
+            q = e + 1;
+        }
+    }
     Layout L(N, N, 8);
     const size_t bytes = (size_t)(L.words() + kSlackRows * L.pitch) * 8;
     u64 *a, *b, *trash, *stamps;
@@ -72,15 +80,18 @@ int main(int argc, char** argv) {
     CK(hipGetDeviceProperties(&prop, 0));
     int bpc = 0;
     CK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, stamped, 64 * kWavesPerBlock, 0));
+    if (argc > 4 && atoi(argv[4]) > 0) bpc = std::min(bpc, atoi(argv[4]));
     const i64 resident = (i64)bpc * prop.multiProcessorCount * kWavesPerBlock;
     std::vector<Region> rg = {{0, N, 0, L.nw}};
     const i64 rows = balanced_rows_per_chunk(rg, L.nw, N, 8, resident, 16, true);
     PlanStats st;
-    const bool weighted = !(hts[0] == hts[1] && hts[1] == hts[2]);
+    const bool weighted = hts.size() > 1;
+    std::string wtxt;
+    for (double x : hts) wtxt += (wtxt.empty() ? "" : ",") + std::to_string(x).substr(0, 4);
     std::vector<LaneDesc> lanes = build_plan(rg, L.nw, N, rows, 8, true, &st, kWavesPerBlock, 8, false, weighted ? &hts : nullptr);
     const i64 waves = (i64)lanes.size() / kWaveLanes;
-    printf("stamp_probe: %lld^2, K 8, %d blocks/CU, plan %lld waves of %lld rows (resident %lld), weights %.2f,%.2f,%.2f\n",
-           (long long)N, bpc, (long long)waves, (long long)rows, (long long)resident, hts[0], hts[1], hts[2]);
+    printf("stamp_probe: %lld^2, K 8, %d blocks/CU, plan %lld waves of %lld rows (resident %lld), weights %s\n",
+           (long long)N, bpc, (long long)waves, (long long)rows, (long long)resident, wtxt.c_str());
     if (waves > resident) printf("  (more waves than resident slots: not one round)\n");
     LaneDesc* dplan = nullptr;
     CK(hipMalloc(&dplan, lanes.size() * sizeof(LaneDesc)));
@@ -140,17 +151,17 @@ int main(int argc, char** argv) {
             }
         };
         stats("age rank", [&](i64 w) { return rank[(size_t)w]; }, (int)max_per_simd);
-        stats("grid third", [&](i64 w) { return (int)(3 * (w / kWavesPerBlock) / blocks); }, 3);
-        // segment heights by grid third
-        for (int c = 0; c < 3; ++c) {
+        stats("dispatch class", [&](i64 w) { return (int)(bpc * (w / kWavesPerBlock) / blocks); }, bpc);
+        // segment heights by dispatch class
+        for (int c = 0; c < bpc; ++c) {
             double sr = 0;
             i64 n = 0;
             for (i64 w = 0; w < waves; ++w)
-                if ((int)(3 * (w / kWavesPerBlock) / blocks) == c && lanes[(size_t)w * kWaveLanes].nrows > 0) {
+                if ((int)(bpc * (w / kWavesPerBlock) / blocks) == c && lanes[(size_t)w * kWaveLanes].nrows > 0) {
                     sr += lanes[(size_t)w * kWaveLanes].nrows;
                     ++n;
                 }
-            printf("  grid third %d: mean segment %.1f rows\n", c, n ? sr / (double)n : 0.0);
+            printf("  dispatch class %d: mean segment %.1f rows\n", c, n ? sr / (double)n : 0.0);
         }
     }
     // back-to-back passes (event timed): the rate a superstep of such passes runs at
@@ -169,7 +180,7 @@ int main(int argc, char** argv) {
         best = std::min(best, ms);
     }
     std::sort(spans.begin(), spans.end());
-    printf("weights %.2f,%.2f,%.2f: stamped pass span median %.1f us; 20 back-to-back passes %.1f us/pass = %.3f us/gen\n",
-           hts[0], hts[1], hts[2], spans.empty() ? 0.0 : spans[spans.size() / 2], best * 1e3 / 20, best * 1e3 / 160);
+    printf("bpc %d weights %s: stamped pass span median %.1f us; 20 back-to-back passes %.1f us/pass = %.3f us/gen\n",
+           bpc, wtxt.c_str(), spans.empty() ? 0.0 : spans[spans.size() / 2], best * 1e3 / 20, best * 1e3 / 160);
     return 0;
 }
