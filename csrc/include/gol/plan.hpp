@@ -65,7 +65,9 @@ struct PlanStats {
 // nwg is in class b * C / nwg.  On MI355X the co-resident waves of a SIMD are issued by age, and in a
 // one-round plan of 3 workgroups per CU the first-dispatched third of the grid finished a pass in ~half
 // the time of the last third (tools/stamp_probe.hip, profiles/stamp_probe.txt): weights (w0 > w1 > w2)
-// give the older waves taller segments so that a SIMD's waves finish together.
+// give the older waves taller segments so that a SIMD's waves finish together.  (Measured: every weight
+// set made the pass slower — it is VALU-bound, the SIMD busy until its last wave ends whatever the
+// split, profiles/stamp_age_weights.txt — so no engine plan uses it; tools/stamp_probe.hip does.)
 std::vector<LaneDesc> build_plan(const std::vector<Region>& regions, i64 nw, i64 h, i64 rows_per_chunk, int k,
                                  bool xwrap, PlanStats* stats = nullptr, int wg_waves = kWavesPerBlock,
                                  int xcds = 8, bool fold = false, const std::vector<double>* age_weights = nullptr);

@@ -121,7 +121,6 @@ const DevPlan& HipEngine::plan(int kind, int k, i64 e) {
     if (it != plans_.end()) return it->second;
     std::vector<Region> rg = regions(kind, k, e);
     DevPlan p;
-    bool age = false;  // age-weighted segment heights (build_plan age_weights)
     i64 rows = cfg_.rows_per_wave;
     if (tile_kernel(kind)) {
         // step_tile: one workgroup per plan wave, one tile per CU per round; rows are capped by
@@ -191,14 +190,12 @@ const DevPlan& HipEngine::plan(int kind, int k, i64 e) {
             const i64 resident = bpc * kWavesPerBlock * cus_;
             // big tiles: several rounds of segments near round_rows() rows (plan.hpp round_balanced_rows)
             rows = round_balanced_rows(rg, L_.nw, L_.h, k, resident, 2 * (i64)k, xwrap_by_plan(), round_rows(k));
-            // one round of bpc workgroups per CU: segment heights weighted by dispatch class
-            age = (i64)age_weights_.size() == bpc && bpc > 1 && rg.size() == 1 &&
-                  plan_waves(rg, L_.nw, L_.h, rows) <= resident;
+            // (Segment heights weighted by dispatch class, plan.hpp build_plan age_weights, made every
+            // pass slower: the pass is VALU-bound, profiles/stamp_age_weights.txt.)
         }
     }
     std::vector<LaneDesc> lanes = build_plan(rg, L_.nw, L_.h, rows, k, xwrap_by_plan(), &p.st,
-                                             (tile_kernel(kind) || pipe) ? 1 : kWavesPerBlock, cfg_.plan_xcds, p.fold,
-                                             age ? &age_weights_ : nullptr);
+                                             (tile_kernel(kind) || pipe) ? 1 : kWavesPerBlock, cfg_.plan_xcds, p.fold);
     const std::string bad = validate_plan(lanes, L_.nw, L_.h, L_.R, k, (step_flags() & hipk::STEP_WRAP_Y) != 0);
     if (!bad.empty()) throw Error(strprintf("refusing to launch an unsafe plan (kind %d, k %d, e %lld): %s", kind, k,
                                             (long long)e, bad.c_str()));

@@ -572,23 +572,7 @@ class HipEngine : public Engine {
     // round_balanced_rows): GOL_ROUND_ROWS_PER_LEVEL (default 45) x the pass depth; 0 = one round always
     i64 round_rows_per_level_ = env_int("GOL_ROUND_ROWS_PER_LEVEL", 45);
     i64 round_rows(int k) const { return round_rows_per_level_ > 0 ? round_rows_per_level_ * k : 0; }
-    // Segment heights of one-round step_temporal plans by dispatch class (plan.hpp build_plan
-    // age_weights: a SIMD's waves are issued by age, so the first-dispatched get taller segments).
-    // GOL_AGE_WEIGHTS="w0,w1,w2" (one weight per resident workgroup of a CU; "1" disables).
-    std::vector<double> age_weights_ = parse_age_weights(env_str("GOL_AGE_WEIGHTS", kAgeWeightsDefault));
-    static constexpr const char* kAgeWeightsDefault = "1";
-    static std::vector<double> parse_age_weights(const std::string& s) {
-        std::vector<double> w;
-        for (size_t p = 0; p < s.size();) {
-            size_t q = s.find(',', p);
-            if (q == std::string::npos) q = s.size();
-            w.push_back(atof(s.substr(p, q - p).c_str()));
-            p = q + 1;
-        }
-        for (double x : w)
-            if (!(x > 0)) throw Error("GOL_AGE_WEIGHTS must be positive numbers separated by commas (got '" + s + "')");
-        return w;
-    }
+
     int tile_inplace_ = (int)env_int("GOL_TILE_INPLACE", -1);
     int tile_fold_ = (int)env_int("GOL_TILE_FOLD", -1);
     int pipe_nw_ = 0, pipe_l_ = 0, pipe_wg_ = 0, pipe_k_ = 0;  // step_pipe geometry (set_pipe)
