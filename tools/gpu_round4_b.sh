@@ -8,7 +8,7 @@ mkdir -p gpurun_out
 export TMPDIR=/tmp
 step() { echo "[batch-b] $(date +%T) $*"; }
 step configs
-bash tools/baseline_configs.sh cfg2 cfg2b cfg3 cfg4 > gpurun_out/configs_summary.txt 2>&1 || { cat gpurun_out/configs_summary.txt; exit 1; }
+bash tools/baseline_configs.sh cfg2 cfg2f cfg2nf cfg2 cfg2f cfg2nf cfg2b cfg3 cfg4 > gpurun_out/configs_summary.txt 2>&1 || { cat gpurun_out/configs_summary.txt; exit 1; }
 step self-exchange
 for v in "GOL_RCCL_REGISTER=1" "GOL_RCCL_REGISTER=0" "GOL_SCHEDULE=flow+ov" "GOL_SCHEDULE=flow"; do
   env $v timeout -k 10 300 python3 bench.py --gpus 1 --steps 20 --warmup 5 --self-exchange > gpurun_out/selfx_$(echo $v | tr '=+' '__').json 2> gpurun_out/selfx_err.txt || { echo "self-exchange $v failed"; tail gpurun_out/selfx_err.txt; exit 1; }
