@@ -61,8 +61,7 @@ bool HipEngine::flow_eligible() {
     // which a single launch cannot do
     if (cfg_.compat || cfg_.profile || cfg_.force_split || kernel_ == "lds" || res_) return false;
     if (cfg_.kernel == "pipe" || cfg_.kernel == "resident") return false;
-    if (self_x() && !L_.aligned()) return false;
-    return env_int("GOL_FLOW", 1) != 0;
+    return !(self_x() && !L_.aligned());
 }
 
 // Passes of a flow superstep: as few as the items' deepest depth allows, as equal as possible

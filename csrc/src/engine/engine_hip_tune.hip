@@ -150,11 +150,15 @@ void HipEngine::choose_schedule() {
         if (cfg_.subtiles == 2) cands.clear();
         cands.insert(cands.end(), dc.begin(), dc.end());
     }
-    // The one-tile superstep as ONE dependency-driven launch (step_flow, engine_hip_flow.hip), eager and
-    // replayed from a graph (with neighbours only where RCCL may be captured).  Timed on scratch: the
-    // candidate needs memory for one more board (agreed over the ranks: the timing is collective).
-    if (cands[0] != "split" && flow_eligible()) {
-        double ok = flow_timing_buffers() ? 1.0 : 0.0;
+    // The one-tile superstep as ONE dependency-driven launch (step_flow, engine_hip_flow.hip): opt-in
+    // (GOL_SCHEDULE=flow / flow+ov forces it, GOL_FLOW=1 adds it to the timed candidates).  It measured
+    // slower than the pass schedules on every configuration (docs/PERFORMANCE.md §15: 32768^2 12.87 vs
+    // 9.55 us/gen, 8192^2 x 1000 1.47 vs 1.40 ms, self-exchange 17.4 vs 13.2 us/gen), and its timing
+    // candidate once won config 2's init against a local candidate timed on shorter supersteps.  Timed
+    // on scratch: the candidate needs memory for one more board (agreed over the ranks: collective).
+    const bool flow_forced = cfg_.sched == "flow" || cfg_.sched == "flow+ov";
+    if (cands[0] != "split" && (flow_forced || env_int("GOL_FLOW", 0) != 0) && flow_eligible()) {
+        double ok = flow_forced ? 1.0 : (flow_timing_buffers() ? 1.0 : 0.0);  // (forced: not timed, no scratch)
         if (t_->size() > 1) ok = t_->allreduce_min(ok);
         // flow+ov also needs its CU-restricted stream (hip_engine.hpp kOvReservedCus) on every rank
         double ov_ok = nbrs && device_transport_ && ov_stream() ? 1.0 : 0.0;
@@ -165,15 +169,14 @@ void HipEngine::choose_schedule() {
             // (no graphed flow candidate: a superstep is one launch whose epoch is an argument, and a
             // graph replay costs more than a direct launch)
         }
-        if (cfg_.sched == "flow" || cfg_.sched == "flow+ov") {  // GOL_SCHEDULE=flow[+ov]: the only candidate
-            if (ok <= 0) throw Error("GOL_SCHEDULE=flow: no device memory for the flow timing scratch");
+        if (flow_forced) {  // GOL_SCHEDULE=flow[+ov]: the only candidate (not timed)
             if (cfg_.sched == "flow+ov" && !(nbrs && device_transport_))
                 throw Error("GOL_SCHEDULE=flow+ov needs neighbours and a device transport (RCCL)");
             if (cfg_.sched == "flow+ov" && ov_ok <= 0)
                 throw Error("GOL_SCHEDULE=flow+ov: no CU-restricted compute stream (hipExtStreamCreateWithCUMask)");
             cands = {cfg_.sched};
         }
-    } else if (cfg_.sched == "flow" || cfg_.sched == "flow+ov") {
+    } else if (flow_forced) {
         throw Error("GOL_SCHEDULE=flow: this tile cannot run flow supersteps (GOL_KERNEL / GOL_COMPAT / width)");
     }
     std::string pick = cands[0];
@@ -188,13 +191,20 @@ void HipEngine::choose_schedule() {
         const int reps = short_run ? 1 : kSchedReps;
         const int rounds = short_run ? 15 : 3;
         std::vector<double> best(cands.size(), 1e30);
+        // flow supersteps of tile items run the whole hinted run as one launch (flow_superstep_depth):
+        // every candidate is then timed over that many generations, the others as whole supersteps of k
+        // (timed on 4 x 32 generations against one 1000-generation launch, the local candidate paid four
+        // graph replays for the flow candidate's one and lost config 2's init, 1.60 vs 1.44 us/gen, to a
+        // flow run that then measured 1.52 against local's 1.36)
+        bool any_flow = false;
+        for (const std::string& c : cands) any_flow = any_flow || c.rfind("flow", 0) == 0;
+        const int span = any_flow && !short_run ? std::max(k, flow_superstep_depth()) : k;
         spin_up();
         for (int round = 0; round < rounds; ++round)
             for (size_t c = 0; c < cands.size(); ++c) {
-                // flow supersteps of tile items run the whole hinted run as one launch (flow_superstep_depth)
                 const bool fl = cands[c].rfind("flow", 0) == 0;
-                const int kc = fl && !short_run ? std::max(k, flow_superstep_depth()) : k;
-                const int rc = std::max(1, reps * k / kc);
+                const int kc = fl ? span : k;
+                const int rc = span > k ? std::max(1, span / kc) : std::max(1, reps * k / kc);
                 if (round == 0) time_schedule(cands[c], kc, rc);  // warm-up: connections, plans, graphs
                 synchronize();
                 t_->barrier();
@@ -542,8 +552,8 @@ void HipEngine::autotune_kernel() {
     // between tiles inside the kernel every kin generations.  Timed on launches of the hinted run's
     // length (at most 256 generations) against the best pass kernel above.  (GOL_SCHEDULE=flow asks
     // for flow supersteps of the pass kernels: no resident candidate.)
-    const bool flow_forced = cfg_.sched == "flow" || cfg_.sched == "flow+ov";
-    if (resident_eligible() && !split_used() && (!flow_forced || cfg_.kernel == "resident")) {
+    const bool flow_forced2 = cfg_.sched == "flow" || cfg_.sched == "flow+ov";
+    if (resident_eligible() && !split_used() && (!flow_forced2 || cfg_.kernel == "resident")) {
         const int G = std::min(res_run_depth(), 256);
         float rbest = 1e30f;
         int rk = 0;

@@ -17,7 +17,7 @@ step rehearsal
 timeout -k 10 900 bash tools/rehearse_torchrun.sh > gpurun_out/rehearse_summary.txt 2>&1 || { tail -30 gpurun_out/rehearse_summary.txt; exit 1; }
 step pmc
 for kn in flow temporal; do
-  if [ $kn = flow ]; then envs="GOL_SCHEDULE=flow"; else envs="GOL_SUBTILES=0 GOL_FLOW=0"; fi
+  if [ $kn = flow ]; then envs="GOL_SCHEDULE=flow"; else envs="GOL_SUBTILES=0"; fi
   env $envs timeout -k 10 120 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_WAIT_INST_ANY SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_INSTS_VMEM_WR SQ_INSTS_VMEM_RD GRBM_GUI_ACTIVE -d gpurun_out/pmc_$kn -o pmc -- python3 bench.py --gpus 1 --steps 20 --warmup 5 --no-phases > gpurun_out/pmc_$kn.txt 2>&1 || { echo "pmc $kn rc=$?"; tail gpurun_out/pmc_$kn.txt; exit 1; }
 done
 step done
