@@ -18,8 +18,9 @@ for round in 1 2; do
 done
 for i in 1 2; do
   echo "== cfg2 CLI GOL_FLOW=1" | tee -a $o
-  GOL_BACKEND=hip GOL_FLOW=1 GOL_VERBOSE=1 timeout -k 10 120 ./build/gol 5 8192 1000 256 0 > gpurun_out/cfg2_flowtimed.log 2>&1 || { echo "cli rc=$?"; tail gpurun_out/cfg2_flowtimed.log; exit 1; }
-  grep -E "TOTAL|schedule|sched:" gpurun_out/cfg2_flowtimed.log | head -5 | tee -a $o
+  GOL_BACKEND=hip GOL_FLOW=1 GOL_METRICS_JSON=gpurun_out/cfg2_flowtimed.json timeout -k 10 120 ./build/gol 5 8192 1000 256 0 > gpurun_out/cfg2_flowtimed.log 2>&1 || { echo "cli rc=$?"; tail gpurun_out/cfg2_flowtimed.log; exit 1; }
+  grep -E "TOTAL" gpurun_out/cfg2_flowtimed.log | tee -a $o
+  python3 -c "import json; d=json.load(open('gpurun_out/cfg2_flowtimed.json')); s=json.dumps(d); import re; print(re.findall(r'\"schedule\": \"[^\"]*\"', s)[:1], re.findall(r'sched:[a-z+]*=[0-9.]*', s))" | tee -a $o
 done
 for i in 1 2 3; do
   r=$(timeout -k 10 240 python3 bench.py --gpus 1 --steps 20 --warmup 5 --self-exchange 2>/dev/null) || { echo "selfx rc=$?"; exit 1; }
