@@ -34,6 +34,18 @@ __device__ __forceinline__ void store_row_word(uint2* p, u32 lo, u32 hi) {
         *p = make_uint2(lo, hi);
 }
 
+// A row load of the wave runner: the plain dereference unless COH.  (Written in place, not through
+// load_row_word<false>: routing the plain loads through the helper changed the K = 12 kernel's
+// schedule — 256 VGPRs with AGPR spills and a vmcnt(0) before the stores in the row loop, the pass
+// 119 -> 163 us at 32768^2 — although the helper inlines to the same load.)
+#define GOL_ROW_LOAD(dst)                            \
+    do {                                             \
+        if constexpr (COH)                           \
+            (dst) = load_row_word<true>(ld);         \
+        else                                         \
+            (dst) = *ld;                             \
+    } while (0)
+
 // Row prefetch: a register triple loaded one row-triple ahead, pinned above the compute with a
 // sched_barrier (otherwise the scheduler sinks the loads to the end of the loop body).  (An LDS
 // DMA ring and a skewed level pipeline were built and measured slower; docs/PERFORMANCE.md §2.)
@@ -118,7 +130,7 @@ struct WaveRunner {
         st_stride = out ? p.pitch : 0;
 #pragma unroll
         for (int j = 0; j < D; ++j) {
-            pf[j] = load_row_word<COH>(ld);
+            GOL_ROW_LOAD(pf[j]);
             next_row();
         }
     }
@@ -129,12 +141,12 @@ struct WaveRunner {
         uint2 x;
         if constexpr (D == 3) {
             x = pf[PH];
-            pf[PH] = load_row_word<COH>(ld);  // prefetch 3 rows ahead (the allocation has slack rows past the halo)
+            GOL_ROW_LOAD(pf[PH]);  // prefetch 3 rows ahead (the allocation has slack rows past the halo)
         } else {
             x = pf[0];  // a queue of D rows (the shift is register renaming in the unrolled code)
 #pragma unroll
             for (int j = 0; j + 1 < D; ++j) pf[j] = pf[j + 1];
-            pf[D - 1] = load_row_word<COH>(ld);
+            GOL_ROW_LOAD(pf[D - 1]);
         }
         next_row();
         lo = x.x;
@@ -144,7 +156,7 @@ struct WaveRunner {
     template <int PH, bool GUARD>
     __device__ __forceinline__ void compute_store(u32 lo, u32 hi, int i) {
         if (!advance<K, PH, GUARD>(P, lo, hi, i)) return;
-        store_row_word<COH>(st, lo, hi);
+        if constexpr (COH) store_row_word<true>(st, lo, hi); else *st = make_uint2(lo, hi);
         st += st_stride;
     }
 
@@ -171,7 +183,7 @@ struct WaveRunner {
             // queue shift of the fill phase collapses the prefetch distance to one triple).
 #define ROW6_STEP(J)                                          \
     compute_store<(J) % 3, false>(pf[J].x, pf[J].y, i + (J)); \
-    pf[J] = load_row_word<COH>(ld);                                             \
+    GOL_ROW_LOAD(pf[J]);                                             \
     next_row();                                              \
     __builtin_amdgcn_sched_barrier(0);
             for (; i + 6 <= n; i += 6) {
@@ -193,21 +205,21 @@ struct WaveRunner {
                 // issued, s_waitcnt vmcnt(0), and the prefetch is lost.)
                 uint2 q[3];
                 for (; i + 6 <= n; i += 6) {
-                    q[0] = load_row_word<COH>(ld);
+                    GOL_ROW_LOAD(q[0]);
                     next_row();
-                    q[1] = load_row_word<COH>(ld);
+                    GOL_ROW_LOAD(q[1]);
                     next_row();
-                    q[2] = load_row_word<COH>(ld);
+                    GOL_ROW_LOAD(q[2]);
                     next_row();
                     __builtin_amdgcn_sched_barrier(0);
                     compute_store<0, false>(pf[0].x, pf[0].y, i);
                     compute_store<1, false>(pf[1].x, pf[1].y, i + 1);
                     compute_store<2, false>(pf[2].x, pf[2].y, i + 2);
-                    pf[0] = load_row_word<COH>(ld);
+                    GOL_ROW_LOAD(pf[0]);
                     next_row();
-                    pf[1] = load_row_word<COH>(ld);
+                    GOL_ROW_LOAD(pf[1]);
                     next_row();
-                    pf[2] = load_row_word<COH>(ld);
+                    GOL_ROW_LOAD(pf[2]);
                     next_row();
                     __builtin_amdgcn_sched_barrier(0);
                     compute_store<0, false>(q[0].x, q[0].y, i + 3);
@@ -218,11 +230,11 @@ struct WaveRunner {
             for (; i + 3 <= n; i += 3) {
                 // hoist the whole next triple's loads above this triple's compute
                 const uint2 x0 = pf[0], x1 = pf[1], x2 = pf[2];
-                pf[0] = load_row_word<COH>(ld);
+                GOL_ROW_LOAD(pf[0]);
                 next_row();
-                pf[1] = load_row_word<COH>(ld);
+                GOL_ROW_LOAD(pf[1]);
                 next_row();
-                pf[2] = load_row_word<COH>(ld);
+                GOL_ROW_LOAD(pf[2]);
                 next_row();
                 __builtin_amdgcn_sched_barrier(0);
                 compute_store<0, false>(x0.x, x0.y, i);
