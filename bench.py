@@ -100,6 +100,24 @@ def launch_children(args) -> int:
     return subprocess.run(cmd, env=env).returncode
 
 
+_RECORD = None
+
+
+def _reserve_stdout():
+    """Keep a private handle on stdout for the JSON record and point file descriptor 1 at stderr."""
+    sys.stdout.flush()
+    fd = os.dup(1)
+    os.dup2(2, 1)
+    return os.fdopen(fd, "w", buffering=1)
+
+
+def emit(record) -> None:
+    """Print the one JSON line (to the real stdout)."""
+    out = _RECORD if _RECORD is not None else sys.stdout
+    out.write(json.dumps(record) + "\n")
+    out.flush()
+
+
 def main() -> int:
     args = parse_args()
     # Decided before anything touches the GPU (importing the package does not; hip_device_count does).
@@ -114,6 +132,11 @@ def main() -> int:
             print(json.dumps({"metric": METRIC, "value": None, "unit": "cell-updates/s", "n_gpus": world,
                               "error": msg}), flush=True)
         return 2
+
+    # stdout carries the JSON record only: what C libraries write to it (RCCL prints a version block at
+    # communicator init) goes to stderr from here on
+    global _RECORD
+    _RECORD = _reserve_stdout()
 
     import gol_amd
     from gol_amd.parallel import init_distributed, rccl_transport, torch_transport
@@ -145,9 +168,9 @@ def main() -> int:
             elif not args.allow_host_staging:
                 # a multi-GPU number measured over host-staged halos is not the RCCL/xGMI design
                 if rank == 0:
-                    print(json.dumps({"metric": METRIC, "value": None, "unit": "cell-updates/s", "n_gpus": P,
-                                      "error": "RCCL unavailable on some rank; refusing to measure host-staged "
-                                               "halos (pass --allow-host-staging to do so)"}), flush=True)
+                    emit({"metric": METRIC, "value": None, "unit": "cell-updates/s", "n_gpus": P,
+                          "error": "RCCL unavailable on some rank; refusing to measure host-staged "
+                                   "halos (pass --allow-host-staging to do so)"})
                 return 3
             elif rank == 0:
                 print("[bench] using host-staged halos on every rank", file=sys.stderr, flush=True)
@@ -270,8 +293,8 @@ def main() -> int:
     }
     if problems:
         if rank == 0:
-            print(json.dumps({"metric": METRIC, "value": None, "unit": "cell-updates/s", "n_gpus": P,
-                              "error": "; ".join(problems), "per_rank": per_rank_block}), flush=True)
+            emit({"metric": METRIC, "value": None, "unit": "cell-updates/s", "n_gpus": P,
+                  "error": "; ".join(problems), "per_rank": per_rank_block})
         return 5
 
     yard = None
@@ -337,7 +360,7 @@ def main() -> int:
         if yard:
             out["yardstick_naive_byte_kernel"] = yard
             out["speedup_vs_yardstick"] = value / (yard["cell_updates_per_s"] * P)
-        print(json.dumps(out), flush=True)
+        emit(out)
     if P > 1 or rccl is not None:
         import gc
 

@@ -117,3 +117,19 @@ def test_bench_rank_problems():
     assert "disagree" in p
     (p,) = bench.rank_problems(same, 4, 2)
     assert "spans 2 of 4" in p
+
+
+def test_bench_stdout_is_the_record_only():
+    """Writes to file descriptor 1 from C libraries (RCCL's version block at communicator init) must not
+    reach stdout: bench.py points fd 1 at stderr and keeps its own handle for the JSON line."""
+    code = (
+        "import os, sys; sys.path.insert(0, %r); import bench; "
+        "bench._RECORD = bench._reserve_stdout(); "
+        "os.write(1, b'RCCL version : banner\\n'); print('python print'); "
+        "bench.emit({'metric': 'm', 'value': 1})" % REPO
+    )
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    lines = [l for l in r.stdout.splitlines() if l.strip()]
+    assert lines == ['{"metric": "m", "value": 1}'], r.stdout
+    assert "RCCL version" in r.stderr and "python print" in r.stderr
