@@ -79,8 +79,12 @@ HipEngine::HipEngine(const Geometry& g, const EngineConfig& c, std::shared_ptr<T
     // Register both boards (their ghost and edge rows are what the one-tile exchanges send and receive)
     // with the device transport: RCCL's user-buffer registration (ncclCommRegister) lets peer
     // transfers read and write them directly instead of staging through its FIFOs.  Sub-tile halves
-    // and 2-D staging buffers stay unregistered.  GOL_RCCL_REGISTER=0 keeps every buffer unregistered.
-    if (device_transport_ && env_int("GOL_RCCL_REGISTER", 1) != 0 && !halo_items(L_.R).empty()) {
+    // and 2-D staging buffers stay unregistered.  Default: on for a one-rank communicator (the
+    // self-exchange proxy, where it was measured: 13.21 vs 13.29 us/gen, exchange 14.96 vs 15.2 us,
+    // profiles/round4_batch_c.txt — the sub-tile schedule that wins there sends from the unregistered
+    // halves), off with peers until a multi-GPU run has measured it; GOL_RCCL_REGISTER=0/1 forces.
+    const int reg_default = t_->size() == 1 ? 1 : 0;
+    if (device_transport_ && env_int("GOL_RCCL_REGISTER", reg_default) != 0 && !halo_items(L_.R).empty()) {
         for (int i = 0; i < 2; ++i) reg_[i] = t_->register_buffer(buf_[i], bytes);
         stats_registered_ = reg_[0] != nullptr && reg_[1] != nullptr;
     }
