@@ -561,6 +561,26 @@ static void test_plan_rounds() {
 
 // Age-weighted plans (build_plan age_weights): the plan still covers every output word exactly once,
 // fits the same waves, and the first-dispatched third of the grid gets the tallest segments.
+// The sub-tile overlap's band on the tile kernel (engine_hip_subtiles.hip sub_plan part 2): one tile
+// per 62-word column of a band with ghost rows above it, every output word once, inside the halo.
+static void test_band_tile_plan() {
+    for (const auto& c : std::vector<std::tuple<i64, i64, int, i64>>{{16384, 512, 12, 8}, {16384, 512, 8, 0}, {4096, 100, 12, 8}}) {
+        const i64 h = std::get<0>(c), nw = std::get<1>(c), e = std::get<3>(c);
+        const int k = std::get<2>(c);
+        for (int s = 0; s < 2; ++s) {
+            const std::vector<Region> rg = {{s == 0 ? -e : h - k, s == 0 ? k : h + e, 0, nw}};
+            const i64 band = rg[0].r1 - rg[0].r0;
+            PlanStats st;
+            const std::vector<LaneDesc> lanes = build_plan(rg, nw, h, band, k, true, &st, 1, 8);
+            CHECK(validate_plan(lanes, nw, h, 128, k, false).empty());
+            CHECK(st.out_words == band * nw);
+            const i64 tiles = (i64)lanes.size() / kWaveLanes;
+            CHECK(tiles >= (nw + kSegWords - 1) / kSegWords && tiles <= (nw + kSegWords - 1) / kSegWords + 4);
+            for (i64 t = 0; t < tiles; ++t) CHECK(lanes[(size_t)(t * kWaveLanes)].nrows == 0 || lanes[(size_t)(t * kWaveLanes)].nrows == band);
+        }
+    }
+}
+
 static void test_plan_age_weights() {
     const std::vector<double> w = {1.6, 1.15, 0.75};
     for (const auto& c : std::vector<std::pair<i64, i64>>{{32768, 512}, {16384, 256}, {8192, 512}, {4000, 100}}) {
@@ -757,6 +777,7 @@ static void test_flow_plan() {
 }
 
 int main() {
+    test_band_tile_plan();
     test_plan_age_weights();
     test_flow_plan();
     test_watchdog();
