@@ -145,33 +145,22 @@ void HipEngine::dual_superstep(int k) {
         launch_half(0, p, k, s_comp_, 0, 2);
         HIP_CHECK(hipStreamWaitEvent(s_comm_, ev_sub_x_, 0));
         launch_half(1, p, k, s_comm_, 0, 2);
-    } else if (ov) {
-        // The exchange is enqueued FIRST, on the comm stream, and half 1's first pass right behind it
-        // there; then half 0's interior, and its band after a wait for the exchange.  Half 1 is the
-        // superstep's critical path (it starts after the exchange and, launched later, loses SIMD issue
-        // to half 0 by age): enqueued after half 0's interior, the RCCL group's host work (~10 us) and
-        // the band's wait and launch sat between the exchange kernel's end and half 1's start (a 10.7-us
-        // gap in the driver-cut trace, profiles/kernel_trace_selfx_round4.txt).
-        wait_pending(s_comm_, ev_sub_a_);  // the exchange sends half 0's edge and writes its halo
-        std::vector<Message> sends, recvs;
-        dual_messages(p, k, sends, recvs);
-        exchange_rows(sends, recvs, s_comm_);
-        stats_.exchanges += 1;
-        stats_.halo_bytes += (u64)(rows_bytes(0, k) + rows_bytes(1, k));
-        HIP_CHECK(hipEventRecord(ev_sub_x_, s_comm_));
-        launch_half(1, p, k, s_comm_, 0);
-        launch_half(0, p, k, s_comp_, 0, 1);
-        HIP_CHECK(hipStreamWaitEvent(s_comp_, ev_sub_x_, 0));
-        launch_half(0, p, k, s_comp_, 0, 2);
     } else if (!self_y()) {
+        hipStream_t xs = s_comp_;
+        if (ov) {
+            launch_half(0, p, k, s_comp_, 0, 1);
+            wait_pending(s_comm_, ev_sub_a_);  // the exchange sends half 0's edge and writes its halo
+            xs = s_comm_;
+        }
         std::vector<Message> sends, recvs;
         dual_messages(p, k, sends, recvs);
-        exchange_rows(sends, recvs, s_comp_);
+        exchange_rows(sends, recvs, xs);
         stats_.exchanges += 1;
         stats_.halo_bytes += (u64)(rows_bytes(0, k) + rows_bytes(1, k));
         // (full: also implies half 0's previous superstep, which ran on the same stream)
-        HIP_CHECK(hipEventRecord(ev_sub_x_, s_comp_));
-        HIP_CHECK(hipStreamWaitEvent(s_comm_, ev_sub_x_, 0));
+        HIP_CHECK(hipEventRecord(ev_sub_x_, xs));
+        HIP_CHECK(hipStreamWaitEvent(ov ? s_comp_ : s_comm_, ev_sub_x_, 0));
+        if (ov) launch_half(0, p, k, s_comp_, 0, 2);
     } else {
         wait_pending(s_comm_, ev_sub_a_);  // half 0's previous superstep is done
     }
@@ -189,7 +178,7 @@ void HipEngine::dual_superstep(int k) {
         for (int j = 0; j < np; ++j)
             for (int i = 0; i < 2; ++i) {
                 const int s = i;  // half 0's pass first (half 1 first measured no better: docs/PERFORMANCE.md §6)
-                if (!((ov || ov2) && j == 0)) {
+                if (!((ov && s == 0 && j == 0) || (ov2 && j == 0))) {
                     if (j == 0 && i == 0) trace::mark("gol.launch0");  // (GOL_ROCTX: host side of the launch latency)
                     launch_half(s, p, k, s ? s_comm_ : s_comp_, j);
                     if (j == 0 && i == 0) trace::mark("gol.launch0_done");
