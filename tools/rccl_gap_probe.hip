@@ -9,6 +9,10 @@
 //   2: A, exchange, event record, B
 //   3: A, exchange of 0 bytes (group with no ops), B
 //   4: A, a hipMemcpyAsync D2D of the same bytes, B   (a copy instead of RCCL)
+//   5: A, exchange, event (hipEventDisableSystemFence), B
+//   6: A, exchange, event (hipEventReleaseToDevice), B
+//   7: A, event (default), B                   (the event alone)
+//   8: A, event (hipEventDisableSystemFence), B
 //   build/rccl_gap_probe [bytes=81920]
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
@@ -53,20 +57,28 @@ int main(int argc, char** argv) {
     CK(hipMalloc(&rb, bytes));
     unsigned long long* st;
     CK(hipMalloc(&st, 64));
-    hipEvent_t ev;
+    hipEvent_t ev, ev_nf, ev_dev;
     CK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
-    const char* names[] = {"A, B", "A, exchange, B", "A, exchange, event, B", "A, empty group, B", "A, D2D copy, B"};
+    CK(hipEventCreateWithFlags(&ev_nf, hipEventDisableTiming | hipEventDisableSystemFence));
+    CK(hipEventCreateWithFlags(&ev_dev, hipEventDisableTiming | hipEventReleaseToDevice));
+    const char* names[] = {"A, B", "A, exchange, B", "A, exchange, event, B", "A, empty group, B", "A, D2D copy, B",
+                           "A, exchange, event nofence, B", "A, exchange, event device, B", "A, event, B",
+                           "A, event nofence, B"};
     printf("rccl_gap_probe: %zu bytes each way, NCCL %d\n", bytes, NCCL_VERSION_CODE);
-    for (int mode = 0; mode < 5; ++mode) {
+    for (int mode = 0; mode < 9; ++mode) {
         std::vector<double> d;
         for (int t = 0; t < 45; ++t) {
             hipLaunchKernelGGL(stamp, dim3(1), dim3(64), 0, s, st, 0);
-            if (mode == 1 || mode == 2) {
+            if (mode == 1 || mode == 2 || mode == 5 || mode == 6) {
                 NK(ncclGroupStart());
                 NK(ncclSend(sb, bytes, ncclChar, 0, comm, s));
                 NK(ncclRecv(rb, bytes, ncclChar, 0, comm, s));
                 NK(ncclGroupEnd());
                 if (mode == 2) CK(hipEventRecord(ev, s));
+                if (mode == 5) CK(hipEventRecord(ev_nf, s));
+                if (mode == 6) CK(hipEventRecord(ev_dev, s));
+            } else if (mode == 7 || mode == 8) {
+                CK(hipEventRecord(mode == 7 ? ev : ev_nf, s));
             } else if (mode == 3) {
                 NK(ncclGroupStart());
                 NK(ncclGroupEnd());
@@ -80,7 +92,7 @@ int main(int argc, char** argv) {
             if (t >= 4) d.push_back((double)(h[1] - h[0]) * 1e-2);  // 100 MHz ticks -> us
         }
         std::sort(d.begin(), d.end());
-        printf("%-26s B.start - A.start: min %7.2f med %7.2f p90 %7.2f us\n", names[mode], d[0], d[d.size() / 2],
+        printf("%-32s B.start - A.start: min %7.2f med %7.2f p90 %7.2f us\n", names[mode], d[0], d[d.size() / 2],
                d[d.size() * 9 / 10]);
     }
     NK(ncclCommDestroy(comm));
