@@ -112,11 +112,9 @@ HipEngine::HipEngine(const Geometry& g, const EngineConfig& c, std::shared_ptr<T
     // flight when it returns, would NOT be ordered before their kernels.)
     for (int i = 0; i < 2; ++i) HIP_CHECK(hipMemsetAsync(buf_[i], 0, bytes, s_comp_));
     HIP_CHECK(hipStreamSynchronize(s_comp_));
-    // Stream-ordering events (never read by the host).  (A device-scope release instead of the default
-    // system-scope fence measured no faster: docs/PERFORMANCE.md §5.)
-    const unsigned evf = hipEventDisableTiming;
-    HIP_CHECK(hipEventCreateWithFlags(&ev_ready_, evf));
-    HIP_CHECK(hipEventCreateWithFlags(&ev_halo_, evf));
+    // Stream-ordering events (never read by the host for data; event_flags: no system-scope fence)
+    HIP_CHECK(hipEventCreateWithFlags(&ev_ready_, event_flags()));
+    HIP_CHECK(hipEventCreateWithFlags(&ev_halo_, event_flags()));
     if (cfg_.profile) {
         for (auto* e : {&ev_t0_, &ev_t1_, &ev_t2_, &ev_t3_}) HIP_CHECK(hipEventCreate(e));
     }
@@ -124,7 +122,7 @@ HipEngine::HipEngine(const Geometry& g, const EngineConfig& c, std::shared_ptr<T
     HIP_CHECK(hipHostMalloc(&h_red_, 2 * sizeof(u64), hipHostMallocDefault));
     if (wd_)
         for (auto& m : mk_)
-            for (auto& e : m.ev) HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+            for (auto& e : m.ev) HIP_CHECK(hipEventCreateWithFlags(&e, event_flags()));
 }
 
 HipEngine::Marker& HipEngine::marker_slot() {

@@ -21,8 +21,8 @@ void HipEngine::setup_dual() {
         }
     }
     if (!ev_sub_own_[0]) {
-        for (auto& e : ev_sub_own_) HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-        HIP_CHECK(hipEventCreateWithFlags(&ev_sub_x_, hipEventDisableTiming));
+        for (auto& e : ev_sub_own_) HIP_CHECK(hipEventCreateWithFlags(&e, event_flags()));
+        HIP_CHECK(hipEventCreateWithFlags(&ev_sub_x_, event_flags()));
         ev_sub_a_ = ev_sub_own_[0];
         ev_sub_b_ = ev_sub_own_[1];
     }

@@ -602,6 +602,14 @@ class HipEngine : public Engine {
     u64* d_red_ = nullptr;
     u64* h_red_ = nullptr;
     bool device_transport_ = false;
+    // Flags of the engine's stream-ordering events: no system-scope fence when they are recorded (they
+    // order kernels of this device against each other; a kernel's own completion already makes its
+    // writes visible device-wide).  tools/rccl_gap_probe.hip: an event record between two kernels
+    // costs 1.7 us with the fence and 0.5 without, 4.6 vs 3.4 us behind RCCL's kernel
+    // (profiles/rccl_gap_probe.txt); a device-scope release saves nothing.  GOL_EVENT_FENCE=1 restores it.
+    unsigned event_flags() const {
+        return hipEventDisableTiming | (env_int("GOL_EVENT_FENCE", 0) != 0 ? 0u : (unsigned)hipEventDisableSystemFence);
+    }
     bool graph_ok_ = true;
     bool graph_rccl_on_ = false;  // one-tile supersteps with an RCCL exchange are captured (choose_schedule)
     bool sub_graphs_on_ = false;  // sub-tile passes replay per-half graphs (choose_schedule)
