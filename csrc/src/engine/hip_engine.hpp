@@ -606,9 +606,10 @@ class HipEngine : public Engine {
     // order kernels of this device against each other; a kernel's own completion already makes its
     // writes visible device-wide).  tools/rccl_gap_probe.hip: an event record between two kernels
     // costs 1.7 us with the fence and 0.5 without, 4.6 vs 3.4 us behind RCCL's kernel
-    // (profiles/rccl_gap_probe.txt); a device-scope release saves nothing.  GOL_EVENT_FENCE=1 restores it.
+    // (profiles/rccl_gap_probe.txt); a device-scope release saves nothing.  Opt-in (GOL_EVENT_FENCE=0)
+    // until the GPU suite and an engine A/B have run with it.
     unsigned event_flags() const {
-        return hipEventDisableTiming | (env_int("GOL_EVENT_FENCE", 0) != 0 ? 0u : (unsigned)hipEventDisableSystemFence);
+        return hipEventDisableTiming | (env_int("GOL_EVENT_FENCE", 1) != 0 ? 0u : (unsigned)hipEventDisableSystemFence);
     }
     bool graph_ok_ = true;
     bool graph_rccl_on_ = false;  // one-tile supersteps with an RCCL exchange are captured (choose_schedule)
