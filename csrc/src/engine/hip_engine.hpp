@@ -602,15 +602,11 @@ class HipEngine : public Engine {
     u64* d_red_ = nullptr;
     u64* h_red_ = nullptr;
     bool device_transport_ = false;
-    // Flags of the engine's stream-ordering events: no system-scope fence when they are recorded (they
-    // order kernels of this device against each other; a kernel's own completion already makes its
-    // writes visible device-wide).  tools/rccl_gap_probe.hip: an event record between two kernels
-    // costs 1.7 us with the fence and 0.5 without, 4.6 vs 3.4 us behind RCCL's kernel
-    // (profiles/rccl_gap_probe.txt); a device-scope release saves nothing.  Opt-in (GOL_EVENT_FENCE=0)
-    // until the GPU suite and an engine A/B have run with it.
-    unsigned event_flags() const {
-        return hipEventDisableTiming | (env_int("GOL_EVENT_FENCE", 1) != 0 ? 0u : (unsigned)hipEventDisableSystemFence);
-    }
+    // Flags of the engine's stream-ordering events.  (Without the system-scope fence an event record
+    // between two kernels costs 0.5 instead of 1.7 us, tools/rccl_gap_probe.hip, but the engine ran
+    // slower with such events: driver command 11.49-12.89 vs 11.11-11.57 us/gen, and the self-exchange
+    // cut lost its overlapped schedule, 13.5-13.8 vs 12.1-12.2; profiles/event_fence_ab.txt.)
+    static constexpr unsigned event_flags() { return hipEventDisableTiming; }
     bool graph_ok_ = true;
     bool graph_rccl_on_ = false;  // one-tile supersteps with an RCCL exchange are captured (choose_schedule)
     bool sub_graphs_on_ = false;  // sub-tile passes replay per-half graphs (choose_schedule)
