@@ -76,26 +76,9 @@ const DevPlan& HipEngine::sub_plan(int s, int k, i64 e, int part) {
     // A band (part 2) is a few rows tall and runs while little else does: its time is the serial
     // level pipeline of one wave, ~(S + K) x K row-levels for S rows per wave, so it is cut into
     // 4-row segments (K = 12, 28-row band: ~38 us as one segment per column, ~14 us in 4-row ones;
-    // 23 us measured in the driver-cut trace, profiles/kernel_trace_selfx_round4.txt).  With
-    // sub_band_tile_ the band runs on the LDS tile kernel instead: one workgroup of 8 waves per 62-word
-    // column holds the band and its 2K halo rows in LDS and steps them a generation at a time, so
-    // its time is K short LDS sweeps, not a K-deep row pipeline.
-    if (part == 2 && sub_band_tile_) {
-        const u32 tf = tile_bits(false);
-        const i64 band = rg[0].r1 - rg[0].r0;
-        if (band <= hipk::tile_max_rows(k, cfg_.tile_waves, sub_flags() | tf)) {
-            DevPlan p;
-            std::vector<LaneDesc> lanes = build_plan(rg, L.nw, L.h, band, k, true, &p.st, 1, cfg_.plan_xcds);
-            const std::string bad = validate_plan(lanes, L.nw, L.h, L.R, k, false);
-            if (!bad.empty()) throw Error(strprintf("refusing to launch an unsafe sub-tile band plan: %s", bad.c_str()));
-            p.waves = (i64)lanes.size() / kWaveLanes;  // (tiles: one workgroup each)
-            p.rows = band;
-            p.tflags = tf;
-            HIP_CHECK(hipMalloc(&p.d, lanes.size() * sizeof(LaneDesc)));
-            upload(p.d, lanes.data(), lanes.size() * sizeof(LaneDesc));
-            return sub_plans_.emplace(key, p).first->second;
-        }
-    }
+    // 23 us measured in the driver-cut trace, profiles/kernel_trace_selfx_round4.txt; the band on the
+    // LDS tile kernel instead, one workgroup per 62-word column, measured no faster end to end:
+    // profiles/selfx_band_and_order_ab.txt).
     // One round per half even on big tiles: the two halves' kernels already fill each other's tails
     // (131072^2: multi-round halves 141.9-142.4 vs 140.2-141.0 us/gen, profiles/bigboard_rounds.txt).
     const i64 rows = part == 2 ? 4
@@ -277,14 +260,7 @@ void HipEngine::launch_half(int s, int p, int k, hipStream_t st, int only, int p
         const int dsti = (j % 2 == 0) ? a : b;
         if (only < 0 || (int)j == only) {
             const DevPlan& pl = sub_plan(s, ps[j], ext_after(ps, j), j == 0 ? part : 0);
-            if (pl.tflags) {  // a band on the LDS tile kernel (sub_plan): its rows never reach the seam
-                hipk::StepParams spt = sp;
-                spt.flags |= pl.tflags;
-                hipk::launch_step_tile(cfg_.tile_waves, ps[j], sub_buf_[s][q], sub_buf_[s][dsti], pl.d, pl.waves, pl.rows,
-                                       spt, st);
-            } else {
-                hipk::launch_step(ps[j], sub_buf_[s][q], sub_buf_[s][dsti], pl.d, pl.waves, j == 0 ? sp0 : sp, st);
-            }
+            hipk::launch_step(ps[j], sub_buf_[s][q], sub_buf_[s][dsti], pl.d, pl.waves, j == 0 ? sp0 : sp, st);
         }
         q = dsti;
     }

@@ -197,9 +197,6 @@ class HipEngine : public Engine {
     const DevPlan& sub_plan(int s, int k, i64 e, int part = 0);
 
     u32 sub_flags() const { return step_flags() & ~hipk::STEP_WRAP_Y; }  // sub-tiles always have ghost rows
-    // GOL_SUB_BAND_TILE=1: the bands of a first pass split around the exchange (part 2) run on the LDS
-    // tile kernel instead of the register kernel in 4-row segments (opt-in until measured on the GPU)
-    const bool sub_band_tile_ = env_int("GOL_SUB_BAND_TILE", 0) != 0;
 
     // rows [r0, r0 + n) of sub-tile s in its buffer `par` (0..2; full pitch, contiguous)
     u64* sub_rows(int s, int par, i64 r0) { return sub_buf_[s][par] + sub_L_[s].index(r0, -1); }
