@@ -561,8 +561,8 @@ static void test_plan_rounds() {
 
 // Age-weighted plans (build_plan age_weights): the plan still covers every output word exactly once,
 // fits the same waves, and the first-dispatched third of the grid gets the tallest segments.
-// The sub-tile overlap's band on the tile kernel (engine_hip_subtiles.hip sub_plan part 2): one tile
-// per 62-word column of a band with ghost rows above it, every output word once, inside the halo.
+// A band with ghost rows above (or below) it as a tile-kernel plan (one tile per 62-word column; the
+// shape of the sub-tile overlap's band, docs/PERFORMANCE.md §11): every output word once, inside the halo.
 static void test_band_tile_plan() {
     for (const auto& c : std::vector<std::tuple<i64, i64, int, i64>>{{16384, 512, 12, 8}, {16384, 512, 8, 0}, {4096, 100, 12, 8}}) {
         const i64 h = std::get<0>(c), nw = std::get<1>(c), e = std::get<3>(c);
