@@ -38,7 +38,7 @@ __device__ __forceinline__ void store_row_word(uint2* p, u32 lo, u32 hi) {
 // load_row_word<false>: routing the plain loads through the helper changed the K = 12 kernel's
 // schedule — 256 VGPRs with AGPR spills and a vmcnt(0) before the stores in the row loop, the pass
 // 119 -> 163 us at 32768^2 — although the helper inlines to the same load.)
-#define GOL_ROW_LOAD(dst)                            \
+#define ROW_LOAD_INTO(dst)                            \
     do {                                             \
         if constexpr (COH)                           \
             (dst) = load_row_word<true>(ld);         \
@@ -130,7 +130,7 @@ struct WaveRunner {
         st_stride = out ? p.pitch : 0;
 #pragma unroll
         for (int j = 0; j < D; ++j) {
-            GOL_ROW_LOAD(pf[j]);
+            ROW_LOAD_INTO(pf[j]);
             next_row();
         }
     }
@@ -141,12 +141,12 @@ struct WaveRunner {
         uint2 x;
         if constexpr (D == 3) {
             x = pf[PH];
-            GOL_ROW_LOAD(pf[PH]);  // prefetch 3 rows ahead (the allocation has slack rows past the halo)
+            ROW_LOAD_INTO(pf[PH]);  // prefetch 3 rows ahead (the allocation has slack rows past the halo)
         } else {
             x = pf[0];  // a queue of D rows (the shift is register renaming in the unrolled code)
 #pragma unroll
             for (int j = 0; j + 1 < D; ++j) pf[j] = pf[j + 1];
-            GOL_ROW_LOAD(pf[D - 1]);
+            ROW_LOAD_INTO(pf[D - 1]);
         }
         next_row();
         lo = x.x;
@@ -183,7 +183,7 @@ struct WaveRunner {
             // queue shift of the fill phase collapses the prefetch distance to one triple).
 #define ROW6_STEP(J)                                          \
     compute_store<(J) % 3, false>(pf[J].x, pf[J].y, i + (J)); \
-    GOL_ROW_LOAD(pf[J]);                                             \
+    ROW_LOAD_INTO(pf[J]);                                             \
     next_row();                                              \
     __builtin_amdgcn_sched_barrier(0);
             for (; i + 6 <= n; i += 6) {
@@ -205,21 +205,21 @@ struct WaveRunner {
                 // issued, s_waitcnt vmcnt(0), and the prefetch is lost.)
                 uint2 q[3];
                 for (; i + 6 <= n; i += 6) {
-                    GOL_ROW_LOAD(q[0]);
+                    ROW_LOAD_INTO(q[0]);
                     next_row();
-                    GOL_ROW_LOAD(q[1]);
+                    ROW_LOAD_INTO(q[1]);
                     next_row();
-                    GOL_ROW_LOAD(q[2]);
+                    ROW_LOAD_INTO(q[2]);
                     next_row();
                     __builtin_amdgcn_sched_barrier(0);
                     compute_store<0, false>(pf[0].x, pf[0].y, i);
                     compute_store<1, false>(pf[1].x, pf[1].y, i + 1);
                     compute_store<2, false>(pf[2].x, pf[2].y, i + 2);
-                    GOL_ROW_LOAD(pf[0]);
+                    ROW_LOAD_INTO(pf[0]);
                     next_row();
-                    GOL_ROW_LOAD(pf[1]);
+                    ROW_LOAD_INTO(pf[1]);
                     next_row();
-                    GOL_ROW_LOAD(pf[2]);
+                    ROW_LOAD_INTO(pf[2]);
                     next_row();
                     __builtin_amdgcn_sched_barrier(0);
                     compute_store<0, false>(q[0].x, q[0].y, i + 3);
@@ -230,11 +230,11 @@ struct WaveRunner {
             for (; i + 3 <= n; i += 3) {
                 // hoist the whole next triple's loads above this triple's compute
                 const uint2 x0 = pf[0], x1 = pf[1], x2 = pf[2];
-                GOL_ROW_LOAD(pf[0]);
+                ROW_LOAD_INTO(pf[0]);
                 next_row();
-                GOL_ROW_LOAD(pf[1]);
+                ROW_LOAD_INTO(pf[1]);
                 next_row();
-                GOL_ROW_LOAD(pf[2]);
+                ROW_LOAD_INTO(pf[2]);
                 next_row();
                 __builtin_amdgcn_sched_barrier(0);
                 compute_store<0, false>(x0.x, x0.y, i);
