@@ -5,9 +5,10 @@
 // whole superstep is one launch of a persistent grid: the passes' plan waves become work items in one
 // ticket order, and each item waits only for the items of the previous pass it reads from or
 // overwrites (plan.hpp build_flow_plan).  With neighbours the exchange runs first on the compute
-// stream (the "full" schedule: the first pass reads the ghost rows it wrote).  The mode is a
-// candidate of the schedule timing ("local+flow" / "full+flow", engine_hip_tune.hip), so the
-// measured rate decides whether a run uses it.
+// stream (the "full" schedule: the first pass reads the ghost rows it wrote), or ("flow+ov") on the
+// comm stream while the launch's interior items run.  Opt-in (GOL_SCHEDULE=flow|flow+ov forces it,
+// GOL_FLOW=1 makes it a candidate of the schedule timing, engine_hip_tune.hip): it measured slower
+// than the pass schedules on every configuration (docs/PERFORMANCE.md §15).
 // Reference: the generation loop gol-main.c:93-116, one launch + device sync per generation in
 // gol-with-cuda.cu:264-284.
 #include <algorithm>
