@@ -13,6 +13,9 @@
 //   6: A, exchange, event (hipEventReleaseToDevice), B
 //   7: A, event (default), B                   (the event alone)
 //   8: A, event (hipEventDisableSystemFence), B
+//   9: A, exchange, hipStreamWriteValue32, B
+//  10: A, hipStreamWriteValue32, B
+//  11: A, hipStreamWaitValue32 on a value already written, B
 //   build/rccl_gap_probe [bytes=81920]
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
@@ -63,13 +66,17 @@ int main(int argc, char** argv) {
     CK(hipEventCreateWithFlags(&ev_dev, hipEventDisableTiming | hipEventReleaseToDevice));
     const char* names[] = {"A, B", "A, exchange, B", "A, exchange, event, B", "A, empty group, B", "A, D2D copy, B",
                            "A, exchange, event nofence, B", "A, exchange, event device, B", "A, event, B",
-                           "A, event nofence, B"};
+                           "A, event nofence, B", "A, exchange, write value, B", "A, write value, B",
+                           "A, wait value (satisfied), B"};
     printf("rccl_gap_probe: %zu bytes each way, NCCL %d\n", bytes, NCCL_VERSION_CODE);
-    for (int mode = 0; mode < 9; ++mode) {
+        unsigned* flag = nullptr;
+    CK(hipMalloc(&flag, 256));
+    CK(hipMemset(flag, 0, 256));
+    for (int mode = 0; mode < 12; ++mode) {
         std::vector<double> d;
         for (int t = 0; t < 45; ++t) {
             hipLaunchKernelGGL(stamp, dim3(1), dim3(64), 0, s, st, 0);
-            if (mode == 1 || mode == 2 || mode == 5 || mode == 6) {
+            if (mode == 1 || mode == 2 || mode == 5 || mode == 6 || mode == 9) {
                 NK(ncclGroupStart());
                 NK(ncclSend(sb, bytes, ncclChar, 0, comm, s));
                 NK(ncclRecv(rb, bytes, ncclChar, 0, comm, s));
@@ -77,6 +84,11 @@ int main(int argc, char** argv) {
                 if (mode == 2) CK(hipEventRecord(ev, s));
                 if (mode == 5) CK(hipEventRecord(ev_nf, s));
                 if (mode == 6) CK(hipEventRecord(ev_dev, s));
+                if (mode == 9) CK(hipStreamWriteValue32(s, flag, (unsigned)t + 1u, 0));
+            } else if (mode == 10) {
+                CK(hipStreamWriteValue32(s, flag, (unsigned)t + 1u, 0));
+            } else if (mode == 11) {
+                CK(hipStreamWaitValue32(s, flag, 0u, hipStreamWaitValueGte, 0xFFFFFFFFu));
             } else if (mode == 7 || mode == 8) {
                 CK(hipEventRecord(mode == 7 ? ev : ev_nf, s));
             } else if (mode == 3) {
