@@ -482,7 +482,9 @@ void HipEngine::autotune_kernel() {
     // when the schedule timing then picks "split", the interior / boundary kernels are tuned below
     // and the later passes run step_temporal at the measured depths.)
     if (!cfg_.compat && cfg_.kernel_depth == 0 && env_int("GOL_PIPE_TUNE", 1) != 0) {
-        const int geo[][3] = {{9, 3, 2}, {13, 2, 1}, {13, 3, 1}, {9, 2, 2}};
+        // ({16, 2, 1}: 15 waves x 2 levels, one workgroup per CU, the fastest geometry on config 3's
+        // per-rank strip, 4096 x 32768: 2.10 vs 2.17 us/gen for {9, 3, 2}; profiles/strip_pipe_sweep.txt)
+        const int geo[][3] = {{9, 3, 2}, {13, 2, 1}, {13, 3, 1}, {9, 2, 2}, {16, 2, 1}};
         for (const auto& g : geo) {
             const int k = (g[0] - 1) * g[1];
             if (k <= L_.R && hipk::pipe_supported(g[0], g[1])) cands.push_back({"pipe", k, nw0, 0, g[0], g[1], g[2]});
