@@ -510,6 +510,24 @@ void HipEngine::autotune_kernel() {
             if (cands[i].pnw) set_pipe(cands[i].pnw, cands[i].pl, cands[i].pwg);
             tbest[i] = std::min(tbest[i], time_pass(0, cands[i].kern, cands[i].k));
         }
+    // Near-ties (within 2% of the best) get four more interleaved rounds: on config 3's strip the
+    // 15x2 and 8x3 step_pipe geometries time within 1-3% of each other, and one 3-round sample
+    // picked the slower one in one init of two (2.17 vs 2.10 us/gen in the run;
+    // profiles/strip_pipe_sweep.txt).
+    {
+        const float b0 = *std::min_element(tbest.begin(), tbest.end());
+        std::vector<size_t> close;
+        for (size_t i = 0; i < cands.size(); ++i)
+            if (tbest[i] <= 1.02f * b0) close.push_back(i);
+        if (close.size() > 1)
+            for (int round = 0; round < 4; ++round)
+                for (size_t i : close) {
+                    cfg_.tile_waves = cands[i].nw;
+                    occ_ = cands[i].occ;
+                    if (cands[i].pnw) set_pipe(cands[i].pnw, cands[i].pl, cands[i].pwg);
+                    tbest[i] = std::min(tbest[i], time_pass(0, cands[i].kern, cands[i].k));
+                }
+    }
     float best = 1e30f;
     Cand pick = cands[0];
     for (size_t i = 0; i < cands.size(); ++i)
