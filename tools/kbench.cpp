@@ -104,7 +104,8 @@ int main(int argc, char** argv) {
     // are meaningless; only the time is.
     // KB_SPLIT2=n (temporal only; 1 means 2): the board as n equal row bands, each with its own
     // one-round plan sized for the whole GPU, launched on n streams with no cross-stream ordering.
-    const int nsplit = (tile_nw == 0 && getenv("KB_SPLIT2")) ? std::max(0, atoi(getenv("KB_SPLIT2"))) : 0;
+    // (with KB_PIPE: each band runs step_pipe, its plan sized for KB_PIPE_WG workgroups per CU)
+    const int nsplit = ((tile_nw == 0 || pipe_l > 0) && getenv("KB_SPLIT2")) ? std::max(0, atoi(getenv("KB_SPLIT2"))) : 0;
     const bool split2 = nsplit > 0;
     const int nparts = nsplit == 1 ? 2 : nsplit;
     std::vector<LaneDesc*> dplan2(std::max(nparts, 1), nullptr);
@@ -115,9 +116,10 @@ int main(int argc, char** argv) {
             std::vector<Region> r2 = {{h * (N / nparts), h == nparts - 1 ? N : (h + 1) * (N / nparts), 0, L.nw}};
             i64 bpc = hipk::step_blocks_per_cu(K, flags);
             if (getenv("KB_BPC")) bpc = std::min<i64>(bpc, atoi(getenv("KB_BPC")));
-            const i64 rr = balanced_rows_per_chunk(r2, L.nw, N, K, bpc * kWavesPerBlock * prop.multiProcessorCount, 2 * K, true);
+            const i64 rr = pipe_l > 0 ? balanced_rows_per_chunk(r2, L.nw, N, K, (i64)pipe_wg * prop.multiProcessorCount, 1, true)
+                                      : balanced_rows_per_chunk(r2, L.nw, N, K, bpc * kWavesPerBlock * prop.multiProcessorCount, 2 * K, true);
             PlanStats st2;
-            std::vector<LaneDesc> l2 = build_plan(r2, L.nw, N, rr, K, true, &st2, kWavesPerBlock, xcds);
+            std::vector<LaneDesc> l2 = build_plan(r2, L.nw, N, rr, K, true, &st2, pipe_l > 0 ? 1 : kWavesPerBlock, xcds);
             CK(hipMalloc(&dplan2[h], l2.size() * sizeof(LaneDesc)));
             CK(hipMemcpy(dplan2[h], l2.data(), l2.size() * sizeof(LaneDesc), hipMemcpyHostToDevice));
             waves2[h] = st2.waves;
@@ -126,7 +128,11 @@ int main(int argc, char** argv) {
     }
     auto launch = [&](const u64* s, u64* d) {
         if (split2) {
-            for (int h = 0; h < nparts; ++h) hipk::launch_step(K, s, d, dplan2[h], waves2[h], sp, ss[h]);
+            for (int h = 0; h < nparts; ++h)
+                if (pipe_l > 0)
+                    hipk::launch_step_pipe(tile_nw, pipe_l, s, d, dplan2[h], waves2[h], sp, ss[h]);
+                else
+                    hipk::launch_step(K, s, d, dplan2[h], waves2[h], sp, ss[h]);
         } else if (pipe_l > 0)
             hipk::launch_step_pipe(tile_nw, pipe_l, s, d, dplan, st.waves, sp, 0);
         else if (tile_nw > 0)
