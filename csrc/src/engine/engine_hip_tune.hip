@@ -191,6 +191,11 @@ void HipEngine::choose_schedule() {
         const int reps = short_run ? 1 : kSchedReps;
         const int rounds = short_run ? 15 : 3;
         std::vector<double> best(cands.size(), 1e30);
+        // (a short run is ONE superstep, a single sample of its latency: the candidates are ranked by
+        // their median round there, not their best one, which favoured a candidate of wide spread --
+        // full+graph timed 12.6 against subtiles+ov's 12.3-12.5 us/gen at best, won one init in five,
+        // and that run measured 13.4 against 12.0-12.4 us/gen, driver's cut through the self-exchange)
+        std::vector<std::vector<double>> samples(cands.size());
         // flow supersteps of tile items run the whole hinted run as one launch (flow_superstep_depth):
         // every candidate is then timed over that many generations, the others as whole supersteps of k
         // (timed on 4 x 32 generations against one 1000-generation launch, the local candidate paid four
@@ -212,7 +217,14 @@ void HipEngine::choose_schedule() {
                 time_schedule(cands[c], kc, rc);
                 synchronize();
                 const double dt = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
-                best[c] = std::min(best[c], t_->allreduce_max(dt) * 1e6 / (rc * kc));
+                const double us = t_->allreduce_max(dt) * 1e6 / (rc * kc);
+                samples[c].push_back(us);
+                best[c] = std::min(best[c], us);
+                if (short_run) {
+                    std::vector<double> v = samples[c];
+                    std::sort(v.begin(), v.end());
+                    best[c] = v[(v.size() - 1) / 2];
+                }
                 // a flow launch whose wait timed out (clears the fault word): the candidate is dropped
                 if (fl && flow_ctl_ && hipk::flow_fault(flow_ctl_, s_comp_)) {
                     fprintf(stderr, "[gol] rank %d: schedule candidate %s: a flow wait timed out (dropped)\n", g_.rank,
