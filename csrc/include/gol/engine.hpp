@@ -61,8 +61,6 @@ struct EngineConfig {
     int graph_rccl = -1;              // one-tile supersteps whose exchange is an RCCL group, captured in
                                       // hipGraphs (GOL_GRAPH_RCCL: 1 on, 0 off, -1 = a candidate of the
                                       // init-time schedule timing, "full+graph")
-    int subtile_graphs = -1;          // sub-tile passes replayed from per-half hipGraphs (GOL_SUBTILE_GRAPHS:
-                                      // 1 on, 0 off, -1 = a timed candidate, "subtiles+graph")
     int subtile_overlap = -1;         // sub-tiles with neighbours: half 0 starts its first pass (all but
                                       // its band next to the rank's north halo) while the exchange is in
                                       // flight (GOL_SUBTILE_OVERLAP: 1 on, 0 off, -1 = a candidate of the
@@ -75,8 +73,7 @@ struct EngineConfig {
                                       // one rank (e.g. a 1-rank RCCL communicator)
     double watchdog_s = 0;            // abort the job after this long without progress (0 = off)
     bool force_split = false;         // run the interior/boundary edge schedule even without neighbours
-    std::string sched = "auto";       // auto (timed at init) | split (overlap, with neighbours) | full | flow
-                                      // (one dependency-driven launch per superstep, step_flow)
+    std::string sched = "auto";       // auto (timed at init) | split (overlap, with neighbours) | full
 };
 
 struct EngineStats {

@@ -106,57 +106,6 @@ int pipe_blocks_per_cu(int nw, int L, bool wrapy);
 bool pipe_fault();
 void launch_step_pipe(int nw, int L, const u64* src, u64* dst, const LaneDesc* plan, i64 n_tiles, const StepParams& p,
                       hipStream_t s);
-// step_flow (flow_kernel.hip): a superstep of several step_temporal passes as ONE launch of a
-// persistent grid whose waves draw the items of a flow plan (plan.hpp build_flow_plan) in ticket
-// order and wait for each item's dependencies through per-item completion flags.
-// Every word the kernel's waves contend for sits in a 128-byte line of its own (a same-line poll
-// doubles the cost of the atomics: tools/ticket_probe.hip, profiles/ticket_probe.txt).
-constexpr int kFlowSeqs = 8;  // ticket sequences: one per XCD
-struct FlowCtl {  // device memory, zero-initialised once
-    // Ticket counters: launch e (FlowArgs::epoch = e) draws from next[e & 1][its sequence] and zeroes
-    // next[(e + 1) & 1] for launch e + 1 (launch e - 1, which used them, has completed: stream order).
-    u32 next[2][kFlowSeqs][32];
-    u32 fault;  // a dependency wait timed out: the board is invalid
-    u32 pad0[31];
-    u32 exch;   // exchange-overlapped launches: set to the launch's epoch by the comm stream once the
-                // halo exchange of its superstep is complete (hipStreamWriteValue32); the items marked
-                // FLOW_ITEM_EXCH wait for it
-    u32 pad1[31];
-};
-struct FlowArgs {
-    u64* a;                  // even passes read a and write b, odd passes the reverse
-    u64* b;
-    const LaneDesc* lanes;   // n_items x 64
-    const FlowItem* items;
-    const u32* deps;
-    u32* flags;              // n_items completion flags (zero-initialised once per plan); an item's flag
-                             // holds the epoch of the launch that completed it last
-    FlowCtl* ctl;
-    u32 n_items;
-    u32 epoch;               // this launch's number (host-counted per control block, from 1; never 0)
-    u32 nseq;                // ticket sequences: kFlowSeqs (item t belongs to sequence t % nseq, drawn by
-                             // the waves of XCD t % nseq) or 1 (one global sequence, any residency)
-    u32 variant;             // host-side kernel choice: bit 0 draws each wave's next ticket at the start
-                             // of its current item (wave items only)
-};
-bool flow_depth_supported(int k);
-int flow_max_depth();
-// Resident 256-thread workgroups per CU of the flow kernel (its persistent grid is this x CUs).
-int flow_blocks_per_cu(u32 flags);
-void launch_step_flow(const FlowArgs& a, i64 n_blocks, const StepParams& p, hipStream_t s);
-// The same with LDS tile items (step_tile / step_tile_fold's device code, one workgroup of `nw_per_wg`
-// waves per item; `rows` the largest chunk height and `kmax` the deepest pass of the plan, which size
-// the dynamic LDS).  p.flags carries the tile variant (STEP_TILE_FOLD, _INPLACE, _L2/_L4); supported:
-// nw_per_wg 8, double-buffered with 4 generations per LDS pass or in place with 2.
-bool flow_tile_supported(int nw_per_wg, u32 flags);
-// Most rows a flow tile item may hold at depth k (the tile kernel's capacity less the ticket slot).
-i64 flow_tile_max_rows(int k, int nw_per_wg, u32 flags);
-int flow_tile_blocks_per_cu(int nw_per_wg, i64 rows, int kmax, u32 flags);
-void launch_step_flow_tile(int nw_per_wg, const FlowArgs& a, i64 n_blocks, i64 rows, int kmax, const StepParams& p,
-                           hipStream_t s);
-// True (and cleared, with every ticket counter) when a wait of a flow launch timed out since the last
-// call (synchronises s).
-bool flow_fault(FlowCtl* ctl, hipStream_t s);
 // Single-generation LDS-tiled kernel over output rows [r0, r1) (all words).
 void launch_step_lds(const u64* src, u64* dst, const Layout& L, i64 r0, i64 r1, u32 flags, hipStream_t s);
 

@@ -104,47 +104,6 @@ i64 balanced_rows_per_chunk(const std::vector<Region>& regions, i64 nw, i64 h, i
 i64 round_balanced_rows(const std::vector<Region>& regions, i64 nw, i64 h, int k, i64 resident_waves, i64 min_rows,
                         bool xwrap, i64 round_rows, i64 max_rounds = 32);
 
-// ---- flow plans (hip_kernels.hpp step_flow): a superstep's passes as one ticket-ordered item list ----
-// One item per plan wave of each pass.  The pass j items depend on the pass j - 1 items that write a
-// (row, word column) one of their lanes reads (read-after-write), and on those that read a (row,
-// column) one of their store lanes writes (write-after-read: passes alternate between two buffers, so
-// pass j overwrites what pass j - 1 read).  Writes of pass j - 2 to the same buffer are ordered
-// transitively (every cell pass j writes was read, as a centre, by the pass j - 1 item that waited for
-// its pass j - 2 writer).  Every dependency has a smaller ticket than its dependant.
-enum : u32 {
-    FLOW_ITEM_EXCH = 1u << 31,  // FlowItem::pass bit: reads ghost cells the superstep's exchange writes
-};
-struct FlowItem {
-    u32 depth;    // generations of the item's pass
-    u32 pass;     // pass index (even: reads buffer a, odd: buffer b), | FLOW_ITEM_EXCH
-    u32 dep_off;  // dependencies: deps[dep_off .. dep_off + ndeps)
-    u32 ndeps;
-};
-struct FlowPass {
-    int k;                        // generations
-    std::vector<Region> regions;  // output regions (tile coordinates, ghost rows/words allowed)
-    i64 rows;                     // segment height of its plan
-    bool fold = false;            // LDS tile items with folded 32-lane tiles (build_plan fold)
-};
-struct FlowPlan {
-    std::vector<LaneDesc> lanes;  // items x 64, in ticket order
-    std::vector<FlowItem> items;
-    std::vector<u32> deps;
-    std::vector<u32> pass_begin;  // first item of each pass, then the item count
-    PlanStats st;                 // summed over the passes
-    u32 max_deps = 0;
-};
-// Build the flow plan of `passes` over a tile of nw words x h rows.  xwrap: the tile is its own E/W
-// neighbour (halo lanes stream the wrapped words); wrap_y: its own N/S neighbour (rows modulo h; each
-// pass then starts one band of the previous pass further down, so its first items depend on the
-// previous pass's first ones).  Returns an empty string or a description of an inconsistency.
-// mark_exch: the first pass's items that read a cell outside the tile (ghost rows / words the halo
-// exchange writes) get FLOW_ITEM_EXCH, and every pass orders its items from the middle of the tile
-// outwards, so the interior runs while the exchange is in flight and the bands next to the halos come
-// last (without it and without wrap_y, bands run top to bottom).
-std::string build_flow_plan(const std::vector<FlowPass>& passes, i64 nw, i64 h, bool xwrap, bool wrap_y, FlowPlan& out,
-                            bool mark_exch = false);
-
 // Neighbour tiles of a resident plan (hip_kernels.hpp step_resident: one plan wave = one tile, kept
 // by one workgroup for a whole run).  Tile t reads, for each of its lanes, rows [row0-k, row0+nrows+k)
 // of the lane's word column (modulo h with wrap_y); its neighbours are the OTHER tiles whose store

@@ -264,7 +264,6 @@ PYBIND11_MODULE(_gol, m) {
         .def_readwrite("sched", &EngineConfig::sched)
         .def_readwrite("kernel_depth", &EngineConfig::kernel_depth)
         .def_readwrite("graph_rccl", &EngineConfig::graph_rccl)
-        .def_readwrite("subtile_graphs", &EngineConfig::subtile_graphs)
         .def_readwrite("plan_xcds", &EngineConfig::plan_xcds);
 
     py::class_<Engine>(m, "Engine")

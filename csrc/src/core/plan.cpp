@@ -307,145 +307,6 @@ std::string validate_plan(const std::vector<LaneDesc>& lanes, i64 nw, i64 h, int
     return "";
 }
 
-std::string build_flow_plan(const std::vector<FlowPass>& passes, i64 nw, i64 h, bool xwrap, bool wrap_y, FlowPlan& out,
-                            bool mark_exch) {
-    out = FlowPlan();
-    if (passes.empty()) return "no passes";
-    // per word column (col + 1 in [0, nw + 2)): the previous pass's written and read row intervals
-    struct Iv {
-        i64 a, b;
-        u32 item;
-    };
-    using Cols = std::vector<std::vector<Iv>>;
-    const size_t ncols = (size_t)nw + 2;
-    Cols prev_w(ncols), prev_r(ncols);
-    i64 prev_wlen = 0, prev_rlen = 0;  // longest interval of each kind (binary-search window)
-    // [a, b) as pieces inside [0, h) (wrap_y), or as is
-    auto pieces = [&](i64 a, i64 b, std::vector<std::pair<i64, i64>>& v) {
-        v.clear();
-        if (b <= a) return;
-        if (!wrap_y) {
-            v.push_back({a, b});
-            return;
-        }
-        if (b - a >= h) {
-            v.push_back({0, h});
-            return;
-        }
-        const i64 a0 = pmod(a, h), b0 = a0 + (b - a);
-        if (b0 <= h) {
-            v.push_back({a0, b0});
-        } else {
-            v.push_back({a0, h});
-            v.push_back({0, b0 - h});
-        }
-    };
-    auto query = [](const std::vector<Iv>& col, i64 maxlen, i64 a, i64 b, std::vector<u32>& hit) {
-        auto it = std::lower_bound(col.begin(), col.end(), a - maxlen, [](const Iv& x, i64 v) { return x.a < v; });
-        for (; it != col.end() && it->a < b; ++it)
-            if (it->b > a) hit.push_back(it->item);
-    };
-    std::vector<std::pair<i64, i64>> pv;
-    i64 offset = 0;
-    for (size_t j = 0; j < passes.size(); ++j) {
-        const FlowPass& ps = passes[j];
-        if (ps.k < 1) return strprintf("pass %zu: depth %d", j, ps.k);
-        PlanStats st;
-        const std::vector<LaneDesc> L = build_plan(ps.regions, nw, h, ps.rows, ps.k, xwrap, &st, 1, 1, ps.fold);
-        out.st.waves += st.waves;
-        out.st.active_lanes += st.active_lanes;
-        out.st.lane_rows += st.lane_rows;
-        out.st.out_words += st.out_words;
-        // ticket order inside the pass: row bands down the board (with the torus wrap starting at
-        // `offset`, one band of the previous pass below its start); a wave holding several narrow
-        // segments sorts by its lowest band.  mark_exch: bands from the middle of the tile outwards
-        // (the key is minus the distance to the nearer edge of the pass's rows)
-        std::vector<std::pair<i64, size_t>> order;
-        i64 rlo = std::numeric_limits<i64>::max(), rhi = std::numeric_limits<i64>::min();
-        for (const Region& r : ps.regions)
-            if (r.r1 > r.r0 && r.c1 > r.c0) rlo = std::min(rlo, r.r0), rhi = std::max(rhi, r.r1);
-        for (size_t w = 0; w < L.size() / kWaveLanes; ++w) {
-            const LaneDesc* d = &L[w * kWaveLanes];
-            if (d[0].nrows <= 0) continue;  // padding wave: no item
-            i64 key = std::numeric_limits<i64>::min();
-            for (int l = 0; l < kWaveLanes; ++l) {
-                const i64 r0 = d[l].row0, r1 = r0 + d[l].nrows;
-                const i64 kk = mark_exch && !wrap_y ? -std::min(r0 - rlo, rhi - r1) : (wrap_y ? pmod(r0 - offset, h) : r0);
-                key = std::max<i64>(key, kk);
-            }
-            order.push_back({key, w});
-        }
-        std::stable_sort(order.begin(), order.end(),
-                         [](const std::pair<i64, size_t>& x, const std::pair<i64, size_t>& y) { return x.first < y.first; });
-        out.pass_begin.push_back((u32)out.items.size());
-        Cols cur_w(ncols), cur_r(ncols);
-        i64 cur_wlen = 0, cur_rlen = 0;
-        std::vector<u32> hit;
-        for (const auto& ow : order) {
-            const u32 id = (u32)out.items.size();
-            const LaneDesc* d = &L[ow.second * kWaveLanes];
-            FlowItem fi{(u32)ps.k, (u32)j, (u32)out.deps.size(), 0u};
-            if (mark_exch && j == 0) {
-                bool ghost = false;
-                for (int l = 0; l < kWaveLanes; ++l) {
-                    const LaneDesc& x = d[l];
-                    if (x.nrows <= 0) continue;
-                    ghost = ghost || x.col < 0 || x.col >= nw ||
-                            (!wrap_y && ((i64)x.row0 - ps.k < 0 || (i64)x.row0 + x.nrows + ps.k > h));
-                }
-                if (ghost) fi.pass |= FLOW_ITEM_EXCH;
-            }
-            hit.clear();
-            for (int l = 0; l < kWaveLanes; ++l) {
-                const LaneDesc& x = d[l];
-                if (x.col < -1 || x.col > nw) return strprintf("pass %zu: lane column %d outside [-1, nw]", j, x.col);
-                const size_t c = (size_t)(x.col + 1);
-                const bool store = x.flags & LANE_STORE;
-                if (j > 0) {
-                    // read-after-write: the rows this lane streams, written by pass j - 1
-                    pieces((i64)x.row0 - ps.k, (i64)x.row0 + x.nrows + ps.k, pv);
-                    for (const auto& q : pv) query(prev_w[c], prev_wlen, q.first, q.second, hit);
-                    // write-after-read: the rows it stores, read by pass j - 1
-                    if (store) {
-                        pieces(x.row0, (i64)x.row0 + x.nrows, pv);
-                        for (const auto& q : pv) query(prev_r[c], prev_rlen, q.first, q.second, hit);
-                    }
-                }
-                pieces((i64)x.row0 - ps.k, (i64)x.row0 + x.nrows + ps.k, pv);
-                for (const auto& q : pv) {
-                    cur_r[c].push_back({q.first, q.second, id});
-                    cur_rlen = std::max(cur_rlen, q.second - q.first);
-                }
-                if (store) {
-                    pieces(x.row0, (i64)x.row0 + x.nrows, pv);
-                    for (const auto& q : pv) {
-                        cur_w[c].push_back({q.first, q.second, id});
-                        cur_wlen = std::max(cur_wlen, q.second - q.first);
-                    }
-                }
-            }
-            std::sort(hit.begin(), hit.end());
-            hit.erase(std::unique(hit.begin(), hit.end()), hit.end());
-            for (u32 dep : hit)
-                if (dep >= id) return strprintf("pass %zu item %u depends on item %u (not earlier)", j, id, dep);
-            fi.ndeps = (u32)hit.size();
-            out.deps.insert(out.deps.end(), hit.begin(), hit.end());
-            out.max_deps = std::max(out.max_deps, fi.ndeps);
-            out.items.push_back(fi);
-            out.lanes.insert(out.lanes.end(), d, d + kWaveLanes);
-        }
-        for (auto* cols : {&cur_w, &cur_r})
-            for (auto& v : *cols) std::sort(v.begin(), v.end(), [](const Iv& x, const Iv& y) { return x.a < y.a; });
-        prev_w.swap(cur_w);
-        prev_r.swap(cur_r);
-        prev_wlen = cur_wlen;
-        prev_rlen = cur_rlen;
-        if (wrap_y) offset = pmod(offset + std::max<i64>(1, ps.rows), h);
-    }
-    out.pass_begin.push_back((u32)out.items.size());
-    return "";
-}
-
 std::string resident_neighbours(const std::vector<LaneDesc>& lanes, i64 nw, i64 h, int k, bool wrap_y,
                                 std::vector<u32>& off, std::vector<u32>& idx) {
     if (lanes.size() % kWaveLanes) return "lane count is not a multiple of 64";

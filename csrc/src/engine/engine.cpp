@@ -197,7 +197,7 @@ void Engine::maybe_inject_fault() {
 }
 
 void Engine::run(u64 generations) {
-    trace::Range range("gol.run");
+    trace::Range range("gol.eager");  // (the HIP engine's run() opens "gol.run" before its graph replays)
     Armed armed(wd_.get());
     while (generations > 0) {
         maybe_inject_fault();

@@ -104,8 +104,6 @@ HipEngine::HipEngine(const Geometry& g, const EngineConfig& c, std::shared_ptr<T
     HIP_CHECK(hipStreamCreateWithPriority(&s_comp_, hipStreamNonBlocking, 0));
     HIP_CHECK(hipStreamCreateWithPriority(&s_comm_, hipStreamNonBlocking,
                                           prio_greatest));
-    s_base_ = s_comp_;
-    engines_on_device(dev_, this, +1);
     events_needed_ = cfg_.force_split || !halo_items(L_.R).empty();
     // All device memory work is ordered on the engine's own streams.  (They are non-blocking:
     // null-stream calls such as hipMemset, or a pageable hipMemcpy whose DMA may still be in
@@ -182,7 +180,6 @@ HipEngine::~HipEngine() {
     wd_.reset();  // its thread calls probe(), which reads the members destroyed below
     hipStreamSynchronize(s_comp_);
     hipStreamSynchronize(s_comm_);
-    destroy_dual_graphs();
     for (auto& kv : sub_plans_) hipFree(kv.second.d);
     for (auto& sb : sub_buf_)
         for (u64* b : sb)
@@ -203,10 +200,6 @@ HipEngine::~HipEngine() {
     for (void* h : reg_)
         if (h) t_->deregister_buffer(h);
     for (int i = 0; i < 2; ++i) hipFree(buf_[i]);
-    for (auto& kv : flow_plans_)
-        for (void* q : {(void*)kv.second.lanes, (void*)kv.second.items, (void*)kv.second.deps, (void*)kv.second.flags})
-            if (q) hipFree(q);
-    if (flow_ctl_) hipFree(flow_ctl_);
     for (auto& kv : res_plans_)
         for (void* q : {(void*)kv.second.d, (void*)kv.second.nbr_off, (void*)kv.second.nbr, (void*)kv.second.counters})
             if (q) hipFree(q);
@@ -222,10 +215,8 @@ HipEngine::~HipEngine() {
             if (e) hipEventDestroy(e);
     if (cfg_.profile)
         for (auto e : {ev_t0_, ev_t1_, ev_t2_, ev_t3_}) hipEventDestroy(e);
-    if (s_ov_) hipStreamDestroy(s_ov_);
-    hipStreamDestroy(s_base_);
+    hipStreamDestroy(s_comp_);
     hipStreamDestroy(s_comm_);
-    engines_on_device(dev_, this, -1);
 }
 
 std::vector<u64> HipEngine::tile_words() {
@@ -267,6 +258,7 @@ void HipEngine::set_tile_words(const std::vector<u64>& dense) {
 }
 
 void HipEngine::run(u64 generations) {
+    trace::Range range("gol.run");
     Armed armed(wd_.get());
     if (dual_ && !sub_current_) {
         // canonical board -> sub-tiles (interior rows), unless the sub-tiles already hold the
@@ -328,8 +320,7 @@ void HipEngine::do_init(const PatternSpec& p) {
         // schedule (and the forced-split measurement mode).  The full schedule
         // exchanges on the compute stream itself: recording the event there every superstep
         // only idles the GPU (~15 us per record, a release fence).
-        events_needed_ = cfg_.force_split || (split_ && !halo_items(L_.R).empty()) ||
-                         (flow_ && flow_ov_ && !halo_items(L_.R).empty());
+        events_needed_ = cfg_.force_split || (split_ && !halo_items(L_.R).empty());
     }
     stats_.kernel = split_ ? kern_[1] + "+boundary:" + kern_[2] : (dual_ ? std::string("temporal") : kern_[0]);
     if (!split_ && !dual_ && kern_[0] == "pipe")
@@ -339,16 +330,8 @@ void HipEngine::do_init(const PatternSpec& p) {
         stats_.kernel = strprintf("resident@%d(%lld tiles x %d waves x %d rows)", res_kin_, (long long)rp.tiles, rp.nw, rp.B);
     }
     stats_.schedule = split_ ? "split" : (halo_items(L_.R).empty() ? "local" : "full");
-    if (dual_) stats_.schedule += sub_overlap_ == 2 ? "+subtiles2ov2" : (sub_overlap_ ? "+subtiles2ov" : "+subtiles2");
-    if (flow_) {
-        stats_.schedule += flow_ov_ ? "+flow+ov" : "+flow";
-        const FlowDev& fd = flow_plan(superstep_depth());
-        stats_.kernel = fd.tile ? strprintf("flow(tile@%d x %dw)", fd.kmax, cfg_.tile_waves)
-                                : strprintf("flow(temporal K<=%d)", hipk::flow_max_depth());
-    }
-    stats_.kernel_depth = dual_ ? tdepth_ : (flow_ ? *std::max_element(pass_depths(superstep_depth()).begin(),
-                                                                       pass_depths(superstep_depth()).end())
-                                                   : kdepth_);
+    if (dual_) stats_.schedule += sub_overlap_ ? "+subtiles2ov" : "+subtiles2";
+    stats_.kernel_depth = dual_ ? tdepth_ : kdepth_;
     stats_.tile_waves = cfg_.tile_waves;
     std::string tn;
     for (const auto& kv : tune_ms_) tn += strprintf("%s%s=%.3fus/gen", tn.empty() ? "" : " ", kv.first.c_str(), kv.second * 1e3);
@@ -368,13 +351,10 @@ void HipEngine::do_init(const PatternSpec& p) {
     // remainder of the hinted run length), so neither graph capture nor a hinted timed loop
     // builds or uploads a plan.  Other remainders are built on first use.
     for (int k : init_depths()) {
-        if (dual_) {
+        if (dual_)
             prepare_dual(k);
-            capture_dual_graphs(k);
-        } else {
+        else
             prepare(k);
-            if (flow_) flow_plan(k);
-        }
     }
     prewarm_graph();
     if (dual_) {
@@ -393,10 +373,6 @@ void HipEngine::do_init(const PatternSpec& p) {
     if (res_) {
         stats_.plan_waves = res_plan(res_kin_).tiles;  // workgroups of the resident launch
         stats_.lane_efficiency = 0;
-    } else if (flow_) {
-        const FlowDev& fd = flow_plan(superstep_depth());
-        stats_.plan_waves = fd.blocks * (fd.tile ? cfg_.tile_waves : kWavesPerBlock);  // the persistent grid
-        stats_.lane_efficiency = fd.st.lane_rows ? (double)fd.st.out_words / (double)fd.st.lane_rows : 0.0;
     } else {
         const DevPlan& fp = full_plan_stats();
         stats_.plan_waves = fp.waves;
@@ -451,14 +427,38 @@ void HipEngine::first_pass(int kx, int kp, i64 e, bool split) {
             HIP_CHECK(hipStreamWaitEvent(s_comm_, ev_ready_, 0));
             HIP_CHECK(hipEventRecord(ev_halo_, s_comm_));
             launch(1, kp, 0, src, dst, s_comp_);
+        } else if (device_transport_ && capturing()) {
+            // Inside a graph capture the RCCL group goes on the capture's origin stream (a group on the
+            // stream forked into the capture crashed in librccl, MI355X / ROCm 7.2), the interior on the
+            // forked one: the same graph.  Bands after the exchange (GOL_SPLIT_BANDS_COMM: concurrently
+            // with the interior; else after it too), joined before the later passes.
+            HIP_CHECK(hipStreamWaitEvent(s_comm_, ev_ready_, 0));
+            launch(1, kp, 0, src, dst, s_comm_);
+            HIP_CHECK(hipEventRecord(ev_halo_, s_comm_));
+            exchange_device(kx, items, cur_, s_comp_);
+            if (!bands_comm_) HIP_CHECK(hipStreamWaitEvent(s_comp_, ev_halo_, 0));
+            launch(2, kp, e, src, dst, s_comp_);
+            post(dst, s_comp_, e);
+            HIP_CHECK(hipStreamWaitEvent(s_comp_, ev_halo_, 0));
+            mark_ready();
+            return;
         } else if (device_transport_) {
             HIP_CHECK(hipStreamWaitEvent(s_comm_, ev_ready_, 0));
             if (prof) HIP_CHECK(hipEventRecord(ev_t0_, s_comm_));
             exchange_device(kx, items, cur_, s_comm_);
             if (prof) HIP_CHECK(hipEventRecord(ev_t1_, s_comm_));
-            HIP_CHECK(hipEventRecord(ev_halo_, s_comm_));
+            if (!bands_comm_) HIP_CHECK(hipEventRecord(ev_halo_, s_comm_));
             if (prof) HIP_CHECK(hipEventRecord(ev_t2_, s_comp_));
             launch(1, kp, 0, src, dst, s_comp_);
+            if (bands_comm_) {
+                launch(2, kp, e, src, dst, s_comm_);
+                post(dst, s_comm_, e);
+                HIP_CHECK(hipEventRecord(ev_halo_, s_comm_));
+                HIP_CHECK(hipStreamWaitEvent(s_comp_, ev_halo_, 0));
+                if (prof) record_profile(true);
+                mark_ready();
+                return;
+            }
         } else {
             if (prof) HIP_CHECK(hipEventRecord(ev_t2_, s_comp_));
             launch(1, kp, 0, src, dst, s_comp_);  // interior first: runs while the host exchanges

@@ -10,9 +10,8 @@ bool HipEngine::graph_shape(int& k, int& m) {
     // Sub-tile supersteps are not captured as a whole: captured with their fork/join across two
     // streams they replayed slower than eager launches on MI355X / ROCm 7.2 (32768^2: 14.2 vs
     // 12.8 us/gen over 20 generations, 13.0 vs 10.4 over 256; profiles/short_run_probe.txt).
-    // A single-stream graph per half and superstep is available (GOL_SUBTILE_GRAPHS=1), also slower.
+    // (A single-stream graph per half and superstep measured slower too: engine_hip_subtiles.hip.)
     if (dual_) return false;
-    if (flow_) return false;  // a flow superstep is one launch (its epoch is an argument: never replayed)
     k = cfg_.compat ? 1 : superstep_depth();
     m = cfg_.graph_supersteps;
     if (m <= 0) m = k >= 8 ? 16 : 32;

@@ -11,10 +11,9 @@ namespace hipeng {
 // depth, so shallow passes cost nearly as much as deep ones (32768^2: ~70-80 us for any depth
 // <= 6, ~90 us at 8; profiles/kb_depth_sweep.txt).
 const std::vector<int>& HipEngine::pass_depths(int k) {
-    const int key = k + (dual_ ? (1 << 20) : 0) + (res_ ? (1 << 21) : 0) + (flow_ ? (1 << 22) : 0);
+    const int key = k + (dual_ ? (1 << 20) : 0) + (res_ ? (1 << 21) : 0);
     auto it = passes_.find(key);
     if (it != passes_.end()) return it->second;
-    if (flow_) return passes_.emplace(key, flow_cut(k)).first->second;  // one step_flow launch
     if (res_) return passes_.emplace(key, std::vector<int>{k}).first->second;  // one resident launch
     // every kind may be temporal, unless only the (any-depth) tile kernel runs; sub-tiles always
     // run the temporal kernel at its own depth

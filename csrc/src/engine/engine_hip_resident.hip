@@ -76,9 +76,7 @@ void HipEngine::res_launch(int G, u64* src, u64* dst, hipStream_t s) {
 void HipEngine::check_res_status() {
     // every launch enqueued so far must be done before its fault words are read (pipe_fault reads its
     // flag with a null-stream copy, which the engine's non-blocking streams do not order)
-    if (flow_used_ || pipe_used_ || res_status_) synchronize();
-    if (flow_used_ && flow_ctl_ && hipk::flow_fault(flow_ctl_, s_comp_))
-        throw Error("step_flow: a dependency wait timed out (an item never saw its inputs); the board is invalid");
+    if (pipe_used_ || res_status_) synchronize();
     if (pipe_used_ && hipk::pipe_fault())
         throw Error("step_pipe: a ring wait timed out (a stage never got its rows); the board is invalid");
     if (!res_status_) return;

@@ -32,7 +32,6 @@ void HipEngine::setup_dual() {
 // Free the sub-tile buffers, plans and copy lists (the measurement chose one tile).
 void HipEngine::teardown_dual() {
     synchronize();
-    destroy_dual_graphs();
     for (auto& kv : sub_plans_) hipFree(kv.second.d);
     sub_plans_.clear();
     for (auto& sb : sub_buf_)
@@ -100,35 +99,18 @@ void HipEngine::dual_superstep(int k) {
     const int p = sub_cur_;
     const int a = (p + 1) % 3, b = (p + 2) % 3;  // the passes alternate a, b, a, ... (never p)
     wait_pending(s_comp_, ev_sub_b_);  // half 1's previous superstep is done
-    hipGraphExec_t gx[2] = {dual_graph(0, p, k), dual_graph(1, p, k)};
-    const bool graphs = gx[0] && gx[1];
     // With neighbours, half 0's first pass can start before the exchange: all its output rows but
     // the k next to the north halo read only rows the halves already hold (its own, and half 1's
     // edge across the seam); that band runs after the exchange.  The exchange then goes on the
     // second stream, the one of greatest priority, so the RCCL kernel is dispatched ahead of the
     // half-tile kernel when both become ready (a kernel that has filled the CUs first would hold
     // it back).  Chosen by measurement (schedule "subtiles+ov"): it costs a second, small kernel
-    // per superstep.
-    const bool ov = sub_overlap_ == 1 && !self_y() && !graphs;
-    const bool ov2 = sub_overlap_ == 2 && !self_y() && !graphs;
-    if (ov2) {
-        // Both halves' interiors first, each on its stream (half 1 reads half 0's edge across the seam:
-        // its stream waits for half 0's previous superstep); the exchange then runs on the compute
-        // stream after half 0's interior (no extra stream, no cross-queue wait before it), half 0's
-        // band follows it on that stream and half 1's band waits for it on the other.
-        launch_half(0, p, k, s_comp_, 0, 1);
-        wait_pending(s_comm_, ev_sub_a_);
-        launch_half(1, p, k, s_comm_, 0, 1);
-        std::vector<Message> sends, recvs;
-        dual_messages(p, k, sends, recvs);
-        exchange_rows(sends, recvs, s_comp_);
-        stats_.exchanges += 1;
-        stats_.halo_bytes += (u64)(rows_bytes(0, k) + rows_bytes(1, k));
-        HIP_CHECK(hipEventRecord(ev_sub_x_, s_comp_));
-        launch_half(0, p, k, s_comp_, 0, 2);
-        HIP_CHECK(hipStreamWaitEvent(s_comm_, ev_sub_x_, 0));
-        launch_half(1, p, k, s_comm_, 0, 2);
-    } else if (!self_y()) {
+    // per superstep.  (Both halves' interiors first, with the exchange between half 0's interior
+    // and its band, measured slower everywhere: 13.2-13.7 vs 12.7-12.8 us/gen at 20 generations
+    // through the RCCL self-exchange, the exchange and its ~10 us tail then sit on half 0's critical
+    // path; docs/PERFORMANCE.md section 6.)
+    const bool ov = sub_overlap_ == 1 && !self_y();
+    if (!self_y()) {
         hipStream_t xs = s_comp_;
         if (ov) {
             launch_half(0, p, k, s_comp_, 0, 1);
@@ -147,27 +129,21 @@ void HipEngine::dual_superstep(int k) {
     } else {
         wait_pending(s_comm_, ev_sub_a_);  // half 0's previous superstep is done
     }
-    // Each half's passes: eager launches on its stream, alternating between the halves (pass j
-    // of half 0, pass j of half 1, ...: issued half by half, the second stream's first kernel
-    // started ~20 us after the first's, three host launches later, and the superstep ended on one
-    // half's lone tail; kernel traces of the driver's 20-generation bench), or
-    // (GOL_SUBTILE_GRAPHS=1) one replay per half of a graph captured at init per half, start
-    // buffer and depth.  The cross-half order stays in the events around them.
-    if (graphs) {
-        for (int s = 0; s < 2; ++s) HIP_CHECK(hipGraphLaunch(gx[s], s ? s_comm_ : s_comp_));
-        stats_.graph_launches += 2;
-    } else {
-        const int np = (int)pass_depths(k).size();
-        for (int j = 0; j < np; ++j)
-            for (int i = 0; i < 2; ++i) {
-                const int s = i;  // half 0's pass first (half 1 first measured no better: docs/PERFORMANCE.md §6)
-                if (!((ov && s == 0 && j == 0) || (ov2 && j == 0))) {
-                    if (j == 0 && i == 0) trace::mark("gol.launch0");  // (GOL_ROCTX: host side of the launch latency)
-                    launch_half(s, p, k, s ? s_comm_ : s_comp_, j);
-                    if (j == 0 && i == 0) trace::mark("gol.launch0_done");
-                }
-            }
-    }
+    // Each half's passes: eager launches on its stream, alternating between the halves (pass j of
+    // half 0, pass j of half 1, ...: issued half by half, the second stream's first kernel started
+    // ~20 us after the first's, three host launches later, and the superstep ended on one half's
+    // lone tail; kernel traces of the driver's 20-generation bench).  The cross-half order stays in
+    // the events around them.  (Per-half graphs of these passes, replayed per superstep, measured
+    // slower than the eager launches on MI355X / ROCm 7.2: 20 generations 13.06-13.23 vs 12.75-12.96
+    // us/gen, 2000 generations 10.35 vs 10.24; profiles/subtile_graphs_ab.txt.)
+    const int np = (int)pass_depths(k).size();
+    for (int j = 0; j < np; ++j)
+        for (int s = 0; s < 2; ++s) {  // half 0's pass first (half 1 first measured no better: docs/PERFORMANCE.md §6)
+            if (ov && s == 0 && j == 0) continue;
+            if (j == 0 && s == 0) trace::mark("gol.launch0");  // (GOL_ROCTX: host side of the launch latency)
+            launch_half(s, p, k, s ? s_comm_ : s_comp_, j);
+            if (j == 0 && s == 0) trace::mark("gol.launch0_done");
+        }
     if (wd_) {
         // with a watchdog the end-of-superstep events are the superstep's progress marker (a fresh
         // pair from the marker ring; ev_sub_a_ / ev_sub_b_ always name the latest pair)
@@ -264,35 +240,6 @@ void HipEngine::launch_half(int s, int p, int k, hipStream_t st, int only, int p
         }
         q = dsti;
     }
-}
-
-void HipEngine::capture_dual_graphs(int k) {
-    if (!dual_graphs_on()) return;
-    for (int s = 0; s < 2; ++s)
-        for (int p = 0; p < 3; ++p) {
-            const int key = (s * 3 + p) * 1000 + k;
-            if (dual_graphs_.count(key)) continue;
-            hipStream_t st = s ? s_comm_ : s_comp_;
-            hipGraph_t graph = nullptr;
-            hipGraphExec_t exec = nullptr;
-            try {
-                HIP_CHECK(hipStreamBeginCapture(st, hipStreamCaptureModeRelaxed));
-                launch_half(s, p, k, st);
-                HIP_CHECK(hipStreamEndCapture(st, &graph));
-                HIP_CHECK(hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0));
-                HIP_CHECK(hipGraphDestroy(graph));
-                HIP_CHECK(hipGraphUpload(exec, st));
-            } catch (const Error& e) {
-                hipGraph_t g2 = nullptr;
-                hipStreamEndCapture(st, &g2);
-                if (g2) hipGraphDestroy(g2);
-                hipGetLastError();
-                graph_ok_ = false;
-                fprintf(stderr, "[gol] sub-tile graph capture disabled: %s\n", e.what());
-                return;
-            }
-            dual_graphs_[key] = exec;
-        }
 }
 
 }  // namespace hipeng

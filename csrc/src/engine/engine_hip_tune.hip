@@ -42,7 +42,7 @@ void HipEngine::spin_up() {
 // kernel passes, never the exchanges.
 void HipEngine::measure_pass_costs() {
     pass_us_.clear();
-    if (cfg_.compat || cfg_.kernel_depth > 0 || kernel_ == "lds" || res_ || flow_ || (!dual_ && tile_kernel(0)) ||
+    if (cfg_.compat || cfg_.kernel_depth > 0 || kernel_ == "lds" || res_ || (!dual_ && tile_kernel(0)) ||
         (!dual_ && !split_ && kern_[0] == "pipe"))
         return;
     // every instantiated depth up to the pass depth, and the deeper ones a superstep could use: a
@@ -102,19 +102,6 @@ void HipEngine::measure_pass_costs() {
     passes_.clear();
 }
 
-bool HipEngine::flow_timing_buffers() {
-    if (flow_scratch_) return true;
-    size_t fr = 0, tot = 0;
-    if (hipMemGetInfo(&fr, &tot) != hipSuccess || fr < alloc_bytes_ + ((size_t)1 << 30)) return false;
-    if (hipMalloc(&flow_scratch_, alloc_bytes_) != hipSuccess) {
-        hipGetLastError();
-        flow_scratch_ = nullptr;
-        return false;
-    }
-    HIP_CHECK(hipMemsetAsync(flow_scratch_, 0, alloc_bytes_, s_comp_));
-    return true;
-}
-
 void HipEngine::choose_schedule() {
     const bool nbrs = !halo_items(L_.R).empty();  // identical on every rank (uniform grid)
     std::vector<std::string> cands;
@@ -129,7 +116,6 @@ void HipEngine::choose_schedule() {
             cands.push_back("full+graph");
     }
     graph_rccl_on_ = cfg_.graph_rccl == 1;
-    sub_graphs_on_ = cfg_.subtile_graphs == 1;
     bool dual_ok = cfg_.subtiles != 0 && cands[0] != "split" && dual_wanted();
     if (dual_ok) {
         double ok = dual_local_ok() ? 1.0 : 0.0;
@@ -140,44 +126,9 @@ void HipEngine::choose_schedule() {
         // the overlapped variant needs the exchange (neighbours, or the self-exchange)
         std::vector<std::string> dc;
         if (cfg_.subtile_overlap <= 0 || self_y()) dc.push_back("subtiles");
-        // (GOL_SUBTILE_OVERLAP: 1 or auto the half-0 variant; 2 forces the symmetric one, which is no
-        // timed candidate: it measured slower everywhere, 13.2-13.7 vs 12.7-12.8 us/gen at 20 generations
-        // through RCCL self-exchange, the exchange and its ~10 us tail land on the compute stream)
-        if (cfg_.subtile_overlap != 0 && !self_y()) dc.push_back(cfg_.subtile_overlap == 2 ? "subtiles+ov2" : "subtiles+ov");
-        // (graph replay excludes the overlapped variants: not a candidate when one is forced)
-        if (cfg_.subtile_graphs < 0 && cfg_.graph && !cfg_.profile && cfg_.subtile_overlap <= 0)
-            dc.push_back("subtiles+graph");
+        if (cfg_.subtile_overlap != 0 && !self_y()) dc.push_back("subtiles+ov");
         if (cfg_.subtiles == 2) cands.clear();
         cands.insert(cands.end(), dc.begin(), dc.end());
-    }
-    // The one-tile superstep as ONE dependency-driven launch (step_flow, engine_hip_flow.hip): opt-in
-    // (GOL_SCHEDULE=flow / flow+ov forces it, GOL_FLOW=1 adds it to the timed candidates).  It measured
-    // slower than the pass schedules on every configuration (docs/PERFORMANCE.md §15: 32768^2 12.87 vs
-    // 9.55 us/gen, 8192^2 x 1000 1.47 vs 1.40 ms, self-exchange 17.4 vs 13.2 us/gen), and its timing
-    // candidate once won config 2's init against a local candidate timed on shorter supersteps.  Timed
-    // on scratch: the candidate needs memory for one more board (agreed over the ranks: collective).
-    const bool flow_forced = cfg_.sched == "flow" || cfg_.sched == "flow+ov";
-    if (cands[0] != "split" && (flow_forced || env_int("GOL_FLOW", 0) != 0) && flow_eligible()) {
-        double ok = flow_forced ? 1.0 : (flow_timing_buffers() ? 1.0 : 0.0);  // (forced: not timed, no scratch)
-        if (t_->size() > 1) ok = t_->allreduce_min(ok);
-        // flow+ov also needs its CU-restricted stream (hip_engine.hpp kOvReservedCus) on every rank
-        double ov_ok = nbrs && device_transport_ && ov_stream() ? 1.0 : 0.0;
-        if (t_->size() > 1) ov_ok = t_->allreduce_min(ov_ok);
-        if (ok > 0) {
-            cands.push_back("flow");
-            if (ov_ok > 0) cands.push_back("flow+ov");
-            // (no graphed flow candidate: a superstep is one launch whose epoch is an argument, and a
-            // graph replay costs more than a direct launch)
-        }
-        if (flow_forced) {  // GOL_SCHEDULE=flow[+ov]: the only candidate (not timed)
-            if (cfg_.sched == "flow+ov" && !(nbrs && device_transport_))
-                throw Error("GOL_SCHEDULE=flow+ov needs neighbours and a device transport (RCCL)");
-            if (cfg_.sched == "flow+ov" && ov_ok <= 0)
-                throw Error("GOL_SCHEDULE=flow+ov: no CU-restricted compute stream (hipExtStreamCreateWithCUMask)");
-            cands = {cfg_.sched};
-        }
-    } else if (flow_forced) {
-        throw Error("GOL_SCHEDULE=flow: this tile cannot run flow supersteps (GOL_KERNEL / GOL_COMPAT / width)");
     }
     std::string pick = cands[0];
     if (cands.size() > 1) {
@@ -196,28 +147,17 @@ void HipEngine::choose_schedule() {
         // full+graph timed 12.6 against subtiles+ov's 12.3-12.5 us/gen at best, won one init in five,
         // and that run measured 13.4 against 12.0-12.4 us/gen, driver's cut through the self-exchange)
         std::vector<std::vector<double>> samples(cands.size());
-        // flow supersteps of tile items run the whole hinted run as one launch (flow_superstep_depth):
-        // every candidate is then timed over that many generations, the others as whole supersteps of k
-        // (timed on 4 x 32 generations against one 1000-generation launch, the local candidate paid four
-        // graph replays for the flow candidate's one and lost config 2's init, 1.60 vs 1.44 us/gen, to a
-        // flow run that then measured 1.52 against local's 1.36)
-        bool any_flow = false;
-        for (const std::string& c : cands) any_flow = any_flow || c.rfind("flow", 0) == 0;
-        const int span = any_flow && !short_run ? std::max(k, flow_superstep_depth()) : k;
         spin_up();
         for (int round = 0; round < rounds; ++round)
             for (size_t c = 0; c < cands.size(); ++c) {
-                const bool fl = cands[c].rfind("flow", 0) == 0;
-                const int kc = fl ? span : k;
-                const int rc = span > k ? std::max(1, span / kc) : std::max(1, reps * k / kc);
-                if (round == 0) time_schedule(cands[c], kc, rc);  // warm-up: connections, plans, graphs
+                if (round == 0) time_schedule(cands[c], k, reps);  // warm-up: connections, plans, graphs
                 synchronize();
                 t_->barrier();
                 const auto t0 = std::chrono::steady_clock::now();
-                time_schedule(cands[c], kc, rc);
+                time_schedule(cands[c], k, reps);
                 synchronize();
                 const double dt = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
-                const double us = t_->allreduce_max(dt) * 1e6 / (rc * kc);
+                const double us = t_->allreduce_max(dt) * 1e6 / (reps * k);
                 samples[c].push_back(us);
                 best[c] = std::min(best[c], us);
                 if (short_run) {
@@ -225,18 +165,11 @@ void HipEngine::choose_schedule() {
                     std::sort(v.begin(), v.end());
                     best[c] = v[(v.size() - 1) / 2];
                 }
-                // a flow launch whose wait timed out (clears the fault word): the candidate is dropped
-                if (fl && flow_ctl_ && hipk::flow_fault(flow_ctl_, s_comp_)) {
-                    fprintf(stderr, "[gol] rank %d: schedule candidate %s: a flow wait timed out (dropped)\n", g_.rank,
-                            cands[c].c_str());
-                    sched_graph_failed_.insert(cands[c]);
-                }
-                init_step("init: schedule timing", cands[c].c_str(), kc, (float)best[c]);
+                init_step("init: schedule timing", cands[c].c_str(), k, (float)best[c]);
             }
         size_t bi = 0;
         for (size_t c = 0; c < cands.size(); ++c) {
-            // a candidate whose timing graph could not be captured (or whose flow launch faulted) on some
-            // rank is dropped
+            // a candidate whose timing graph could not be captured on some rank is dropped
             if (t_->allreduce_max(sched_graph_failed_.count(cands[c]) ? 1.0 : 0.0) > 0) best[c] = 1e30;
             sched_us_[cands[c]] = best[c];
             if (best[c] < best[bi]) bi = c;
@@ -256,25 +189,11 @@ void HipEngine::choose_schedule() {
         stats_.graph_launches = 0;
     }
     destroy_sched_graphs();  // (they captured the communicator: destroy them before the comm can go)
-    free_flow_scratch();
     sched_pick_ = pick;
-    flow_ = pick.rfind("flow", 0) == 0;
-    flow_ov_ = pick == "flow+ov";
-    // flow+ov runs on the CU-restricted compute stream from here on (every later launch of the engine
-    // is ordered on it)
-    hipStream_t sc = flow_ov_ ? s_ov_ : s_base_;
-    if (s_comp_ != sc) {
-        HIP_CHECK(hipStreamSynchronize(s_comp_));
-        s_comp_ = sc;
-    }
     split_ = pick == "split";
     dual_ = pick.rfind("subtiles", 0) == 0;
-    sub_overlap_ = pick == "subtiles+ov" ? 1 : (pick == "subtiles+ov2" ? 2 : 0);
+    sub_overlap_ = pick == "subtiles+ov" ? 1 : 0;
     graph_rccl_on_ = cfg_.graph_rccl == 1 || pick == "full+graph";
-    sub_graphs_on_ = cfg_.subtile_graphs == 1 || pick == "subtiles+graph";
-    // The timing's per-half graphs baked in the pass cut of that moment; measure_pass_costs may change
-    // the cut (and with it the buffer parity a superstep ends on): always recapture after it (do_init).
-    destroy_dual_graphs();
     if (dual_) {
         setup_dual();
         sub_current_ = false;  // the halves hold timing scratch: load the board at the next run
@@ -289,17 +208,10 @@ void HipEngine::time_schedule(const std::string& c, int k, int reps, bool eager)
     if (c.rfind("subtiles", 0) == 0) {
         setup_dual();
         dual_ = true;
-        sub_overlap_ = c == "subtiles+ov" ? 1 : (c == "subtiles+ov2" ? 2 : 0);
-        const bool sg = sub_graphs_on_;
-        sub_graphs_on_ = c == "subtiles+graph" || cfg_.subtile_graphs == 1;
-        if (sub_graphs_on_) {
-            prepare_dual(k);
-            capture_dual_graphs(k);  // once per (half, start buffer, depth)
-        }
+        sub_overlap_ = c == "subtiles+ov" ? 1 : 0;
         for (int i = 0; i < reps; ++i) dual_superstep(k);
         dual_ = false;
         sub_overlap_ = 0;
-        sub_graphs_on_ = sg;
         return;
     }
     // One-tile supersteps as the runs replay them (graphs: "local" always, the "full+graph"
@@ -342,51 +254,6 @@ void HipEngine::time_schedule(const std::string& c, int k, int reps, bool eager)
             HIP_CHECK(hipGraphLaunch(sg.exec, s_comp_));
         else
             time_schedule(base, k, reps, true);  // the same exchanges as the peers' replays
-        return;
-    }
-    if (c == "flow" || c == "flow+ov") {
-        // flow supersteps on scratch (a flow launch writes both of its buffers): the launches run between
-        // flow_scratch_ and buf[cur ^ 1]; the exchange writes the board's ghost rows, as the other
-        // candidates' do (the next real superstep rewrites them).  The kernel's run time does not depend
-        // on the cell values, so the scratch's are never refreshed.
-        if (!flow_timing_buffers()) throw Error("flow schedule timing: no scratch buffer");
-        const bool f = flow_, fo = flow_ov_;
-        flow_ = true;
-        flow_ov_ = c == "flow+ov";
-        const std::vector<HaloItem>& items = items_for(k);
-        // (flow+ov on its CU-restricted stream, as the runs)
-        const hipStream_t keep = s_comp_;
-        if (flow_ov_active(k) && s_comp_ != s_ov_) {
-            if (!ov_stream()) throw Error("flow+ov timing: no CU-restricted compute stream");
-            HIP_CHECK(hipStreamSynchronize(s_comp_));
-            s_comp_ = s_ov_;
-        }
-        for (int i = 0; i < reps; ++i) {
-            if (flow_ov_active(k)) {  // as flow_superstep's overlapped path, on scratch
-                flow_plan(k);  // (allocates the control block the flag lives in)
-                prepare(k);
-                HIP_CHECK(hipStreamWaitEvent(s_comm_, ev_ready_, 0));
-                exchange_device(k, items, cur_, s_comm_);
-                HIP_CHECK(hipStreamWriteValue32(s_comm_, &flow_ctl_->exch, next_flow_epoch(), 0));
-                flow_launch(k, flow_scratch_, buf_[cur_ ^ 1], s_comp_);
-                HIP_CHECK(hipEventRecord(ev_ready_, s_comp_));
-                continue;
-            }
-            if (!items.empty()) {
-                prepare(k);
-                if (device_transport_)
-                    exchange_device(k, items, cur_, s_comp_);
-                else
-                    exchange_staged(k, items, cur_, s_comp_);
-            }
-            flow_launch(k, flow_scratch_, buf_[cur_ ^ 1], s_comp_);
-        }
-        if (s_comp_ != keep) {
-            HIP_CHECK(hipStreamSynchronize(s_comp_));
-            s_comp_ = keep;
-        }
-        flow_ = f;
-        flow_ov_ = fo;
         return;
     }
     split_ = c == "split";
@@ -582,10 +449,8 @@ void HipEngine::autotune_kernel() {
     pipe_used_ = false;  // (the candidates ran on scratch; faults were checked above)
     // The resident kernel (small boards without neighbours): one launch per run, halos exchanged
     // between tiles inside the kernel every kin generations.  Timed on launches of the hinted run's
-    // length (at most 256 generations) against the best pass kernel above.  (GOL_SCHEDULE=flow asks
-    // for flow supersteps of the pass kernels: no resident candidate.)
-    const bool flow_forced2 = cfg_.sched == "flow" || cfg_.sched == "flow+ov";
-    if (resident_eligible() && !split_used() && (!flow_forced2 || cfg_.kernel == "resident")) {
+    // length (at most 256 generations) against the best pass kernel above.
+    if (resident_eligible() && !split_used()) {
         const int G = std::min(res_run_depth(), 256);
         float rbest = 1e30f;
         int rk = 0;
@@ -672,9 +537,8 @@ std::map<std::string, double> HipEngine::phase_probe(int k) {
     // the schedule the runs use, as choose_schedule timed it (graph variants included)
     std::string sched = sched_pick_;
     if (sched.empty())
-        sched = dual_ ? (sub_overlap_ == 2 ? "subtiles+ov2" : (sub_overlap_ ? "subtiles+ov" : "subtiles"))
+        sched = dual_ ? (sub_overlap_ ? "subtiles+ov" : "subtiles")
                       : (split_ ? "split" : (halo_items(L_.R).empty() ? "local" : "full"));
-    if (sched.rfind("flow", 0) == 0 && !flow_timing_buffers()) sched = halo_items(L_.R).empty() ? "local" : "full";
     const int reps = 2;
     double best = 1e30;
     for (int round = 0; round < 3; ++round) {
@@ -690,7 +554,6 @@ std::map<std::string, double> HipEngine::phase_probe(int k) {
     out["superstep_gens"] = k;
     synchronize();
     destroy_sched_graphs();
-    free_flow_scratch();
     HIP_CHECK(hipEventDestroy(e0));
     HIP_CHECK(hipEventDestroy(e1));
     dual_ = was_dual;

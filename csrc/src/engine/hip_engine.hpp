@@ -7,7 +7,7 @@
 //   engine_hip_subtiles.hip  two sub-tiles per rank on two streams
 //   engine_hip_graph.hip     hipGraph capture and replay of one-tile supersteps
 //   engine_hip_halo.hip      halo exchange (device transport or host staging)
-//   engine_hip_flow.hip      supersteps as one dependency-driven launch (step_flow)
+//   engine_hip_resident.hip  whole runs as one resident launch (step_resident)
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -184,12 +184,7 @@ class HipEngine : public Engine {
         for (size_t j = 0; j < ps.size(); ++j)
             for (int s = 0; s < 2; ++s) sub_plan(s, ps[j], ext_after(ps, j));
         if (sub_overlap_ && !self_y())
-            for (int s = 0; s < (sub_overlap_ == 2 ? 2 : 1); ++s)
-                for (int part : {1, 2}) sub_plan(s, ps[0], ext_after(ps, 0), part);
-    }
-    void destroy_dual_graphs() {
-        for (auto& kv : dual_graphs_) hipGraphExecDestroy(kv.second);
-        dual_graphs_.clear();
+            for (int part : {1, 2}) sub_plan(0, ps[0], ext_after(ps, 0), part);
     }
 
     // part: 0 the whole pass; a first pass split around the exchange (sub_overlap_): 1 all output
@@ -237,20 +232,6 @@ class HipEngine : public Engine {
 
     void launch_half(int s, int p, int k, hipStream_t st, int only = -1, int part = 0);
 
-    // Graph of launch_half(s, p, k): captured at init only (capture_dual_graphs), nullptr otherwise.
-    // A candidate of the schedule timing ("subtiles+graph"; GOL_SUBTILE_GRAPHS=1 forces it): replayed
-    // per half and superstep, these measured slower than the eager launches in round 2 on MI355X /
-    // ROCm 7.2 (32768^2, same box, alternating: 20 generations 13.06-13.23 vs 12.75-12.96 us/gen, 2000
-    // generations 10.35 vs 10.24; profiles/subtile_graphs_ab.txt), as did one graph of both halves
-    // with fork/join events (see graph_shape), so the node they run on decides.
-    bool dual_graphs_on() const { return cfg_.graph && !cfg_.profile && graph_ok_ && sub_graphs_on_; }
-    hipGraphExec_t dual_graph(int s, int p, int k) {
-        if (!dual_graphs_on()) return nullptr;
-        auto it = dual_graphs_.find((s * 3 + p) * 1000 + k);
-        return it == dual_graphs_.end() ? nullptr : it->second;
-    }
-    void capture_dual_graphs(int k);
-
     const DevPlan& full_plan_stats() {
         const int R = superstep_depth();
         return plan(0, pass_depths(R)[0], ext_after(pass_depths(R), 0));
@@ -262,8 +243,6 @@ class HipEngine : public Engine {
     // generation).  With neighbours every rank keeps R: the exchanges must match.
     int superstep_depth() const override {
         if (res_) return std::max(L_.R, res_run_depth());
-        // (flow_superstep_depth builds and caches tile plans: logically const)
-        if (flow_) return const_cast<HipEngine*>(this)->flow_superstep_depth();
         if (dual_ || !tuned_ || cfg_.compat || kdepth_ <= 0 || kdepth_ >= L_.R || !halo_items(L_.R).empty())
             return L_.R;
         return (L_.R / kdepth_) * kdepth_;
@@ -287,8 +266,6 @@ class HipEngine : public Engine {
     void do_superstep(int k) override {
         if (dual_)
             dual_superstep(k);
-        else if (flow_)
-            flow_superstep(k);
         else
             tile_superstep(k);
     }
@@ -309,6 +286,12 @@ class HipEngine : public Engine {
     }
 
     void first_pass(int kx, int kp, i64 e, bool split);
+    // The compute stream is being captured into a graph.
+    bool capturing() const {
+        hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+        HIP_CHECK(hipStreamIsCapturing(s_comp_, &cs));
+        return cs == hipStreamCaptureStatusActive;
+    }
 
     void spin_up();
 
@@ -490,41 +473,6 @@ class HipEngine : public Engine {
     // time resident launches of G generations from a scratch copy of the board; ms per generation
     float time_resident(int kin, int G);
 
-    // ----- flow supersteps (step_flow, engine_hip_flow.hip) -----
-    struct FlowDev {
-        LaneDesc* lanes = nullptr;
-        FlowItem* items = nullptr;
-        u32* deps = nullptr;
-        u32* flags = nullptr;
-        u32 n_items = 0, max_deps = 0;
-        std::vector<int> cut;
-        PlanStats st;
-        bool tile = false;  // LDS tile items (the tuned full-tile kernel is step_tile)
-        i64 rows = 0;       // tile items: chunk height of the plans
-        int kmax = 0;       // tile items: deepest pass
-        u32 tflags = 0;     // tile items: variant bits (STEP_TILE_*)
-        i64 blocks = 0;     // persistent grid (workgroups)
-    };
-    bool flow_eligible();
-    // Flow items are LDS tiles when the tuned full-tile kernel is the tile kernel and a flow tile variant
-    // exists for its workgroup size and the variant bits of the cut's deepest pass (flow_cut,
-    // flow_tile_cut_ok); otherwise step_temporal waves.
-    bool flow_tiles() const { return kern_[0] == "tile"; }
-    bool flow_tile_cut_ok(const std::vector<int>& ps);
-    // Generations per flow superstep: the halo depth R with neighbours (the exchanges must match); on a
-    // rank without neighbours the hinted run length (at least R, at most 1024), so a whole run is one
-    // launch of passes that flow into each other (8192^2 x 1000: 32 tile passes, no kernel boundary).
-    // (Wave items keep R: a superstep's plan holds ~3000 items of 1 KiB of lane descriptors per pass.)
-    int flow_superstep_depth() {
-        if (!flow_tiles() || !halo_items(L_.R).empty() || cfg_.run_hint == 0) return L_.R;
-        const int d = (int)std::max<u64>((u64)L_.R, std::min<u64>(cfg_.run_hint, 1024));
-        return flow_tile_cut_ok(flow_cut(d)) ? d : L_.R;
-    }
-    std::vector<int> flow_cut(int k);
-    const FlowDev& flow_plan(int k);
-    void flow_launch(int k, const u64* src, u64* dst, hipStream_t s);
-    void flow_superstep(int k);
-
     // ----- watchdog support: progress markers -----
     // With a watchdog, every superstep (or graph replay) publishes a marker: HIP events recorded at
     // its end on the streams it used.  The watchdog thread retires completed markers (probe), so GPU
@@ -581,6 +529,7 @@ class HipEngine : public Engine {
     bool multipass_ = false;
     std::map<int, std::vector<int>> passes_;
     bool split_ = false;   // superstep schedule: interior/boundary split with overlapped exchange
+    bool bands_comm_ = env_int("GOL_SPLIT_BANDS_COMM", 0) != 0;  // split: bands on the comm stream after the exchange
     std::map<std::string, double> sched_us_;  // choose_schedule: us per generation per candidate
     std::map<int, double> pass_us_;           // measure_pass_costs: us per pass by depth (chosen mode)
     bool tuned_ = false;
@@ -606,7 +555,6 @@ class HipEngine : public Engine {
     static constexpr unsigned event_flags() { return hipEventDisableTiming; }
     bool graph_ok_ = true;
     bool graph_rccl_on_ = false;  // one-tile supersteps with an RCCL exchange are captured (choose_schedule)
-    bool sub_graphs_on_ = false;  // sub-tile passes replay per-half graphs (choose_schedule)
     // timing graphs of the graphed schedule candidates ("local", "full+graph"), by name
     struct SchedGraph {
         hipGraphExec_t exec = nullptr;
@@ -622,37 +570,6 @@ class HipEngine : public Engine {
         sched_graphs_.clear();
     }
     std::string sched_pick_;     // the schedule candidate choose_schedule picked (phase_probe times it)
-    // flow supersteps with neighbours ("flow+ov"): the exchange runs on the comm stream while the
-    // launch's interior items run; the items reading ghost cells wait for its device flag
-    bool flow_ov_ = false;
-    bool flow_ov_active(int k) { return flow_ov_ && device_transport_ && !items_for(k).empty(); }
-    // The flow+ov launch holds every wave slot it is given until its band items have seen the exchange
-    // flag, so the exchange's own kernels (RCCL's send/recv kernel: 248-256 VGPRs and 37.6 KB of LDS per
-    // 256-512-thread workgroup on gfx950, read from librccl's code-object notes; HIP's copy kernels)
-    // must find CUs the persistent grid does not occupy: a wave flow grid at 3 waves/SIMD leaves 8 of
-    // the 512 VGPRs per SIMD lane, a tile flow grid the LDS of its CU.  flow+ov launches therefore go
-    // to a compute stream restricted (hipExtStreamCreateWithCUMask) to all CUs but kOvReservedCus, and
-    // their grid is sized to the CUs it may use.  Engines sharing a device (thread ranks) split those
-    // CUs, so no engine's launch can take the CUs another's exchange waits for.
-    static constexpr int kOvReservedCus = 8;
-    hipStream_t s_base_ = nullptr;  // the engine's unrestricted compute stream
-    hipStream_t s_ov_ = nullptr;    // the CU-restricted one (s_comp_ while flow+ov is the schedule)
-    int ov_cus_ = 0;                // CUs of s_ov_
-    bool ov_stream();               // create s_ov_ (false: not possible here)
-    // The live engines of a device in this process: op +1 registers e, -1 removes it, 0 queries;
-    // returns {e's slot among them, their count}.
-    static std::pair<int, int> engines_on_device(int dev, const HipEngine* e, int op);
-    i64 flow_cus(bool ov) const { return ov ? (i64)ov_cus_ : (i64)cus_; }
-    u64* flow_scratch_ = nullptr;  // timing scratch of flow candidates (a flow launch writes both buffers)
-    // Flow candidates are timed on scratch: the board copied to flow_scratch_, the launch between it and
-    // buf[cur ^ 1].  False when there is no memory for one more board.
-    bool flow_timing_buffers();
-    void free_flow_scratch() {
-        if (!flow_scratch_) return;
-        hipStreamSynchronize(s_comp_);
-        hipFree(flow_scratch_);
-        flow_scratch_ = nullptr;
-    }
     bool events_needed_ = true;  // another stream waits on ev_ready_
     std::vector<void*> deferred_free_;
     std::map<i64, DevPlan> plans_;
@@ -660,9 +577,7 @@ class HipEngine : public Engine {
     bool dual_ = false;
     // Exchange overlap of the sub-tile superstep (timed candidates): 0 none ("subtiles"); 1 half 0's
     // first pass, but for its band next to the north halo, runs while the exchange is in flight
-    // ("subtiles+ov"); 2 both halves' first passes, but for their bands next to the rank's halos,
-    // run before the exchange, which then runs on the compute stream between half 0's interior and its
-    // band ("subtiles+ov2")
+    // ("subtiles+ov")
     int sub_overlap_ = 0;
     Layout sub_L_[2];
     i64 sub_r0_[2] = {0, 0};
@@ -671,7 +586,6 @@ class HipEngine : public Engine {
     bool sub_current_ = false;  // the halves hold the current board
     bool canon_stale_ = false;  // buf_[cur_] lags the halves (sync_canonical before reading it)
     std::map<int, DevPlan> sub_plans_;
-    std::map<int, hipGraphExec_t> dual_graphs_;  // (half, start buffer, depth) -> launch_half graph
     hipEvent_t ev_sub_a_ = nullptr, ev_sub_b_ = nullptr;  // half 0 / half 1 done with its last superstep
     bool events_synced_ = false;  // both streams synchronised since ev_sub_a_ / ev_sub_b_ were last recorded
                                                            // (ev_sub_own_, or a progress marker's pair)
@@ -681,13 +595,6 @@ class HipEngine : public Engine {
     std::map<int, std::vector<HaloItem>> items_;
     std::map<i64, hipGraphExec_t> graphs_;
     std::vector<u64*> dstage_s_, dstage_r_, hstage_s_, hstage_r_;
-    bool flow_ = false;                     // supersteps run as one step_flow launch (schedule "+flow")
-    bool flow_used_ = false;                // a flow launch ran (fault check at readouts)
-    hipk::FlowCtl* flow_ctl_ = nullptr;     // its ticket / fault / exchange words
-    u32 flow_epoch_ = 0;                    // flow launches made on flow_ctl_ (FlowArgs::epoch of the last)
-    u32 next_flow_epoch() const { return flow_epoch_ + 1u == 0u ? 1u : flow_epoch_ + 1u; }
-    int flow_nseq_ = 0;                     // the device's XCDs (ticket sequences; 1 when the device is shared)
-    std::map<int, FlowDev> flow_plans_;     // by superstep depth x 2 + exchange-overlapped
     bool res_ = false;  // supersteps run the resident kernel
     int res_kin_ = 0;   // its generations per in-kernel halo exchange
     std::map<int, ResPlan> res_plans_;

@@ -72,7 +72,7 @@ __global__ __launch_bounds__(64 * NW) void step_tile(const u64* __restrict__ src
     const LaneDesc d = plan[(i64)blockIdx.x * kWaveLanes + lane];
     const int nrows = __builtin_amdgcn_readfirstlane(d.nrows);
     if (nrows <= 0) return;  // padding tile (uniform over the workgroup)
-    tile_item<NW, WRAPY, LV, IP, false>(src, dst, d, nrows, p, K, tile_lds, wv, lane, blockIdx.x);
+    tile_item<NW, WRAPY, LV, IP>(src, dst, d, nrows, p, K, tile_lds, wv, lane, blockIdx.x);
 }
 
 template <int NW, bool WRAPY, int LV, bool IP>
@@ -84,7 +84,7 @@ __global__ __launch_bounds__(64 * NW) void step_tile_fold(const u64* __restrict_
     const LaneDesc d = plan[(i64)blockIdx.x * kWaveLanes + lane];  // lanes 32-63 repeat lanes 0-31
     const int nrows = __builtin_amdgcn_readfirstlane(d.nrows);
     if (nrows <= 0) return;  // padding tile (uniform over the workgroup)
-    fold_item<NW, WRAPY, LV, IP, false>(src, dst, d, nrows, p, K, tile_lds, wv, lane, blockIdx.x);
+    fold_item<NW, WRAPY, LV, IP>(src, dst, d, nrows, p, K, tile_lds, wv, lane, blockIdx.x);
 }
 
 template <int NW, bool IP>

@@ -1,8 +1,6 @@
-// gol-mi355x: the LDS tile kernels' device code (step_tile / step_tile_fold in step_kernels.hip, and
-// step_flow's tile items in flow_kernel.hip): a workgroup of NW waves stages one tile of the plan
-// plus its K-row halos into LDS with global_load_lds DMA and runs K generations LDS -> LDS, the last
-// LDS pass storing to HBM.  COH: the staging DMAs and the output stores are `sc1` (device-coherent:
-// loads that bypass the CU's L1, write-through stores), as wave_runner.hpp's COH streaming wave.
+// gol-mi355x: the LDS tile kernels' device code (step_tile / step_tile_fold in step_kernels.hip): a
+// workgroup of NW waves stages one tile of the plan plus its K-row halos into LDS with global_load_lds
+// DMA and runs K generations LDS -> LDS, the last LDS pass storing to HBM.
 #pragma once
 
 #include "gol/bits.hpp"
@@ -13,8 +11,6 @@
 namespace gol {
 namespace hipk {
 namespace {
-
-constexpr int kCacheSc1 = 16;  // global_load_lds cache-policy operand: sc1 (gfx950: cpol bit 4)
 
 typedef __attribute__((address_space(3))) void lds_void_t;
 typedef __attribute__((address_space(1))) void glb_void_t;
@@ -34,7 +30,7 @@ typedef __attribute__((address_space(1))) void glb_void_t;
 // ------------------------------------------------------------------------------------------
 constexpr int kTileRowU32 = 128;  // one LDS row: 64 lo words then 64 hi words
 
-template <bool LAST, bool COH = false>
+template <bool LAST>
 struct BandSink {
     static constexpr bool kLast = LAST;
     u32* lds;       // !LAST: destination buffer (row-major, kTileRowU32 per row)
@@ -44,7 +40,7 @@ struct BandSink {
     int lane;
     __device__ __forceinline__ void put(u32 lo, u32 hi) {
         if constexpr (LAST) {
-            store_row_word<COH>(st, lo, hi);
+            *st = make_uint2(lo, hi);
             st += st_stride;
         } else {
             lds[row * kTileRowU32 + lane] = lo;
@@ -173,7 +169,7 @@ __host__ __device__ constexpr int tile_side_rows(int lv) { return 2 * lv + 4; }
 //   and writes its output rows back into A.  A wave only ever writes its own band's rows and reads
 //   other bands' rows only from its copy, so one tile buffer suffices: twice the rows per tile in the
 //   160 KiB of LDS (one round of tiles where the double buffer needed two or three).
-template <int NW, int LV, bool IP, bool COH>
+template <int NW, int LV, bool IP>
 __device__ __forceinline__ void tile_pass(u32* A, u32* B, u32* side, u64* dst, const LaneDesc& d,
                                           const StepParams& p, int K, int g, int n_in, int wv, int lane, i64 trash_id) {
     const int lo_r = g + LV, cnt = n_in - 2 * g - 2 * LV;
@@ -212,15 +208,14 @@ __device__ __forceinline__ void tile_pass(u32* A, u32* B, u32* side, u64* dst, c
         const bool out_lane = d.flags & LANE_STORE;
         uint2* st = out_lane ? reinterpret_cast<uint2*>(dst + (i64)(d.row0 + r0 - K + p.R) * p.pitch + (d.col + 1))
                              : reinterpret_cast<uint2*>(p.trash + ((trash_id * NW + wv) & (kTrashWaves - 1)) * 64 + lane);
-        BandSink<true, COH> s{nullptr, st, out_lane ? p.pitch : 0, 0, lane};
+        BandSink<true> s{nullptr, st, out_lane ? p.pitch : 0, 0, lane};
         stream(s);
     }
 }
 
 
-// One tile (plan wave `d` of this lane, nrows > 0): stage, K generations, store.  COH: the staging
-// DMAs and the stores are `sc1` (step_flow's tile items, flow_kernel.hip).
-template <int NW, bool WRAPY, int LV, bool IP, bool COH>
+// One tile (plan wave `d` of this lane, nrows > 0): stage, K generations, store.
+template <int NW, bool WRAPY, int LV, bool IP>
 __device__ __forceinline__ void tile_item(const u64* __restrict__ src, u64* __restrict__ dst, const LaneDesc& d, int nrows,
                                           const StepParams& p, int K, u32* tile_lds, int wv, int lane, i64 trash_id) {
     const int n_in = nrows + 2 * K;
@@ -234,8 +229,8 @@ __device__ __forceinline__ void tile_item(const u64* __restrict__ src, u64* __re
         if (WRAPY) r = r < 0 ? r + p.h : (r >= p.h ? r - p.h : r);
         const u32* g = reinterpret_cast<const u32*>(src + (i64)(r + p.R) * p.pitch + (d.col + 1));
         u32* l = A + i * kTileRowU32;
-        __builtin_amdgcn_global_load_lds((glb_void_t*)g, (lds_void_t*)l, 4, 0, COH ? kCacheSc1 : 0);
-        __builtin_amdgcn_global_load_lds((glb_void_t*)(g + 1), (lds_void_t*)(l + 64), 4, 0, COH ? kCacheSc1 : 0);
+        __builtin_amdgcn_global_load_lds((glb_void_t*)g, (lds_void_t*)l, 4, 0, 0);
+        __builtin_amdgcn_global_load_lds((glb_void_t*)(g + 1), (lds_void_t*)(l + 64), 4, 0, 0);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
@@ -249,12 +244,12 @@ __device__ __forceinline__ void tile_item(const u64* __restrict__ src, u64* __re
         int lv = 1;
         if (LV >= 4 && left >= 4) {
             lv = 4;
-            tile_pass<NW, (LV >= 4 ? 4 : 1), IP, COH>(A, B, side, dst, d, p, K, g, n_in, wv, lane, trash_id);
+            tile_pass<NW, (LV >= 4 ? 4 : 1), IP>(A, B, side, dst, d, p, K, g, n_in, wv, lane, trash_id);
         } else if (LV >= 2 && left >= 2) {
             lv = 2;
-            tile_pass<NW, (LV >= 2 ? 2 : 1), IP, COH>(A, B, side, dst, d, p, K, g, n_in, wv, lane, trash_id);
+            tile_pass<NW, (LV >= 2 ? 2 : 1), IP>(A, B, side, dst, d, p, K, g, n_in, wv, lane, trash_id);
         } else {
-            tile_pass<NW, 1, IP, COH>(A, B, side, dst, d, p, K, g, n_in, wv, lane, trash_id);
+            tile_pass<NW, 1, IP>(A, B, side, dst, d, p, K, g, n_in, wv, lane, trash_id);
         }
         g += lv;
         if (g < K) {
@@ -314,7 +309,7 @@ __host__ __device__ constexpr int fold_buffer_rows(int T) { return (T + 1) / 2 +
 // as step_tile's in-place pass, each wave first copies its band's LV rows above and below into its
 // side rows; the mirrors past the middle are such rows for the middle band, so they too are read from
 // the copy while the pass rewrites them).
-template <int NW, int LV, bool IP, bool COH>
+template <int NW, int LV, bool IP>
 __device__ __forceinline__ void fold_pass(u32* A, u32* B, u32* side, u64* dst, const LaneDesc& d, const StepParams& p,
                                           int K, int g, int T, int wv, int lane, i64 trash_id) {
     const int Th = (T + 1) / 2;
@@ -356,13 +351,13 @@ __device__ __forceinline__ void fold_pass(u32* A, u32* B, u32* side, u64* dst, c
         const bool out_lane = d.flags & LANE_STORE;
         uint2* st = out_lane ? reinterpret_cast<uint2*>(dst + (i64)(d.row0 + t0 - K + p.R) * p.pitch + (d.col + 1))
                              : reinterpret_cast<uint2*>(p.trash + ((trash_id * NW + wv) & (kTrashWaves - 1)) * 64 + lane);
-        BandSink<true, COH> sk{nullptr, st, out_lane ? (half ? -p.pitch : p.pitch) : 0, 0, lane};
+        BandSink<true> sk{nullptr, st, out_lane ? (half ? -p.pitch : p.pitch) : 0, 0, lane};
         stream(sk);
     }
 }
 
-// One folded tile (lanes 32-63 of `d` repeat lanes 0-31; nrows > 0).  COH as tile_item.
-template <int NW, bool WRAPY, int LV, bool IP, bool COH>
+// One folded tile (lanes 32-63 of `d` repeat lanes 0-31; nrows > 0).
+template <int NW, bool WRAPY, int LV, bool IP>
 __device__ __forceinline__ void fold_item(const u64* __restrict__ src, u64* __restrict__ dst, const LaneDesc& d, int nrows,
                                           const StepParams& p, int K, u32* tile_lds, int wv, int lane, i64 trash_id) {
     const int T = nrows + 2 * K;
@@ -380,8 +375,8 @@ __device__ __forceinline__ void fold_item(const u64* __restrict__ src, u64* __re
         if (WRAPY) r = r < 0 ? r + p.h : (r >= p.h ? r - p.h : r);
         const u32* g = reinterpret_cast<const u32*>(src + (i64)(r + p.R) * p.pitch + (d.col + 1));
         u32* l = A + i * kTileRowU32;
-        __builtin_amdgcn_global_load_lds((glb_void_t*)g, (lds_void_t*)l, 4, 0, COH ? kCacheSc1 : 0);
-        __builtin_amdgcn_global_load_lds((glb_void_t*)(g + 1), (lds_void_t*)(l + 64), 4, 0, COH ? kCacheSc1 : 0);
+        __builtin_amdgcn_global_load_lds((glb_void_t*)g, (lds_void_t*)l, 4, 0, 0);
+        __builtin_amdgcn_global_load_lds((glb_void_t*)(g + 1), (lds_void_t*)(l + 64), 4, 0, 0);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
@@ -392,12 +387,12 @@ __device__ __forceinline__ void fold_item(const u64* __restrict__ src, u64* __re
         int lv = 1;
         if (LV >= 4 && left >= 4) {
             lv = 4;
-            fold_pass<NW, (LV >= 4 ? 4 : 1), IP, COH>(A, B, side, dst, d, p, K, g, T, wv, lane, trash_id);
+            fold_pass<NW, (LV >= 4 ? 4 : 1), IP>(A, B, side, dst, d, p, K, g, T, wv, lane, trash_id);
         } else if (LV >= 2 && left >= 2) {
             lv = 2;
-            fold_pass<NW, (LV >= 2 ? 2 : 1), IP, COH>(A, B, side, dst, d, p, K, g, T, wv, lane, trash_id);
+            fold_pass<NW, (LV >= 2 ? 2 : 1), IP>(A, B, side, dst, d, p, K, g, T, wv, lane, trash_id);
         } else {
-            fold_pass<NW, 1, IP, COH>(A, B, side, dst, d, p, K, g, T, wv, lane, trash_id);
+            fold_pass<NW, 1, IP>(A, B, side, dst, d, p, K, g, T, wv, lane, trash_id);
         }
         g += lv;
         if (g < K) {

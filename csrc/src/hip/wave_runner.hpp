@@ -1,12 +1,6 @@
-// gol-mi355x: the streaming wave of the register-pipeline kernels (step_temporal in step_kernels.hip,
-// step_flow in flow_kernel.hip): one wave streams one plan segment (64 word columns, nrows + 2K input
-// rows) through the K-level register pipeline of stencil_device.hpp and stores its output rows.
-//
-// COH (step_flow): every load of a board row and every store of an output row is an agent-scope
-// relaxed atomic, i.e. `global_load/store ... sc1` on gfx950: the stores write through to memory and
-// the loads bypass the CU's L1, so a wave of the SAME launch may consume rows another CU produced once
-// it has seen that CU's completion flag (flow_kernel.hip has the protocol).  The plain variant (COH
-// false) is what step_temporal runs: there, kernel boundaries order the passes.
+// gol-mi355x: the streaming wave of the register-pipeline kernel (step_temporal in step_kernels.hip): one
+// wave streams one plan segment (64 word columns, nrows + 2K input rows) through the K-level register
+// pipeline of stencil_device.hpp and stores its output rows.  Kernel boundaries order the passes.
 #pragma once
 
 #include "gol/bits.hpp"
@@ -17,34 +11,11 @@ namespace gol {
 namespace hipk {
 namespace {
 
-template <bool COH>
-__device__ __forceinline__ uint2 load_row_word(const uint2* p) {
-    if constexpr (COH) {
-        const u64 v = __hip_atomic_load(reinterpret_cast<const u64*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        return make_uint2((u32)v, (u32)(v >> 32));
-    } else {
-        return *p;
-    }
-}
-template <bool COH>
-__device__ __forceinline__ void store_row_word(uint2* p, u32 lo, u32 hi) {
-    if constexpr (COH)
-        __hip_atomic_store(reinterpret_cast<u64*>(p), ((u64)hi << 32) | lo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    else
-        *p = make_uint2(lo, hi);
-}
-
-// A row load of the wave runner: the plain dereference unless COH.  (Written in place, not through
-// load_row_word<false>: routing the plain loads through the helper changed the K = 12 kernel's
-// schedule — 256 VGPRs with AGPR spills and a vmcnt(0) before the stores in the row loop, the pass
-// 119 -> 163 us at 32768^2 — although the helper inlines to the same load.)
-#define ROW_LOAD_INTO(dst)                            \
-    do {                                             \
-        if constexpr (COH)                           \
-            (dst) = load_row_word<true>(ld);         \
-        else                                         \
-            (dst) = *ld;                             \
-    } while (0)
+// A row load of the wave runner: a plain dereference, written in place.  (Routing the loads through
+// an inline helper once changed the K = 12 kernel's schedule -- 256 VGPRs with AGPR spills and a
+// vmcnt(0) before the stores in the row loop, the pass 119 -> 163 us at 32768^2 -- although the helper
+// inlines to the same load.)
+#define ROW_LOAD_INTO(dst) ((dst) = *ld)
 
 // Row prefetch: a register triple loaded one row-triple ahead, pinned above the compute with a
 // sched_barrier (otherwise the scheduler sinks the loads to the end of the loop body).  (An LDS
@@ -77,7 +48,7 @@ constexpr bool pingpong_loop() {
     return K < 32 && (((kPingpongMask >> K) & 1) != 0 || (ROWS == 0 && ((kPingpongGhostMask >> K) & 1) != 0));
 }
 
-template <int K, int ROWS, bool COH = false>
+template <int K, int ROWS>
 struct WaveRunner {
     static constexpr int D = prefetch_rows<K>();
     const StepParams& p;
@@ -156,7 +127,7 @@ struct WaveRunner {
     template <int PH, bool GUARD>
     __device__ __forceinline__ void compute_store(u32 lo, u32 hi, int i) {
         if (!advance<K, PH, GUARD>(P, lo, hi, i)) return;
-        if constexpr (COH) store_row_word<true>(st, lo, hi); else *st = make_uint2(lo, hi);
+        *st = make_uint2(lo, hi);
         st += st_stride;
     }
 

@@ -177,14 +177,13 @@ EngineConfig engine_config(const Options& o, const std::string& backend, int dev
         return env_str(name, "auto") == "auto" ? -1 : (int)(env_int(name, 0) != 0);
     };
     c.subtile_overlap = env_str("GOL_SUBTILE_OVERLAP", "auto") == "auto" ? -1 : (int)env_int("GOL_SUBTILE_OVERLAP", 0);
-    c.subtile_graphs = tri("GOL_SUBTILE_GRAPHS");
     c.self_exchange = env_int("GOL_SELF_EXCHANGE", 0) != 0;
     c.force_split = env_int("GOL_FORCE_SPLIT", 0) != 0;
     c.graph_rccl = tri("GOL_GRAPH_RCCL");
     c.plan_xcds = (int)env_int("GOL_PLAN_XCDS", 8);
     c.sched = env_str("GOL_SCHEDULE", "auto");
-    if (c.sched != "auto" && c.sched != "split" && c.sched != "full" && c.sched != "flow" && c.sched != "flow+ov")
-        throw Error("GOL_SCHEDULE must be auto, split, full, flow or flow+ov (got " + c.sched + ")");
+    if (c.sched != "auto" && c.sched != "split" && c.sched != "full")
+        throw Error("GOL_SCHEDULE must be auto, split or full (got " + c.sched + ")");
     return c;
 }
 

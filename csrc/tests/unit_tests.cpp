@@ -623,163 +623,9 @@ static void test_plan_age_weights() {
     }
 }
 
-// Flow plans (plan.hpp build_flow_plan, flow_kernel.hip): race freedom checked exhaustively.  Two items
-// may run concurrently unless one is an ancestor of the other in the dependency graph; for every such
-// pair, no cell of a buffer may be written by one and read or written by the other.  Also: every
-// dependency is an earlier ticket of the previous pass, each pass covers its regions exactly once, and
-// a pass's first items depend only on early items of the pass before (the torus-wrap band rotation).
-static void test_flow_plan() {
-    struct Case {
-        i64 nw, h;
-        std::vector<int> cut;
-        i64 rows;
-        bool xwrap, wrap_y;
-        int ext;  // ghost-row extension per remaining generation (1: y neighbours, multi-pass)
-        bool fold = false;  // folded 32-lane tile items (step_flow_tile)
-    };
-    const std::vector<Case> cases = {
-        {3, 48, {2, 2, 1}, 8, true, true, 0},   {5, 40, {3, 3}, 7, true, true, 0},
-        {1, 30, {1, 2, 3}, 6, true, true, 0},   {130, 24, {2, 2}, 5, true, true, 0},
-        {4, 40, {3, 2, 2}, 9, false, false, 1}, {2, 36, {2, 2, 2, 2}, 6, true, false, 1},
-        {64, 64, {4, 4}, 16, true, true, 0},
-        // folded tile items (plans of 32-lane tiles, lanes 32-63 repeating 0-31), torus and ghost rows
-        {64, 120, {6, 5, 6}, 30, true, true, 0, true}, {70, 96, {4, 4}, 28, false, false, 1, true},
-    };
-    for (const Case& cs : cases) {
-        std::vector<FlowPass> ps;
-        int left = 0;
-        for (int k : cs.cut) left += k;
-        for (int k : cs.cut) {
-            left -= k;
-            const i64 e = cs.ext ? left : 0;
-            ps.push_back({k, {{-e, cs.h + e, 0, cs.nw}}, cs.rows, cs.fold});
-        }
-        FlowPlan fp;
-        const bool mark = cs.ext != 0;  // ranks with neighbours: the exchange-overlapped variant's plan
-        const std::string err = build_flow_plan(ps, cs.nw, cs.h, cs.xwrap, cs.wrap_y, fp, mark);
-        CHECK(err.empty());
-        if (!err.empty()) {
-            fprintf(stderr, "  build_flow_plan: %s\n", err.c_str());
-            continue;
-        }
-        const size_t n = fp.items.size();
-        CHECK(fp.pass_begin.size() == cs.cut.size() + 1 && fp.pass_begin.back() == n && fp.lanes.size() == n * 64);
-        // every store of pass j covers its region exactly once
-        const i64 R = 16, rows_all = cs.h + 2 * R, cols_all = cs.nw + 2;
-        for (size_t j = 0; j < cs.cut.size(); ++j) {
-            std::vector<int> cov((size_t)(rows_all * cols_all), 0);
-            for (u32 t = fp.pass_begin[j]; t < fp.pass_begin[j + 1]; ++t) {
-                CHECK((fp.items[t].pass & ~FLOW_ITEM_EXCH) == j && fp.items[t].depth == (u32)cs.cut[j]);
-                for (int l = 0; l < (cs.fold ? 32 : 64); ++l) {  // (folded tiles: lanes 32-63 repeat 0-31)
-                    const LaneDesc& d = fp.lanes[(size_t)t * 64 + l];
-                    if (!(d.flags & LANE_STORE)) continue;
-                    for (i64 r = d.row0; r < d.row0 + d.nrows; ++r) cov[(size_t)((r + R) * cols_all + d.col + 1)]++;
-                }
-            }
-            const Region& g = ps[j].regions[0];
-            bool exact = true;
-            for (i64 r = -R; r < cs.h + R; ++r)
-                for (i64 c = -1; c <= cs.nw; ++c) {
-                    const bool in = r >= g.r0 && r < g.r1 && c >= g.c0 && c < g.c1;
-                    exact = exact && cov[(size_t)((r + R) * cols_all + c + 1)] == (in ? 1 : 0);
-                }
-            CHECK(exact);
-        }
-        // dependencies: earlier tickets of the previous pass
-        bool order_ok = true;
-        for (u32 t = 0; t < n; ++t)
-            for (u32 q = 0; q < fp.items[t].ndeps; ++q) {
-                const u32 d = fp.deps[fp.items[t].dep_off + q];
-                order_ok = order_ok && d < t && (fp.items[d].pass & ~FLOW_ITEM_EXCH) + 1 == (fp.items[t].pass & ~FLOW_ITEM_EXCH);
-            }
-        CHECK(order_ok);
-        // ancestors (transitive closure; deps point backwards, so one forward sweep)
-        std::vector<std::vector<char>> anc(n, std::vector<char>(n, 0));
-        for (u32 t = 0; t < n; ++t)
-            for (u32 q = 0; q < fp.items[t].ndeps; ++q) {
-                const u32 d = fp.deps[fp.items[t].dep_off + q];
-                anc[t][d] = 1;
-                for (u32 x = 0; x < d; ++x)
-                    if (anc[d][x]) anc[t][x] = 1;
-            }
-        // access sets per item: cell (buffer, row, col) -> read / write
-        auto cell = [&](int buf, i64 r, i64 c) {
-            const i64 rr = cs.wrap_y ? pmod(r, cs.h) : r;
-            return ((size_t)buf * (size_t)rows_all + (size_t)(rr + R)) * (size_t)cols_all + (size_t)(c + 1);
-        };
-        std::vector<std::vector<size_t>> rd(n), wr(n);
-        for (u32 t = 0; t < n; ++t) {
-            const int in = (int)(fp.items[t].pass & 1), out = in ^ 1, k = (int)fp.items[t].depth;
-            for (int l = 0; l < 64; ++l) {
-                const LaneDesc& d = fp.lanes[(size_t)t * 64 + l];
-                if (d.nrows <= 0) continue;
-                for (i64 r = d.row0 - k; r < d.row0 + d.nrows + k; ++r) rd[t].push_back(cell(in, r, d.col));
-                if (d.flags & LANE_STORE)
-                    for (i64 r = d.row0; r < d.row0 + d.nrows; ++r) wr[t].push_back(cell(out, r, d.col));
-            }
-            for (auto* v : {&rd[t], &wr[t]}) {
-                std::sort(v->begin(), v->end());
-                v->erase(std::unique(v->begin(), v->end()), v->end());
-            }
-        }
-        auto meet = [](const std::vector<size_t>& x, const std::vector<size_t>& y) {
-            size_t i = 0, j = 0;
-            while (i < x.size() && j < y.size()) {
-                if (x[i] == y[j]) return true;
-                if (x[i] < y[j])
-                    ++i;
-                else
-                    ++j;
-            }
-            return false;
-        };
-        int races = 0;
-        for (u32 m = 0; m < n; ++m)
-            for (u32 t = 0; t < m; ++t) {
-                if (anc[m][t]) continue;
-                if (meet(wr[t], wr[m]) || meet(wr[t], rd[m]) || meet(rd[t], wr[m])) ++races;
-            }
-        CHECK(races == 0);
-        // exchange marks: exactly the first pass's items that read a cell outside the tile
-        bool marks_ok = true;
-        for (u32 t = 0; t < n; ++t) {
-            const FlowItem& f = fp.items[t];
-            bool ghost = false;
-            for (int l = 0; l < 64; ++l) {
-                const LaneDesc& d = fp.lanes[(size_t)t * 64 + l];
-                if (d.nrows <= 0) continue;
-                ghost = ghost || d.col < 0 || d.col >= cs.nw ||
-                        (!cs.wrap_y && (d.row0 - (i64)f.depth < 0 || d.row0 + d.nrows + (i64)f.depth > cs.h));
-            }
-            const bool want = mark && (f.pass & ~FLOW_ITEM_EXCH) == 0 && ghost;
-            marks_ok = marks_ok && ((f.pass & FLOW_ITEM_EXCH) != 0) == want;
-        }
-        CHECK(marks_ok);
-        if (races) fprintf(stderr, "  flow plan nw %lld h %lld: %d racing item pairs\n", (long long)cs.nw, (long long)cs.h, races);
-        // the first item of every later pass waits only for items in the first half of the pass before
-        // (plans without packed narrow segments: a wave packing segments of several bands depends on
-        // all of them)
-        bool early = true, packed = false;
-        for (size_t w = 0; w < n; ++w)
-            for (int l = 0; l < 64; ++l) packed = packed || fp.lanes[w * 64 + l].row0 != fp.lanes[w * 64].row0;
-        for (size_t j = 1; j < cs.cut.size() && !packed; ++j) {
-            const FlowItem& f = fp.items[fp.pass_begin[j]];
-            const u32 half = fp.pass_begin[j - 1] + (fp.pass_begin[j] - fp.pass_begin[j - 1]) / 2 + 1;
-            for (u32 q = 0; q < f.ndeps; ++q) {
-                if (fp.deps[f.dep_off + q] > half)
-                    fprintf(stderr, "  flow plan nw %lld h %lld pass %zu: first item waits for item %u (pass starts %u, half %u)\n",
-                            (long long)cs.nw, (long long)cs.h, j, fp.deps[f.dep_off + q], fp.pass_begin[j - 1], half);
-                early = early && fp.deps[f.dep_off + q] <= half;
-            }
-        }
-        CHECK(early);
-    }
-}
-
 int main() {
     test_band_tile_plan();
     test_plan_age_weights();
-    test_flow_plan();
     test_watchdog();
     test_plan_rounds();
     test_cli();

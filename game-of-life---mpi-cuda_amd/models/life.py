@@ -112,7 +112,7 @@ class Simulation:
         cfg.tune_tile_waves = "GOL_TILE_WAVES" not in os.environ
         cfg.sub_occ = int(sub_occ)
         # 1 on / 0 off / -1 auto: a candidate of the init-time schedule timing (GOL_* env defaults)
-        if subtile_overlap is None:  # 0 off, 1 half 0 only, 2 both halves, auto: timed candidates
+        if subtile_overlap is None:  # 0 off, 1 on (half 0's interior overlaps the exchange), auto: timed
             v = os.environ.get("GOL_SUBTILE_OVERLAP", "auto")
             subtile_overlap = -1 if v == "auto" else int(v)
         cfg.subtile_overlap = int(subtile_overlap)
@@ -120,7 +120,6 @@ class Simulation:
         cfg.force_split = bool(force_split)
         cfg.sched = schedule
         cfg.graph_rccl = _tri("GOL_GRAPH_RCCL")
-        cfg.subtile_graphs = _tri("GOL_SUBTILE_GRAPHS")
         cfg.plan_xcds = int(os.environ.get("GOL_PLAN_XCDS", "8"))
         if self.backend == "hip":
             n = _gol.hip_device_count()

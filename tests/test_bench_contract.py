@@ -104,16 +104,16 @@ def test_bench_rank_problems():
     sys.path.insert(0, REPO)
     import bench
 
-    same = [{"schedule": "full+flow", "kernel": "flow", "depth": 128}] * 4
+    same = [{"schedule": "full+subtiles2ov", "kernel": "temporal", "depth": 128}] * 4
     assert bench.rank_problems(same, 4, 4) == []
     assert bench.rank_problems(same, 4, None) == []  # host transport: no communicator to check
     diff = same[:3] + [{"schedule": "full+subtiles2", "kernel": "temporal", "depth": 128}]
     (p,) = bench.rank_problems(diff, 4, 4)
     assert "disagree" in p and "3:full+subtiles2/temporal/128" in p
     # a per-rank kernel choice is reported, not an error; a halo depth mismatch is
-    kern = same[:3] + [{"schedule": "full+flow", "kernel": "pipe@24", "depth": 128}]
+    kern = same[:3] + [{"schedule": "full+subtiles2ov", "kernel": "pipe@24", "depth": 128}]
     assert bench.rank_problems(kern, 4, 4) == []
-    (p,) = bench.rank_problems(same[:3] + [{"schedule": "full+flow", "kernel": "flow", "depth": 64}], 4, 4)
+    (p,) = bench.rank_problems(same[:3] + [{"schedule": "full+subtiles2ov", "kernel": "temporal", "depth": 64}], 4, 4)
     assert "disagree" in p
     (p,) = bench.rank_problems(same, 4, 2)
     assert "spans 2 of 4" in p

@@ -20,8 +20,6 @@ for c in "$@"; do
     cfg1) step cfg1_cpu_256 120 env GOL_BACKEND=cpu ./build/gol 5 256 100 256 0 ;;
     cfg2) step cfg2_cli_8192 120 env GOL_BACKEND=hip ./build/gol 5 8192 1000 256 0 ;;
     cfg2b) step cfg2_bench_8192 120 python bench.py --size 8192 --steps 1000 --warmup 100 ;;
-    cfg2f) step cfg2_cli_8192_flow 120 env GOL_BACKEND=hip GOL_SCHEDULE=flow ./build/gol 5 8192 1000 256 0 ;;
-    cfg2nf) step cfg2_cli_8192_flowtimed 120 env GOL_BACKEND=hip GOL_FLOW=1 ./build/gol 5 8192 1000 256 0 ;;
     cfg3) step cfg3_bench_32768 300 python bench.py --size 32768 --steps 2000 --warmup 200 ;;
     cfg4) step cfg4_bench_65536_2d 300 python bench.py --size 65536 --scaling strong --decomp 2d --steps 400 --warmup 40 ;;
     cfg5) step cfg5_capacity_1048576 600 python bench.py --size 1048576 --steps 16 --warmup 8 ;;
