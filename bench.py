@@ -81,6 +81,16 @@ def rank_problems(ranks, P, rccl_ranks):
     return problems
 
 
+def prediction_fields(predicted_us, measured_us):
+    """The engine's init-time prediction of this run next to the measurement: the chosen schedule timed at
+    the end of init the way the run executes it (same supersteps, graph replay or eager launches, after a
+    device barrier, from an idle GPU; median of a few samples, max over ranks).  None where the backend
+    does not measure one (CPU)."""
+    p = round(float(predicted_us), 3) if predicted_us else None
+    return {"sched_predicted_us_per_gen": p,
+            "predicted_over_measured": round(p / measured_us, 4) if p and measured_us > 0 else None}
+
+
 def _free_port() -> int:
     with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
         s.bind(("127.0.0.1", 0))
@@ -353,6 +363,7 @@ def main() -> int:
                 "init_s_per_rank": init_per_rank,
             },
             "start_skew_us": round(start_skew * 1e6, 2),
+            **prediction_fields(st.get("predicted_us_per_gen"), elapsed / steps * 1e6),
             "phases": phases,
             "per_rank": per_rank_block,
             "baseline_note": "reference publishes no numbers (BASELINE.md); vs_baseline is null",

@@ -87,6 +87,11 @@ struct EngineStats {
     int tile_waves = 0;       // HIP: workgroup size of the LDS tile kernel (waves)
     i64 plan_waves = 0;       // waves of the full-tile plan
     double lane_efficiency = 0;  // output words / (64 * input rows * waves) for the full plan
+    // HIP: us per generation of the chosen schedule, timed at the end of init the way a hinted run
+    // executes (same supersteps, graphs or eager launches, after a device barrier, from an idle GPU);
+    // 0 when not measured
+    double predicted_us_per_gen = 0;
+    int predicted_gens = 0;     // generations of the timed supersteps behind it
     double t_exchange_ms = 0;  // profile only
     double t_compute_ms = 0;   // profile only
     std::string kernel;        // stencil kernel in use (HIP: temporal | tile | lds; CPU: cpu)

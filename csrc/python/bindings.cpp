@@ -100,6 +100,8 @@ py::dict stats_dict(const EngineStats& s) {
     d["depth"] = s.depth;
     d["plan_waves"] = s.plan_waves;
     d["lane_efficiency"] = s.lane_efficiency;
+    d["predicted_us_per_gen"] = s.predicted_us_per_gen;
+    d["predicted_gens"] = s.predicted_gens;
     d["t_exchange_ms"] = s.t_exchange_ms;
     d["t_compute_ms"] = s.t_compute_ms;
     d["kernel"] = s.kernel;

@@ -7,6 +7,8 @@
 // ones read).  With neighbours, the first pass runs one of two schedules (chosen by measurement):
 //   split:  s_comm:  wait(ev_ready) -> pack (2-D) -> RCCL group send/recv (or host staging) -> unpack -> ev_halo
 //           s_comp:  interior kernel -> wait(ev_halo) -> boundary kernel -> later passes -> ev_ready
+//           (a one-pass superstep runs its boundary kernel on s_comm after the exchange instead,
+//           concurrently with the interior, and joins the streams at the next superstep)
 //   full:   s_comp:  exchange -> full-region kernel -> later passes
 // With graphs on, G/(m*R) captures of m supersteps (even pass count => parity preserved) are replayed.
 //
@@ -309,10 +311,16 @@ void HipEngine::do_init(const PatternSpec& p) {
         };
         kick("init: kernel autotune");
         if (cfg_.kernel == "auto" || cfg_.kernel == "resident") autotune_kernel();
-        kick("init: schedule timing");
-        choose_schedule();  // collective when ranks have neighbours
+        // The one-tile pass costs first: the schedule candidates are timed on the pass cuts the runs
+        // will use (config 3's strip: one step_pipe pass of 20 instead of 7 + 7 + 6 changed the winner)
         kick("init: pass costs");
         measure_pass_costs();
+        kick("init: schedule timing");
+        choose_schedule();  // collective when ranks have neighbours
+        if (dual_) {
+            kick("init: pass costs");
+            measure_pass_costs();  // the two halves' (the sub-tile candidates ran the default cuts)
+        }
         kick("init: plans and graphs");
         tuned_ = true;
         passes_.clear();  // the pass cuts may depend on the tuned kernel (pass_depths)
@@ -324,20 +332,35 @@ void HipEngine::do_init(const PatternSpec& p) {
     }
     stats_.kernel = split_ ? kern_[1] + "+boundary:" + kern_[2] : (dual_ ? std::string("temporal") : kern_[0]);
     if (!split_ && !dual_ && kern_[0] == "pipe")
-        stats_.kernel = strprintf("pipe@%d(%dx%d,%d/CU)", pipe_k_, pipe_nw_ - 1, pipe_l_, pipe_wg_);
+        stats_.kernel = strprintf("pipe@%d(%dx%d,%d/CU)", pipe_k_, pipe_cur_.nw - 1, pipe_cur_.l, pipe_cur_.wg);
     if (res_) {
         const ResPlan& rp = res_plan(res_kin_);
         stats_.kernel = strprintf("resident@%d(%lld tiles x %d waves x %d rows)", res_kin_, (long long)rp.tiles, rp.nw, rp.B);
     }
     stats_.schedule = split_ ? "split" : (halo_items(L_.R).empty() ? "local" : "full");
-    if (dual_) stats_.schedule += sub_overlap_ ? "+subtiles2ov" : "+subtiles2";
+    if (dual_) stats_.schedule += sub_overlap_ == 2 ? "+subtiles2xf" : (sub_overlap_ ? "+subtiles2ov" : "+subtiles2");
     stats_.kernel_depth = dual_ ? tdepth_ : kdepth_;
     stats_.tile_waves = cfg_.tile_waves;
     std::string tn;
     for (const auto& kv : tune_ms_) tn += strprintf("%s%s=%.3fus/gen", tn.empty() ? "" : " ", kv.first.c_str(), kv.second * 1e3);
     for (const auto& kv : sched_us_)
         tn += strprintf("%ssched:%s=%.3fus/gen", tn.empty() ? "" : " ", kv.first.c_str(), kv.second);
-    for (const auto& kv : pass_us_) tn += strprintf("%spass%d=%.1fus", tn.empty() ? "" : " ", kv.first, kv.second);
+    for (const auto& kv : pass_costs()) tn += strprintf("%spass%d=%.1fus", tn.empty() ? "" : " ", kv.first, kv.second);
+    // the kernel passes of the supersteps the runs use (the full superstep, the hinted run's remainder)
+    if (!dual_ && !res_ && kernel_ != "lds")
+        for (int k : init_depths()) {
+            std::string c;
+            const std::vector<int>& ps = pass_depths(k);
+            for (size_t j = 0; j < ps.size(); ++j) {
+                const int kind = j == 0 && split_ ? 1 : 0;
+                const PipeGeo* g = pipe_geo(ps[j]);
+                const PassKernel pk = pass_kernel(kind, ps[j]);
+                c += (j ? "+" : "") + (pk == PK_PIPE   ? strprintf("pipe@%d(%dx%d,%d/CU)", ps[j], g->nw - 1, g->l, g->wg)
+                                       : pk == PK_TILE ? strprintf("tile@%d", ps[j])
+                                                       : strprintf("temporal@%d", ps[j]));
+            }
+            tn += strprintf("%scut%d=%s", tn.empty() ? "" : " ", k, c.c_str());
+        }
     if (!split_ && !dual_ && !res_ && tile_kernel(0) && kernel_ != "lds") {  // the tile variant the full superstep runs
         const DevPlan& p0 = plan(0, kdepth_, 0);
         tn += strprintf("%stile_plan=%s,%lldrows,%lldtiles", tn.empty() ? "" : " ",
@@ -370,6 +393,7 @@ void HipEngine::do_init(const PatternSpec& p) {
         stats_.graph_launches = 0;
     }
     spin_up();  // init ends with the GPU at its steady clock (plan building and captures idle it)
+    predict_run();
     if (res_) {
         stats_.plan_waves = res_plan(res_kin_).tiles;  // workgroups of the resident launch
         stats_.lane_efficiency = 0;
@@ -392,6 +416,7 @@ void HipEngine::tile_superstep(int k) {
     for (size_t j = 1; j < ps.size(); ++j) {
         // later passes need no halo: the ghost rows computed by the earlier passes carry the
         // neighbours' cells forward (communication-avoiding deep halos)
+        join_halo();
         const i64 e = ext_after(ps, j);
         launch(0, ps[j], e, buf_[cur_], buf_[cur_ ^ 1], s_comp_);
         post(buf_[cur_ ^ 1], s_comp_, e);
@@ -405,6 +430,7 @@ void HipEngine::tile_superstep(int k) {
 // boundary bands with the exchange overlapped (else exchange, then one full-region kernel).
 void HipEngine::first_pass(int kx, int kp, i64 e, bool split) {
     prepare(kx);
+    join_halo();
     u64* src = buf_[cur_];
     u64* dst = buf_[cur_ ^ 1];
     const std::vector<HaloItem>& items = items_for(kx);
@@ -427,35 +453,28 @@ void HipEngine::first_pass(int kx, int kp, i64 e, bool split) {
             HIP_CHECK(hipStreamWaitEvent(s_comm_, ev_ready_, 0));
             HIP_CHECK(hipEventRecord(ev_halo_, s_comm_));
             launch(1, kp, 0, src, dst, s_comp_);
-        } else if (device_transport_ && capturing()) {
-            // Inside a graph capture the RCCL group goes on the capture's origin stream (a group on the
-            // stream forked into the capture crashed in librccl, MI355X / ROCm 7.2), the interior on the
-            // forked one: the same graph.  Bands after the exchange (GOL_SPLIT_BANDS_COMM: concurrently
-            // with the interior; else after it too), joined before the later passes.
-            HIP_CHECK(hipStreamWaitEvent(s_comm_, ev_ready_, 0));
-            launch(1, kp, 0, src, dst, s_comm_);
-            HIP_CHECK(hipEventRecord(ev_halo_, s_comm_));
-            exchange_device(kx, items, cur_, s_comp_);
-            if (!bands_comm_) HIP_CHECK(hipStreamWaitEvent(s_comp_, ev_halo_, 0));
-            launch(2, kp, e, src, dst, s_comp_);
-            post(dst, s_comp_, e);
-            HIP_CHECK(hipStreamWaitEvent(s_comp_, ev_halo_, 0));
-            mark_ready();
-            return;
         } else if (device_transport_) {
-            HIP_CHECK(hipStreamWaitEvent(s_comm_, ev_ready_, 0));
+            // The exchange on the comm stream (it waits only for the previous superstep), the interior
+            // on the compute stream meanwhile.  A superstep of ONE pass (e == 0) also runs its bands on
+            // the comm stream, right after the exchange and concurrently with the interior, and leaves
+            // the two streams unjoined: the next superstep, or whatever reads the board, joins them
+            // (join_halo).  A wait on an event still pending costs the waiting queue ~17 us after the
+            // event, more than the ~14 us exchange it would hide (kernel traces of config 3's strip,
+            // profiles/strip_split_round5.txt); with later passes the bands follow the interior on the
+            // compute stream, whose wait then finds the exchange done.
+            const bool bands_comm = e == 0 && !prof;
+            wait_pending(s_comm_, ev_ready_);
             if (prof) HIP_CHECK(hipEventRecord(ev_t0_, s_comm_));
             exchange_device(kx, items, cur_, s_comm_);
             if (prof) HIP_CHECK(hipEventRecord(ev_t1_, s_comm_));
-            if (!bands_comm_) HIP_CHECK(hipEventRecord(ev_halo_, s_comm_));
+            if (!bands_comm) record_halo();
             if (prof) HIP_CHECK(hipEventRecord(ev_t2_, s_comp_));
             launch(1, kp, 0, src, dst, s_comp_);
-            if (bands_comm_) {
+            if (bands_comm) {
                 launch(2, kp, e, src, dst, s_comm_);
                 post(dst, s_comm_, e);
-                HIP_CHECK(hipEventRecord(ev_halo_, s_comm_));
-                HIP_CHECK(hipStreamWaitEvent(s_comp_, ev_halo_, 0));
-                if (prof) record_profile(true);
+                record_halo();
+                halo_pending_ = true;
                 mark_ready();
                 return;
             }
@@ -512,10 +531,12 @@ void HipEngine::launch(int kind, int k, i64 e, const u64* src, u64* dst, hipStre
         const DevPlan& p = plan(kind, k, e);
         if (p.st.out_words == 0) return;
         hipk::StepParams sp{L_.pitch, (i32)L_.h, (i32)L_.nw, L_.R, step_flags() | p.tflags};
-        if (tile_kernel(kind)) {
+        const PassKernel pk = pass_kernel(kind, k);
+        if (pk == PK_TILE) {
             hipk::launch_step_tile(cfg_.tile_waves, k, src, dst, p.d, p.waves, p.rows, sp, s);
-        } else if (pipe_pass(kind, k)) {
-            hipk::launch_step_pipe(pipe_nw_, pipe_l_, src, dst, p.d, p.waves, sp, s);
+        } else if (pk == PK_PIPE) {
+            const PipeGeo* g = pipe_geo(k);
+            hipk::launch_step_pipe(g->nw, g->l, src, dst, p.d, p.waves, sp, s);
             pipe_used_ = true;
         } else
             hipk::launch_step(k, src, dst, p.d, p.waves, sp, s);

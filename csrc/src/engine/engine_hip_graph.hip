@@ -22,6 +22,10 @@ bool HipEngine::graph_shape(int& k, int& m) {
     // or forced with GOL_GRAPH_RCCL=1; eager otherwise (an eager exchange keeps RCCL's own error
     // handling, and with R-deep supersteps the eager launch cost is small).
     if (!local && !graph_rccl_on_) return false;
+    // Split supersteps with an exchange stay eager: captured (the RCCL group on the capture's origin
+    // stream, the interior on a forked one) the exchange kernel started ~140 us into the replay,
+    // 5.5 ms per 20-generation strip run against 4.1-4.9 eager (profiles/strip_split_round5.txt).
+    if (!local && split_) return false;
     return true;
 }
 
@@ -80,6 +84,7 @@ void HipEngine::run_graphed(u64& generations) {
 void HipEngine::replay(hipGraphExec_t exec, int k, int m, int rem) {
     const u64 per = (u64)m * (u64)k + (u64)rem;
     maybe_inject_fault();
+    join_halo();
     {
         trace::Range r("gol.graph_launch");
         HIP_CHECK(hipGraphLaunch(exec, s_comp_));
@@ -109,6 +114,7 @@ hipGraphExec_t HipEngine::graph_for(int k, int m, int rem) {
     hipGraph_t graph = nullptr;
     hipGraphExec_t exec = nullptr;
     const int p0 = par();
+    join_halo();  // (never inside the capture)
     try {
         HIP_CHECK(hipStreamBeginCapture(s_comp_, hipStreamCaptureModeRelaxed));
         mark_ready();  // fork points for the comm stream, recorded inside the capture

@@ -17,22 +17,42 @@ const std::vector<int>& HipEngine::pass_depths(int k) {
     if (res_) return passes_.emplace(key, std::vector<int>{k}).first->second;  // one resident launch
     // every kind may be temporal, unless only the (any-depth) tile kernel runs; sub-tiles always
     // run the temporal kernel at its own depth
+    const bool any_depth = !dual_ && (cfg_.kernel == "tile" || (tuned_ && !split_ && tile_kernel(0)));
+    auto ok = [&](int d) { return any_depth || hipk::step_depth_supported(d); };
+    const int K = std::max(1, dual_ ? tdepth_ : kdepth_);
+    std::vector<int> ps;
+    if (!pass_costs().empty() && !any_depth) {
+        // cheapest cut by the measured per-depth pass times (dynamic programming over k; the depths
+        // include step_pipe geometries when that is the tuned kernel: measure_pass_costs)
+        std::vector<double> best((size_t)k + 1, 1e300);
+        std::vector<int> pick((size_t)k + 1, 0);
+        best[0] = 0;
+        for (int x = 1; x <= k; ++x)
+            for (const auto& dc : pass_costs())
+                if (dc.first <= x && best[(size_t)(x - dc.first)] + dc.second < best[(size_t)x]) {
+                    best[(size_t)x] = best[(size_t)(x - dc.first)] + dc.second;
+                    pick[(size_t)x] = dc.first;
+                }
+        for (int x = k; x > 0; x -= pick[(size_t)x]) ps.push_back(pick[(size_t)x]);
+        std::sort(ps.begin(), ps.end(), std::greater<int>());  // deepest first (8 + 12 measured slower than 12 + 8)
+        return passes_.emplace(key, ps).first->second;
+    }
     if (!dual_ && kern_[0] == "pipe" && pipe_k_ > 0 && !split_) {
-        // whole step_pipe passes; the remainder in step_temporal passes of <= tdepth_, as equal as
-        // the instantiated depths allow (greedy otherwise)
+        // (before the pass costs are measured) whole step_pipe passes; the remainder in step_temporal
+        // passes of <= tdepth_, as equal as the instantiated depths allow (greedy otherwise)
         std::vector<int> v;
         int left = k;
         for (; left >= pipe_k_; left -= pipe_k_) v.push_back(pipe_k_);
         const size_t m = v.size();
         if (left > 0) {
             const int n = (left + tdepth_ - 1) / tdepth_;
-            bool ok = true;
+            bool okd = true;
             for (int j = 0; j < n; ++j) {
                 const int d = left / n + (j < left % n ? 1 : 0);
-                ok = ok && hipk::step_depth_supported(d);
+                okd = okd && hipk::step_depth_supported(d);
                 v.push_back(d);
             }
-            if (!ok) {
+            if (!okd) {
                 v.resize(m);
                 while (left > 0) {
                     const int d = supported_kernel_depth(std::min(left, tdepth_));
@@ -42,25 +62,6 @@ const std::vector<int>& HipEngine::pass_depths(int k) {
             }
         }
         return passes_.emplace(key, v).first->second;
-    }
-    const bool any_depth = !dual_ && (cfg_.kernel == "tile" || (tuned_ && !split_ && tile_kernel(0)));
-    auto ok = [&](int d) { return any_depth || hipk::step_depth_supported(d); };
-    const int K = std::max(1, dual_ ? tdepth_ : kdepth_);
-    std::vector<int> ps;
-    if (tuned_ && !pass_us_.empty() && !any_depth) {
-        // cheapest cut by the measured per-depth pass times (dynamic programming over k)
-        std::vector<double> best((size_t)k + 1, 1e300);
-        std::vector<int> pick((size_t)k + 1, 0);
-        best[0] = 0;
-        for (int x = 1; x <= k; ++x)
-            for (const auto& dc : pass_us_)
-                if (dc.first <= x && best[(size_t)(x - dc.first)] + dc.second < best[(size_t)x]) {
-                    best[(size_t)x] = best[(size_t)(x - dc.first)] + dc.second;
-                    pick[(size_t)x] = dc.first;
-                }
-        for (int x = k; x > 0; x -= pick[(size_t)x]) ps.push_back(pick[(size_t)x]);
-        std::sort(ps.begin(), ps.end(), std::greater<int>());  // deepest first (8 + 12 measured slower than 12 + 8)
-        return passes_.emplace(key, ps).first->second;
     }
     const int n = (k + K - 1) / K;
     bool balanced = true;
@@ -113,15 +114,16 @@ const DevPlan& HipEngine::plan(int kind, int k, i64 e) {
     // ghost words when x has neighbours (so one plan serves every e of a local rank)
     const i64 ek = self_y() ? (self_x() ? 0 : (e > 0 ? 1 : 0)) : e;
     // tile plans also depend on the workgroup size (the LDS rows a tile may hold)
-    const bool pipe = pipe_pass(kind, k);
-    const i64 key = (((((i64)(pipe ? pipe_nw_ * 16 + pipe_wg_ : 0) * 8 + occ_) * 2 + (tile_kernel(kind) ? 1 : 0)) * 32 +
-                      (tile_kernel(kind) ? cfg_.tile_waves : 0)) * 4 + kind) * 100000 + (i64)ek * 100 + k;
+    const bool pipe = pipe_pass(kind, k), tile = tile_pass(kind, k);
+    const PipeGeo* pg = pipe ? pipe_geo(k) : nullptr;
+    const i64 key = (((((i64)(pipe ? pg->nw * 16 + pg->wg : 0) * 8 + occ_) * 2 + (tile ? 1 : 0)) * 32 +
+                      (tile ? cfg_.tile_waves : 0)) * 4 + kind) * 100000 + (i64)ek * 100 + k;
     auto it = plans_.find(key);
     if (it != plans_.end()) return it->second;
     std::vector<Region> rg = regions(kind, k, e);
     DevPlan p;
     i64 rows = cfg_.rows_per_wave;
-    if (tile_kernel(kind)) {
+    if (tile) {
         // step_tile: one workgroup per plan wave, one tile per CU per round; rows are capped by
         // the 160 KiB of LDS (2k halo rows + the tile, double-buffered or in place), extra rounds
         // beyond that.  The double-buffered tile is used when one round of tiles fits it (cheaper:
@@ -175,8 +177,8 @@ const DevPlan& HipEngine::plan(int kind, int k, i64 e) {
                                                                         xwrap_by_plan()));
         }
     } else if (pipe) {
-        // step_pipe: one workgroup per plan wave, pipe_wg_ of them per CU in one round
-        if (rows <= 0) rows = balanced_rows_per_chunk(rg, L_.nw, L_.h, k, (i64)pipe_wg_ * cus_, 1, xwrap_by_plan());
+        // step_pipe: one workgroup per plan wave, wg of them per CU in one round
+        if (rows <= 0) rows = balanced_rows_per_chunk(rg, L_.nw, L_.h, k, (i64)pg->wg * cus_, 1, xwrap_by_plan());
     } else {
         if (rows <= 0 && cfg_.waves_target > 0)
             rows = choose_rows_per_chunk(rg, k, cfg_.waves_target, 4 * (i64)k);
@@ -194,7 +196,7 @@ const DevPlan& HipEngine::plan(int kind, int k, i64 e) {
         }
     }
     std::vector<LaneDesc> lanes = build_plan(rg, L_.nw, L_.h, rows, k, xwrap_by_plan(), &p.st,
-                                             (tile_kernel(kind) || pipe) ? 1 : kWavesPerBlock, cfg_.plan_xcds, p.fold);
+                                             (tile || pipe) ? 1 : kWavesPerBlock, cfg_.plan_xcds, p.fold);
     const std::string bad = validate_plan(lanes, L_.nw, L_.h, L_.R, k, (step_flags() & hipk::STEP_WRAP_Y) != 0);
     if (!bad.empty()) throw Error(strprintf("refusing to launch an unsafe plan (kind %d, k %d, e %lld): %s", kind, k,
                                             (long long)e, bad.c_str()));

@@ -110,7 +110,24 @@ void HipEngine::dual_superstep(int k) {
     // through the RCCL self-exchange, the exchange and its ~10 us tail then sit on half 0's critical
     // path; docs/PERFORMANCE.md section 6.)
     const bool ov = sub_overlap_ == 1 && !self_y();
-    if (!self_y()) {
+    const bool xf = sub_overlap_ == 2 && !self_y();
+    if (xf) {
+        // The exchange first, on the compute stream (issued before any kernel, so its RCCL kernel is
+        // dispatched first); half 1's first pass, but for its band next to the south halo, meanwhile on
+        // the second stream; then half 0's whole first pass after the exchange, and half 1's band after
+        // the exchange's event, which its stream finds complete by then.
+        std::vector<Message> sends, recvs;
+        dual_messages(p, k, sends, recvs);
+        exchange_rows(sends, recvs, s_comp_);
+        stats_.exchanges += 1;
+        stats_.halo_bytes += (u64)(rows_bytes(0, k) + rows_bytes(1, k));
+        HIP_CHECK(hipEventRecord(ev_sub_x_, s_comp_));
+        wait_pending(s_comm_, ev_sub_a_);  // half 0's previous superstep (the seam rows half 1 reads)
+        launch_half(1, p, k, s_comm_, 0, 1);
+        launch_half(0, p, k, s_comp_, 0);
+        HIP_CHECK(hipStreamWaitEvent(s_comm_, ev_sub_x_, 0));
+        launch_half(1, p, k, s_comm_, 0, 2);
+    } else if (!self_y()) {
         hipStream_t xs = s_comp_;
         if (ov) {
             launch_half(0, p, k, s_comp_, 0, 1);
@@ -139,7 +156,7 @@ void HipEngine::dual_superstep(int k) {
     const int np = (int)pass_depths(k).size();
     for (int j = 0; j < np; ++j)
         for (int s = 0; s < 2; ++s) {  // half 0's pass first (half 1 first measured no better: docs/PERFORMANCE.md §6)
-            if (ov && s == 0 && j == 0) continue;
+            if (j == 0 && (xf || (ov && s == 0))) continue;
             if (j == 0 && s == 0) trace::mark("gol.launch0");  // (GOL_ROCTX: host side of the launch latency)
             launch_half(s, p, k, s ? s_comm_ : s_comp_, j);
             if (j == 0 && s == 0) trace::mark("gol.launch0_done");

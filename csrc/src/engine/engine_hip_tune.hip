@@ -41,25 +41,53 @@ void HipEngine::spin_up() {
 // slower per pass than depth 8; profiles/kb_depth_sweep.txt).  Rank-local: the cut only changes
 // kernel passes, never the exchanges.
 void HipEngine::measure_pass_costs() {
-    pass_us_.clear();
-    if (cfg_.compat || cfg_.kernel_depth > 0 || kernel_ == "lds" || res_ || (!dual_ && tile_kernel(0)) ||
-        (!dual_ && !split_ && kern_[0] == "pipe"))
-        return;
+    std::map<int, double>& costs = pass_us_[dual_ ? 1 : 0];
+    costs.clear();
+    if (!dual_) pipe_geo_.clear();
+    if (cfg_.compat || cfg_.kernel_depth > 0 || kernel_ == "lds" || res_ || (!dual_ && tile_kernel(0))) return;
     // every instantiated depth up to the pass depth, and the deeper ones a superstep could use: a
     // 20-generation superstep cut 12 + 8 measured cheaper than 8 + 8 + 4 (the K=12 pass runs 2 waves
     // per SIMD at ~10.6 us/gen as two halves, vs 10.3 at K=8; profiles/pingpong_loop_ab.txt)
     const int K = dual_ ? tdepth_ : kdepth_;
     const int kmax = std::min(superstep_depth(), hipk::max_step_depth());
-    std::vector<int> ds;
+    struct Cand {
+        int d;
+        PipeGeo g;  // g.nw > 0: a step_pipe pass of this geometry
+    };
+    std::vector<Cand> cs;
     for (int d = 1; d <= std::max(K, kmax); ++d)
-        if (hipk::step_depth_supported(d)) ds.push_back(d);
-    if (ds.size() < 2) return;
-    for (int d : ds) {  // every plan first: plan building idles the GPU and drops its clock
+        if (hipk::step_depth_supported(d)) cs.push_back({d, {}});
+    // A one tile whose tuned kernel is step_pipe: its passes may be step_pipe at any depth one of these
+    // geometries reaches (and the superstep allows), so a superstep is cut into the cheapest mix, e.g.
+    // the driver's 20-generation run on config 3's 4096 x 32768 strip as ONE step_pipe pass of 20
+    // (10 stages x 2) instead of three step_temporal passes of 7 + 7 + 6.
+    if (!dual_ && kern_[0] == "pipe" && pipe_k_ > 0) {
+        std::vector<PipeGeo> gs = {pipe_cur_};
+        for (int l : {2, 3})
+            for (int nw : {5, 7, 9, 11, 13, 16})
+                if (!(l == 3 && (nw == 11 || nw == 16))) gs.push_back({nw, l, 1});
+        for (const PipeGeo& g : gs) {
+            const int d = (g.nw - 1) * g.l;
+            if (d > superstep_depth() || !hipk::pipe_supported(g.nw, g.l)) continue;
+            bool dup = false;
+            for (const Cand& c : cs) dup = dup || (c.g.nw == g.nw && c.g.l == g.l && c.g.wg == g.wg);
+            if (!dup) cs.push_back({d, g});
+        }
+    }
+    if (cs.size() < 2) return;
+    // pipe_geo_ lists exactly the depths that run step_pipe (the -1 entry marks it as authoritative)
+    auto select = [&](const Cand& c) {
+        pipe_geo_.clear();
+        pipe_geo_[-1] = PipeGeo{};
+        if (c.g.nw > 0) pipe_geo_[c.d] = c.g;
+    };
+    for (const Cand& c : cs) {  // every plan first: plan building idles the GPU and drops its clock
         if (dual_) {
-            sub_plan(0, d, 0);
-            sub_plan(1, d, 0);
+            sub_plan(0, c.d, 0);
+            sub_plan(1, c.d, 0);
         } else {
-            plan(0, d, 0);
+            select(c);
+            plan(0, c.d, 0);
         }
     }
     hipEvent_t e0, e1;
@@ -67,13 +95,14 @@ void HipEngine::measure_pass_costs() {
     HIP_CHECK(hipEventCreate(&e1));
     spin_up();
     const int reps = 4;
-    std::map<int, double> best;
+    std::vector<double> best(cs.size(), 1e30);
     for (int round = 0; round < 3; ++round)
-        for (int d : ds) {
+        for (size_t i = 0; i < cs.size(); ++i) {
+            const int d = cs[i].d;
             HIP_CHECK(hipEventRecord(e0, s_comp_));
             if (dual_) {
                 HIP_CHECK(hipStreamWaitEvent(s_comm_, e0, 0));
-                for (int i = 0; i < reps; ++i)
+                for (int r = 0; r < reps; ++r)
                     for (int sub = 0; sub < 2; ++sub) {
                         const DevPlan& pl = sub_plan(sub, d, 0);
                         const Layout& Ls = sub_L_[sub];
@@ -85,20 +114,35 @@ void HipEngine::measure_pass_costs() {
                 HIP_CHECK(hipEventRecord(ev_sub_b_, s_comm_));
                 HIP_CHECK(hipStreamWaitEvent(s_comp_, ev_sub_b_, 0));
             } else {
-                for (int i = 0; i < reps; ++i) launch(0, d, 0, buf_[cur_], buf_[cur_ ^ 1], s_comp_);
+                select(cs[i]);
+                for (int r = 0; r < reps; ++r) launch(0, d, 0, buf_[cur_], buf_[cur_ ^ 1], s_comp_);
             }
             HIP_CHECK(hipEventRecord(e1, s_comp_));
             HIP_CHECK(hipEventSynchronize(e1));
             float ms = 0;
             HIP_CHECK(hipEventElapsedTime(&ms, e0, e1));
-            const double us = ms * 1e3 / reps;
-            best[d] = round == 0 ? us : std::min(best[d], us);
-            init_step("init: pass costs", "pass", d, (float)(us / d));
+            best[i] = std::min(best[i], ms * 1e3 / reps);
+            init_step("init: pass costs", cs[i].g.nw ? "pipe pass" : "pass", d, (float)(best[i] / d));
         }
     HIP_CHECK(hipEventDestroy(e0));
     HIP_CHECK(hipEventDestroy(e1));
     HIP_CHECK(hipGetLastError());
-    pass_us_ = best;
+    if (!dual_ && kern_[0] == "pipe" && pipe_k_ > 0 && hipk::pipe_fault())
+        throw Error("step_pipe: a ring wait timed out while measuring pass costs; the board is invalid");
+    std::map<int, PipeGeo> geo = {{-1, PipeGeo{}}};
+    for (size_t i = 0; i < cs.size(); ++i) {
+        auto it = costs.find(cs[i].d);
+        if (it != costs.end() && it->second <= best[i]) continue;
+        costs[cs[i].d] = best[i];
+        if (cs[i].g.nw > 0)
+            geo[cs[i].d] = cs[i].g;
+        else
+            geo.erase(cs[i].d);
+    }
+    if (!dual_) {
+        pipe_geo_.clear();
+        if (kern_[0] == "pipe") pipe_geo_ = geo;  // (otherwise no step_pipe passes: the tuned default)
+    }
     passes_.clear();
 }
 
@@ -126,7 +170,7 @@ void HipEngine::choose_schedule() {
         // the overlapped variant needs the exchange (neighbours, or the self-exchange)
         std::vector<std::string> dc;
         if (cfg_.subtile_overlap <= 0 || self_y()) dc.push_back("subtiles");
-        if (cfg_.subtile_overlap != 0 && !self_y()) dc.push_back("subtiles+ov");
+        if (cfg_.subtile_overlap != 0 && !self_y()) dc.push_back(cfg_.subtile_overlap == 2 ? "subtiles+xf" : "subtiles+ov");
         if (cfg_.subtiles == 2) cands.clear();
         cands.insert(cands.end(), dc.begin(), dc.end());
     }
@@ -151,13 +195,7 @@ void HipEngine::choose_schedule() {
         for (int round = 0; round < rounds; ++round)
             for (size_t c = 0; c < cands.size(); ++c) {
                 if (round == 0) time_schedule(cands[c], k, reps);  // warm-up: connections, plans, graphs
-                synchronize();
-                t_->barrier();
-                const auto t0 = std::chrono::steady_clock::now();
-                time_schedule(cands[c], k, reps);
-                synchronize();
-                const double dt = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
-                const double us = t_->allreduce_max(dt) * 1e6 / (reps * k);
+                const double us = sample_schedule(cands[c], k, reps);
                 samples[c].push_back(us);
                 best[c] = std::min(best[c], us);
                 if (short_run) {
@@ -192,7 +230,7 @@ void HipEngine::choose_schedule() {
     sched_pick_ = pick;
     split_ = pick == "split";
     dual_ = pick.rfind("subtiles", 0) == 0;
-    sub_overlap_ = pick == "subtiles+ov" ? 1 : 0;
+    sub_overlap_ = pick == "subtiles+ov" ? 1 : (pick == "subtiles+xf" ? 2 : 0);
     graph_rccl_on_ = cfg_.graph_rccl == 1 || pick == "full+graph";
     if (dual_) {
         setup_dual();
@@ -203,15 +241,63 @@ void HipEngine::choose_schedule() {
     passes_.clear();
 }
 
+// One timed sample of `reps` supersteps of k generations of schedule `c`, bracketed as bench.py
+// brackets its timed run: the engine's streams synchronised, the ranks aligned by device_barrier (host
+// barrier, then the transport's device barrier completed on the GPU), the supersteps, then a device-wide
+// synchronisation (bench.py: torch.cuda.synchronize()).  us per generation, the max over the ranks.
+double HipEngine::sample_schedule(const std::string& c, int k, int reps) {
+    device_barrier();
+    const auto t0 = std::chrono::steady_clock::now();
+    time_schedule(c, k, reps);
+    end_sync();
+    const double dt = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    return t_->allreduce_max(dt) * 1e6 / ((double)reps * k);
+}
+
+// The chosen schedule timed at the end of init the way the hinted runs execute (same superstep depth,
+// graphs or eager launches, pass cuts and kernels, after a device barrier, from an idle GPU): the
+// median of a few samples, reported as stats.predicted_us_per_gen next to what a run then measures.
+// Collective (every rank runs the same samples).  Long samples (big boards) are cut short.
+void HipEngine::predict_run() {
+    if (cfg_.run_hint == 0 || cfg_.compat || sched_pick_.empty()) return;
+    const int k = supported_depth((int)std::min<u64>(cfg_.run_hint, (u64)superstep_depth()));
+    const int reps = (int)std::min<u64>(kSchedReps, std::max<u64>(1, cfg_.run_hint / (u64)k));
+    const EngineStats saved = stats_;
+    std::vector<double> v;
+    const int rounds = reps == 1 ? 9 : 5;
+    if (res_) {
+        for (int r = 0; r < rounds; ++r) v.push_back((double)time_resident(res_kin_, k) * 1e3);
+    } else {
+        sync_canonical();
+        time_schedule(sched_pick_, k, reps);  // warm-up (and the candidate's timing graph)
+        const auto t0 = std::chrono::steady_clock::now();
+        for (int r = 0; r < rounds; ++r) {
+            v.push_back(sample_schedule(sched_pick_, k, reps));
+            if (t_->allreduce_max(std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count()) > 1.0)
+                break;  // (agreed: every rank stops after the same sample)
+        }
+        synchronize();
+        destroy_sched_graphs();
+        if (dual_) sub_current_ = false;  // the halves hold timing scratch: load the board at the next run
+    }
+    std::sort(v.begin(), v.end());
+    stats_ = saved;  // the samples' exchanges and replays are not part of any run
+    stats_.predicted_us_per_gen = v[(v.size() - 1) / 2];
+    stats_.predicted_gens = k * reps;
+    init_step("init: prediction", sched_pick_.c_str(), k, (float)stats_.predicted_us_per_gen);
+}
+
 // `reps` supersteps of k generations of schedule `c` on scratch state (see choose_schedule).
 void HipEngine::time_schedule(const std::string& c, int k, int reps, bool eager) {
     if (c.rfind("subtiles", 0) == 0) {
         setup_dual();
+        const bool d0 = dual_;
+        const int o0 = sub_overlap_;
         dual_ = true;
-        sub_overlap_ = c == "subtiles+ov" ? 1 : 0;
+        sub_overlap_ = c == "subtiles+ov" ? 1 : (c == "subtiles+xf" ? 2 : 0);
         for (int i = 0; i < reps; ++i) dual_superstep(k);
-        dual_ = false;
-        sub_overlap_ = 0;
+        dual_ = d0;
+        sub_overlap_ = o0;
         return;
     }
     // One-tile supersteps as the runs replay them (graphs: "local" always, the "full+graph"
@@ -230,7 +316,7 @@ void HipEngine::time_schedule(const std::string& c, int k, int reps, bool eager)
         if (!sg.exec && !sched_graph_failed_.count(c)) {
             prepare(k);
             time_schedule(base, k, 1, true);
-            HIP_CHECK(hipStreamSynchronize(s_comp_));
+            synchronize();  // (also joins the streams: no event query inside the capture)
             hipGraph_t graph = nullptr;
             try {
                 HIP_CHECK(hipStreamBeginCapture(s_comp_, hipStreamCaptureModeRelaxed));
@@ -256,12 +342,14 @@ void HipEngine::time_schedule(const std::string& c, int k, int reps, bool eager)
             time_schedule(base, k, reps, true);  // the same exchanges as the peers' replays
         return;
     }
+    const bool split0 = split_;
     split_ = c == "split";
     const std::vector<int>& ps = pass_depths(k);
     for (int i = 0; i < reps; ++i) {
         first_pass(k, ps[0], ext_after(ps, 0), split_);
         for (size_t j = 1; j < ps.size(); ++j) {
             const i64 e = ext_after(ps, j);
+            join_halo();
             launch(0, ps[j], e, buf_[cur_], buf_[cur_ ^ 1], s_comp_);
             post(buf_[cur_ ^ 1], s_comp_, e);
         }
@@ -270,7 +358,7 @@ void HipEngine::time_schedule(const std::string& c, int k, int reps, bool eager)
         // later passes, which a real run cannot: 2.78 timed vs 3.26 us/gen run, 4096 x 32768)
         if (ps.size() > 1) mark_ready();
     }
-    split_ = false;
+    split_ = split0;
 }
 
 // GOL_KERNEL=auto: for every plan kind a run uses (full tile; interior + boundary bands when
@@ -309,11 +397,11 @@ void HipEngine::autotune_kernel() {
         init_step("init: kernel autotune", kern, k, per_gen);
         if (pipe && hipk::pipe_fault()) {  // a ring wait timed out: never pick this geometry
             fprintf(stderr, "[gol] step_pipe %dx%d: a ring wait timed out in the kernel autotune; candidate dropped\n",
-                    pipe_nw_ - 1, pipe_l_);
+                    pipe_cur_.nw - 1, pipe_cur_.l);
             per_gen = 1e30f;
         }
         const std::string key = tile   ? strprintf("%d:%s@%dx%dw", kind, kern, k, cfg_.tile_waves)
-                                : pipe ? strprintf("%d:pipe@%d(%dx%d,%d/CU)", kind, k, pipe_nw_ - 1, pipe_l_, pipe_wg_)
+                                : pipe ? strprintf("%d:pipe@%d(%dx%d,%d/CU)", kind, k, pipe_cur_.nw - 1, pipe_cur_.l, pipe_cur_.wg)
                                 : occ_ ? strprintf("%d:%s@%d/%dw", kind, kern, k, occ_)
                                        : strprintf("%d:%s@%d", kind, kern, k);
         auto it = tune_ms_.find(key);
@@ -427,13 +515,22 @@ void HipEngine::autotune_kernel() {
     passes_.clear();
     // interior / boundary plans of split supersteps, at the chosen pass depth
     if (split_used()) {
+        // (the interior and the bands may run step_pipe when the full tile does: the bands' passes at
+        // the depths of step_pipe passes are latency-bound, 10 stages x 2 generations streaming a 60-row
+        // segment, where the tile kernel runs 20 generations of barriers: 38 us for a 20-row band of
+        // config 3's strip, profiles/strip_split_round5.txt)
+        auto kcands = [&](int kind) {
+            std::vector<const char*> v = {"temporal", "tile"};
+            if (kern_[0] == "pipe") v.push_back("pipe");
+            return v;
+        };
         for (int kind : {1, 2})
-            for (const char* c : {"temporal", "tile"}) time_pass(kind, c, kdepth_, true);
+            for (const char* c : kcands(kind)) time_pass(kind, c, kdepth_, true);
         spin_up();
         for (int kind : {1, 2}) {
             float bk = 1e30f;
             const char* pk = "temporal";
-            for (const char* c : {"temporal", "tile"}) {
+            for (const char* c : kcands(kind)) {
                 const float t = time_pass(kind, c, kdepth_);
                 if (t < bk) {
                     bk = t;
@@ -537,7 +634,7 @@ std::map<std::string, double> HipEngine::phase_probe(int k) {
     // the schedule the runs use, as choose_schedule timed it (graph variants included)
     std::string sched = sched_pick_;
     if (sched.empty())
-        sched = dual_ ? (sub_overlap_ ? "subtiles+ov" : "subtiles")
+        sched = dual_ ? (sub_overlap_ == 2 ? "subtiles+xf" : (sub_overlap_ ? "subtiles+ov" : "subtiles"))
                       : (split_ ? "split" : (halo_items(L_.R).empty() ? "local" : "full"));
     const int reps = 2;
     double best = 1e30;

@@ -70,7 +70,20 @@ class HipEngine : public Engine {
         // split schedule): skip them — an event record between two kernels costs ~15 us on the
         // GPU (a release fence), measured between eager supersteps on one MI355X.
         if (!events_needed_) return;
+        events_synced_ = false;
         HIP_CHECK(hipEventRecord(ev_ready_, s_comp_));
+    }
+    // The exchange (and, for one-pass split supersteps, the bands) done on the comm stream.
+    void record_halo() {
+        events_synced_ = false;
+        HIP_CHECK(hipEventRecord(ev_halo_, s_comm_));
+    }
+    // A split superstep of one pass left its bands on the comm stream unjoined: the compute stream waits
+    // for them before it touches the board again (skipped once both streams were synchronised).
+    void join_halo() {
+        if (!halo_pending_) return;
+        halo_pending_ = false;
+        wait_pending(s_comp_, ev_halo_);
     }
 
     ~HipEngine() override;
@@ -84,6 +97,7 @@ class HipEngine : public Engine {
         HIP_CHECK(hipStreamSynchronize(s_comm_));
         HIP_CHECK(hipStreamSynchronize(s_comp_));
         events_synced_ = true;
+        halo_pending_ = false;
     }
 
     bool gpu_idle() override {
@@ -184,7 +198,7 @@ class HipEngine : public Engine {
         for (size_t j = 0; j < ps.size(); ++j)
             for (int s = 0; s < 2; ++s) sub_plan(s, ps[j], ext_after(ps, j));
         if (sub_overlap_ && !self_y())
-            for (int part : {1, 2}) sub_plan(0, ps[0], ext_after(ps, 0), part);
+            for (int part : {1, 2}) sub_plan(sub_overlap_ == 2 ? 1 : 0, ps[0], ext_after(ps, 0), part);
     }
 
     // part: 0 the whole pass; a first pass split around the exchange (sub_overlap_): 1 all output
@@ -203,6 +217,7 @@ class HipEngine : public Engine {
 
     // Both halves done -> the canonical buffer (before anything reads it).
     void sync_canonical() {
+        join_halo();
         if (!canon_stale_) return;
         HIP_CHECK(hipStreamWaitEvent(s_comp_, ev_sub_b_, 0));  // the second half's last superstep
         for (int s = 0; s < 2; ++s)
@@ -315,6 +330,18 @@ class HipEngine : public Engine {
 
     // (eager: the one-tile candidates without their graph replay; used to capture those graphs)
     void time_schedule(const std::string& c, int k, int reps, bool eager = false);
+    double sample_schedule(const std::string& c, int k, int reps);
+    void predict_run();
+    // The end of a timed sample: bench.py's device-wide synchronisation when this process's engines do not
+    // share the device (one rank, or RCCL: one rank per GPU), else the engine's own streams (thread ranks
+    // on one GPU: a device-wide wait could wait for a peer's exchange this thread has yet to issue).
+    void end_sync() {
+        if (t_->size() > 1 && t_->name().rfind("rccl", 0) != 0) return synchronize();
+        Armed armed(wd_.get());
+        HIP_CHECK(hipDeviceSynchronize());
+        events_synced_ = true;
+        halo_pending_ = false;
+    }
 
     void do_set_compat_halos(const std::vector<u64>& above, const std::vector<u64>& below) override;
 
@@ -359,16 +386,37 @@ class HipEngine : public Engine {
         return hipk::tile_max_rows(k, cfg_.tile_waves, step_flags() | tile_bits(tile_inplace_ != 0));
     }
 
+    // The tuned kernel of plan kind `kind` is the LDS tile kernel (every depth of that kind runs it).
     bool tile_kernel(int kind) const { return kern_[kind] == "tile"; }
-    // A pass of the level-pipelined workgroup kernel (step_pipe): its one depth (pipe_k_); the other
-    // passes of a superstep (remainders) of a "pipe" kind run step_temporal.
-    bool pipe_pass(int kind, int k) const { return kern_[kind] == "pipe" && pipe_k_ > 0 && k == pipe_k_; }
-    // Set the step_pipe geometry: nw waves per workgroup (one loader + nw - 1 stages of l generations),
-    // wg workgroups per CU in its plans.
+    // step_pipe geometry: nw waves per workgroup (one loader + nw - 1 stages of l generations), wg
+    // workgroups per CU in its plans; depth (nw - 1) l.
+    struct PipeGeo {
+        int nw = 0, l = 0, wg = 0;
+    };
+    // The step_pipe geometry of a pass of depth k: after measure_pass_costs, the measured cheapest one
+    // where step_pipe beat step_temporal at that depth (pipe_geo_); before, the tuned geometry at its own
+    // depth only.  nullptr: no step_pipe pass of that depth.
+    const PipeGeo* pipe_geo(int k) const {
+        if (!pipe_geo_.empty()) {
+            auto it = pipe_geo_.find(k);
+            return it == pipe_geo_.end() ? nullptr : &it->second;
+        }
+        return pipe_k_ > 0 && k == pipe_k_ ? &pipe_cur_ : nullptr;
+    }
+    // The kernel of a pass of plan kind `kind` at depth k: the LDS tile kernel when tuned so; step_pipe when
+    // that kind's tuned kernel is step_pipe (the interior of a split first pass too, when the full tile's
+    // is) and a geometry of depth k exists; else step_temporal where it is instantiated, else the tile
+    // kernel (any depth: the bands of a first pass at a step_pipe depth).
+    enum PassKernel { PK_TEMPORAL, PK_TILE, PK_PIPE };
+    PassKernel pass_kernel(int kind, int k) const {
+        if (kern_[kind] == "tile") return PK_TILE;
+        if ((kern_[kind] == "pipe" || (kind == 1 && kern_[0] == "pipe")) && pipe_geo(k)) return PK_PIPE;
+        return hipk::step_depth_supported(k) ? PK_TEMPORAL : PK_TILE;
+    }
+    bool tile_pass(int kind, int k) const { return pass_kernel(kind, k) == PK_TILE; }
+    bool pipe_pass(int kind, int k) const { return pass_kernel(kind, k) == PK_PIPE; }
     void set_pipe(int nw, int l, int wg) {
-        pipe_nw_ = nw;
-        pipe_l_ = l;
-        pipe_wg_ = wg;
+        pipe_cur_ = {nw, l, wg};
         pipe_k_ = (nw - 1) * l;
     }
 
@@ -523,15 +571,19 @@ class HipEngine : public Engine {
 
     int tile_inplace_ = (int)env_int("GOL_TILE_INPLACE", -1);
     int tile_fold_ = (int)env_int("GOL_TILE_FOLD", -1);
-    int pipe_nw_ = 0, pipe_l_ = 0, pipe_wg_ = 0, pipe_k_ = 0;  // step_pipe geometry (set_pipe)
+    PipeGeo pipe_cur_;  // the tuned step_pipe geometry (set_pipe); depth pipe_k_
+    int pipe_k_ = 0;
+    std::map<int, PipeGeo> pipe_geo_;  // measure_pass_costs: depth -> step_pipe geometry, where it wins
     bool pipe_used_ = false;                                    // some pass ran step_pipe (fault check)
     int tile_lv_ = (int)env_int("GOL_TILE_LEVELS", 0);  // tile kernel: generations per LDS pass (1, 2, 4; 0 auto)
     bool multipass_ = false;
     std::map<int, std::vector<int>> passes_;
     bool split_ = false;   // superstep schedule: interior/boundary split with overlapped exchange
-    bool bands_comm_ = env_int("GOL_SPLIT_BANDS_COMM", 0) != 0;  // split: bands on the comm stream after the exchange
+    bool halo_pending_ = false;  // split: the last superstep's bands on the comm stream are not joined (join_halo)
     std::map<std::string, double> sched_us_;  // choose_schedule: us per generation per candidate
-    std::map<int, double> pass_us_;           // measure_pass_costs: us per pass by depth (chosen mode)
+    // measure_pass_costs: us per pass by depth, [0] one tile (kind-0 passes), [1] the two sub-tiles
+    std::map<int, double> pass_us_[2];
+    const std::map<int, double>& pass_costs() const { return pass_us_[dual_ ? 1 : 0]; }
     bool tuned_ = false;
     std::map<std::string, float> tune_ms_;
     Marker mk_[kMarkers];
@@ -577,7 +629,8 @@ class HipEngine : public Engine {
     bool dual_ = false;
     // Exchange overlap of the sub-tile superstep (timed candidates): 0 none ("subtiles"); 1 half 0's
     // first pass, but for its band next to the north halo, runs while the exchange is in flight
-    // ("subtiles+ov")
+    // ("subtiles+ov"); 2 the exchange first on the compute stream, half 1's first pass but for its
+    // south band meanwhile ("subtiles+xf", GOL_SUBTILE_OVERLAP=2)
     int sub_overlap_ = 0;
     Layout sub_L_[2];
     i64 sub_r0_[2] = {0, 0};

@@ -427,6 +427,7 @@ void write_metrics(const Options& o, Engine& eng, const CliArgs& a, double durat
     f << "  \"schedule\": \"" << s.schedule << "\",\n";
     f << "  \"autotune\": \"" << s.tuning << "\",\n";
     f << "  \"plan_waves\": " << s.plan_waves << ",\n  \"lane_efficiency\": " << s.lane_efficiency << ",\n";
+    f << "  \"predicted_us_per_gen\": " << s.predicted_us_per_gen << ",\n";
     f << "  \"t_exchange_ms\": " << s.t_exchange_ms << ",\n  \"t_compute_ms\": " << s.t_compute_ms << "\n";
     f << "}\n";
 }

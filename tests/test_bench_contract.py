@@ -40,6 +40,19 @@ def _run(cmd, env_extra=None):
 def test_bench_single_process():
     out = _run([sys.executable, "bench.py", "--steps", "20", "--warmup", "2"])
     assert out["config"]["parallelism"].endswith("p1 (1x1)")
+    # the init-time prediction next to the measurement (HIP engines measure one; the CPU backend does not)
+    assert "sched_predicted_us_per_gen" in out and "predicted_over_measured" in out
+    assert out["sched_predicted_us_per_gen"] is None and out["predicted_over_measured"] is None
+
+
+def test_bench_prediction_fields():
+    sys.path.insert(0, REPO)
+    import bench
+
+    f = bench.prediction_fields(11.0, 11.2)
+    assert f == {"sched_predicted_us_per_gen": 11.0, "predicted_over_measured": round(11.0 / 11.2, 4)}
+    assert bench.prediction_fields(0.0, 11.2) == {"sched_predicted_us_per_gen": None, "predicted_over_measured": None}
+    assert bench.prediction_fields(None, 11.2)["sched_predicted_us_per_gen"] is None
 
 
 def test_bench_torchrun_two_ranks():
