@@ -182,6 +182,7 @@ HipEngine::~HipEngine() {
     wd_.reset();  // its thread calls probe(), which reads the members destroyed below
     hipStreamSynchronize(s_comp_);
     hipStreamSynchronize(s_comm_);
+    destroy_xgraphs();  // (they captured the communicator)
     for (auto& kv : sub_plans_) hipFree(kv.second.d);
     for (auto& sb : sub_buf_)
         for (u64* b : sb)
@@ -374,10 +375,12 @@ void HipEngine::do_init(const PatternSpec& p) {
     // remainder of the hinted run length), so neither graph capture nor a hinted timed loop
     // builds or uploads a plan.  Other remainders are built on first use.
     for (int k : init_depths()) {
-        if (dual_)
+        if (dual_) {
             prepare_dual(k);
-        else
+            capture_xgraphs(k);
+        } else {
             prepare(k);
+        }
     }
     prewarm_graph();
     if (dual_) {

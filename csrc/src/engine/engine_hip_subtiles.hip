@@ -32,6 +32,7 @@ void HipEngine::setup_dual() {
 // Free the sub-tile buffers, plans and copy lists (the measurement chose one tile).
 void HipEngine::teardown_dual() {
     synchronize();
+    destroy_xgraphs();
     for (auto& kv : sub_plans_) hipFree(kv.second.d);
     sub_plans_.clear();
     for (auto& sb : sub_buf_)
@@ -116,9 +117,7 @@ void HipEngine::dual_superstep(int k) {
         // dispatched first); half 1's first pass, but for its band next to the south halo, meanwhile on
         // the second stream; then half 0's whole first pass after the exchange, and half 1's band after
         // the exchange's event, which its stream finds complete by then.
-        std::vector<Message> sends, recvs;
-        dual_messages(p, k, sends, recvs);
-        exchange_rows(sends, recvs, s_comp_);
+        dual_exchange(p, k, s_comp_);
         stats_.exchanges += 1;
         stats_.halo_bytes += (u64)(rows_bytes(0, k) + rows_bytes(1, k));
         HIP_CHECK(hipEventRecord(ev_sub_x_, s_comp_));
@@ -134,9 +133,7 @@ void HipEngine::dual_superstep(int k) {
             wait_pending(s_comm_, ev_sub_a_);  // the exchange sends half 0's edge and writes its halo
             xs = s_comm_;
         }
-        std::vector<Message> sends, recvs;
-        dual_messages(p, k, sends, recvs);
-        exchange_rows(sends, recvs, xs);
+        dual_exchange(p, k, xs);
         stats_.exchanges += 1;
         stats_.halo_bytes += (u64)(rows_bytes(0, k) + rows_bytes(1, k));
         // (full: also implies half 0's previous superstep, which ran on the same stream)
@@ -188,6 +185,57 @@ void HipEngine::dual_messages(int p, int k, std::vector<Message>& sends, std::ve
     recvs.push_back({g_.nbr[DIR_S], sub_rows(1, p, h1), rows_bytes(1, k)});
     sends.push_back({g_.nbr[DIR_S], sub_rows(1, p, h1 - k), rows_bytes(1, k)});
     recvs.push_back({g_.nbr[DIR_N], sub_rows(0, p, -k), rows_bytes(0, k)});
+}
+
+// The rank's exchange into / out of the halves' buffer p, on stream xs: replayed from a graph captured at
+// init when GOL_SUBTILE_XGRAPH=1 (an eager RCCL group leaves a ~10 us gap before the next kernel on its
+// queue, a captured one none: kernel traces of the 32768^2 and strip cuts, profiles/strip_split_round5.txt).
+void HipEngine::dual_exchange(int p, int k, hipStream_t xs) {
+    auto it = xgraphs_.find(p * 1000 + k);
+    if (it != xgraphs_.end()) {
+        HIP_CHECK(hipGraphLaunch(it->second, xs));
+        return;
+    }
+    std::vector<Message> sends, recvs;
+    dual_messages(p, k, sends, recvs);
+    exchange_rows(sends, recvs, xs);
+}
+
+void HipEngine::capture_xgraphs(int k) {
+    if (!xgraph_wanted_ || !device_transport_ || !t_->graph_capturable() || self_y()) return;
+    for (int p = 0; p < 3; ++p) {
+        const int key = p * 1000 + k;
+        if (xgraphs_.count(key)) continue;
+        hipGraph_t graph = nullptr;
+        hipGraphExec_t exec = nullptr;
+        try {
+            HIP_CHECK(hipStreamBeginCapture(s_comm_, hipStreamCaptureModeRelaxed));
+            std::vector<Message> sends, recvs;
+            dual_messages(p, k, sends, recvs);
+            t_->exchange(sends, recvs, (void*)s_comm_);
+            HIP_CHECK(hipStreamEndCapture(s_comm_, &graph));
+            HIP_CHECK(hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0));
+            HIP_CHECK(hipGraphDestroy(graph));
+            HIP_CHECK(hipGraphUpload(exec, s_comm_));
+        } catch (const Error& e) {
+            hipGraph_t g2 = nullptr;
+            hipStreamEndCapture(s_comm_, &g2);
+            if (g2) hipGraphDestroy(g2);
+            hipGetLastError();
+            xgraph_wanted_ = false;
+            fprintf(stderr, "[gol] sub-tile exchange graph capture disabled: %s\n", e.what());
+            return;
+        }
+        xgraphs_[key] = exec;
+    }
+}
+
+void HipEngine::destroy_xgraphs() {
+    if (xgraphs_.empty()) return;
+    hipStreamSynchronize(s_comm_);
+    hipStreamSynchronize(s_comp_);
+    for (auto& kv : xgraphs_) hipGraphExecDestroy(kv.second);
+    xgraphs_.clear();
 }
 
 // Device transports (RCCL) are stream ordered on `s`.  Host transports are staged through pinned

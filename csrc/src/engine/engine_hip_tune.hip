@@ -249,6 +249,7 @@ double HipEngine::sample_schedule(const std::string& c, int k, int reps) {
     device_barrier();
     const auto t0 = std::chrono::steady_clock::now();
     time_schedule(c, k, reps);
+    if (wd_) note_progress();  // (a run publishes a progress marker per superstep or replay: an event record)
     end_sync();
     const double dt = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     return t_->allreduce_max(dt) * 1e6 / ((double)reps * k);
@@ -295,6 +296,7 @@ void HipEngine::time_schedule(const std::string& c, int k, int reps, bool eager)
         const int o0 = sub_overlap_;
         dual_ = true;
         sub_overlap_ = c == "subtiles+ov" ? 1 : (c == "subtiles+xf" ? 2 : 0);
+        capture_xgraphs(k);  // (GOL_SUBTILE_XGRAPH: once per depth, in the untimed warm-up call)
         for (int i = 0; i < reps; ++i) dual_superstep(k);
         dual_ = d0;
         sub_overlap_ = o0;

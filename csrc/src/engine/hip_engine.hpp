@@ -244,6 +244,11 @@ class HipEngine : public Engine {
     void dual_superstep(int k);
     void dual_messages(int p, int k, std::vector<Message>& sends, std::vector<Message>& recvs);
     void exchange_rows(const std::vector<Message>& sends, const std::vector<Message>& recvs, hipStream_t s);
+    void dual_exchange(int p, int k, hipStream_t xs);
+    void capture_xgraphs(int k);
+    void destroy_xgraphs();
+    bool xgraph_wanted_ = env_int("GOL_SUBTILE_XGRAPH", 0) != 0;
+    std::map<int, hipGraphExec_t> xgraphs_;  // (start buffer, depth) -> the rank's exchange, captured
 
     void launch_half(int s, int p, int k, hipStream_t st, int only = -1, int part = 0);
 
