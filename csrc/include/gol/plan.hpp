@@ -16,6 +16,7 @@
 #pragma once
 
 #include <string>
+#include <map>
 #include <vector>
 
 #include "gol/common.hpp"
@@ -103,6 +104,12 @@ i64 balanced_rows_per_chunk(const std::vector<Region>& regions, i64 nw, i64 h, i
 // 180: 46.7 vs 44.8-45.8).  round_rows <= 0 disables it (one round).
 i64 round_balanced_rows(const std::vector<Region>& regions, i64 nw, i64 h, int k, i64 resident_waves, i64 min_rows,
                         bool xwrap, i64 round_rows, i64 max_rounds = 32);
+
+// The cheapest cut of a k-generation superstep into kernel passes, given the measured cost (us) of one
+// pass at each available depth: dynamic programming over k (a pass streams the board through HBM once
+// whatever its depth, so the costs are far from linear in the depth).  Deepest pass first (12 + 8 measured
+// faster than 8 + 12).  Empty when no depth sums to k.
+std::vector<int> cheapest_cut(int k, const std::map<int, double>& pass_cost);
 
 // Neighbour tiles of a resident plan (hip_kernels.hpp step_resident: one plan wave = one tile, kept
 // by one workgroup for a whole run).  Tile t reads, for each of its lanes, rows [row0-k, row0+nrows+k)

@@ -307,6 +307,23 @@ std::string validate_plan(const std::vector<LaneDesc>& lanes, i64 nw, i64 h, int
     return "";
 }
 
+std::vector<int> cheapest_cut(int k, const std::map<int, double>& pass_cost) {
+    std::vector<double> best((size_t)std::max(k, 0) + 1, 1e300);
+    std::vector<int> pick((size_t)std::max(k, 0) + 1, 0);
+    best[0] = 0;
+    for (int x = 1; x <= k; ++x)
+        for (const auto& dc : pass_cost)
+            if (dc.first >= 1 && dc.first <= x && best[(size_t)(x - dc.first)] + dc.second < best[(size_t)x]) {
+                best[(size_t)x] = best[(size_t)(x - dc.first)] + dc.second;
+                pick[(size_t)x] = dc.first;
+            }
+    std::vector<int> ps;
+    if (k < 1 || pick[(size_t)k] == 0) return ps;
+    for (int x = k; x > 0; x -= pick[(size_t)x]) ps.push_back(pick[(size_t)x]);
+    std::sort(ps.begin(), ps.end(), std::greater<int>());
+    return ps;
+}
+
 std::string resident_neighbours(const std::vector<LaneDesc>& lanes, i64 nw, i64 h, int k, bool wrap_y,
                                 std::vector<u32>& off, std::vector<u32>& idx) {
     if (lanes.size() % kWaveLanes) return "lane count is not a multiple of 64";

@@ -466,13 +466,17 @@ void HipEngine::first_pass(int kx, int kp, i64 e, bool split) {
             // profiles/strip_split_round5.txt); with later passes the bands follow the interior on the
             // compute stream, whose wait then finds the exchange done.
             const bool bands_comm = e == 0 && !prof;
+            // (a step_pipe interior leaves every CU the registers and LDS RCCL's kernel needs, so it may
+            // be issued first without holding the exchange back; measurement knob GOL_SPLIT_ORDER)
+            const bool int_first = bands_comm && split_int_first_ && pass_kernel(1, kp) == PK_PIPE;
+            if (int_first) launch(1, kp, 0, src, dst, s_comp_);
             wait_pending(s_comm_, ev_ready_);
             if (prof) HIP_CHECK(hipEventRecord(ev_t0_, s_comm_));
             exchange_device(kx, items, cur_, s_comm_);
             if (prof) HIP_CHECK(hipEventRecord(ev_t1_, s_comm_));
             if (!bands_comm) record_halo();
             if (prof) HIP_CHECK(hipEventRecord(ev_t2_, s_comp_));
-            launch(1, kp, 0, src, dst, s_comp_);
+            if (!int_first) launch(1, kp, 0, src, dst, s_comp_);
             if (bands_comm) {
                 launch(2, kp, e, src, dst, s_comm_);
                 post(dst, s_comm_, e);

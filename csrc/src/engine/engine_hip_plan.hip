@@ -22,20 +22,10 @@ const std::vector<int>& HipEngine::pass_depths(int k) {
     const int K = std::max(1, dual_ ? tdepth_ : kdepth_);
     std::vector<int> ps;
     if (!pass_costs().empty() && !any_depth) {
-        // cheapest cut by the measured per-depth pass times (dynamic programming over k; the depths
-        // include step_pipe geometries when that is the tuned kernel: measure_pass_costs)
-        std::vector<double> best((size_t)k + 1, 1e300);
-        std::vector<int> pick((size_t)k + 1, 0);
-        best[0] = 0;
-        for (int x = 1; x <= k; ++x)
-            for (const auto& dc : pass_costs())
-                if (dc.first <= x && best[(size_t)(x - dc.first)] + dc.second < best[(size_t)x]) {
-                    best[(size_t)x] = best[(size_t)(x - dc.first)] + dc.second;
-                    pick[(size_t)x] = dc.first;
-                }
-        for (int x = k; x > 0; x -= pick[(size_t)x]) ps.push_back(pick[(size_t)x]);
-        std::sort(ps.begin(), ps.end(), std::greater<int>());  // deepest first (8 + 12 measured slower than 12 + 8)
-        return passes_.emplace(key, ps).first->second;
+        // cheapest cut by the measured per-depth pass times (the depths include step_pipe geometries when
+        // that is the tuned kernel: measure_pass_costs)
+        ps = cheapest_cut(k, pass_costs());
+        if (!ps.empty()) return passes_.emplace(key, ps).first->second;
     }
     if (!dual_ && kern_[0] == "pipe" && pipe_k_ > 0 && !split_) {
         // (before the pass costs are measured) whole step_pipe passes; the remainder in step_temporal

@@ -623,7 +623,31 @@ static void test_plan_age_weights() {
     }
 }
 
+// cheapest_cut: the pass cut of a superstep from measured per-depth pass costs (plan.hpp).
+static void test_cheapest_cut() {
+    // one tile, 32768^2-like costs: shallow passes cost nearly as much as deep ones
+    std::map<int, double> c = {{4, 74}, {6, 78}, {7, 80}, {8, 83}, {12, 122}};
+    CHECK((cheapest_cut(20, c) == std::vector<int>{12, 8}));
+    CHECK((cheapest_cut(16, c) == std::vector<int>{8, 8}));
+    CHECK((cheapest_cut(8, c) == std::vector<int>{8}));
+    // a step_pipe depth of 20 cheaper than any mix of shallower passes (config 3's strip)
+    std::map<int, double> s = {{6, 15.2}, {7, 20.0}, {8, 21.5}, {16, 38.0}, {20, 46.0}};
+    CHECK((cheapest_cut(20, s) == std::vector<int>{20}));
+    CHECK((cheapest_cut(27, s) == std::vector<int>{20, 7}));
+    // the sum of the cut is always k when depth 1 exists; empty when no depth sums to k
+    std::map<int, double> d = {{1, 10}, {5, 20}};
+    for (int k = 1; k <= 40; ++k) {
+        const std::vector<int> v = cheapest_cut(k, d);
+        int sum = 0;
+        for (int x : v) sum += x;
+        CHECK(sum == k && std::is_sorted(v.rbegin(), v.rend()));
+    }
+    CHECK(cheapest_cut(3, {{2, 1.0}}).empty());
+    CHECK(cheapest_cut(0, d).empty());
+}
+
 int main() {
+    test_cheapest_cut();
     test_band_tile_plan();
     test_plan_age_weights();
     test_watchdog();
