@@ -182,7 +182,6 @@ HipEngine::~HipEngine() {
     wd_.reset();  // its thread calls probe(), which reads the members destroyed below
     hipStreamSynchronize(s_comp_);
     hipStreamSynchronize(s_comm_);
-    destroy_xgraphs();  // (they captured the communicator)
     for (auto& kv : sub_plans_) hipFree(kv.second.d);
     for (auto& sb : sub_buf_)
         for (u64* b : sb)
@@ -339,7 +338,7 @@ void HipEngine::do_init(const PatternSpec& p) {
         stats_.kernel = strprintf("resident@%d(%lld tiles x %d waves x %d rows)", res_kin_, (long long)rp.tiles, rp.nw, rp.B);
     }
     stats_.schedule = split_ ? "split" : (halo_items(L_.R).empty() ? "local" : "full");
-    if (dual_) stats_.schedule += sub_overlap_ == 2 ? "+subtiles2xf" : (sub_overlap_ ? "+subtiles2ov" : "+subtiles2");
+    if (dual_) stats_.schedule += sub_overlap_ ? "+subtiles2ov" : "+subtiles2";
     stats_.kernel_depth = dual_ ? tdepth_ : kdepth_;
     stats_.tile_waves = cfg_.tile_waves;
     std::string tn;
@@ -375,12 +374,10 @@ void HipEngine::do_init(const PatternSpec& p) {
     // remainder of the hinted run length), so neither graph capture nor a hinted timed loop
     // builds or uploads a plan.  Other remainders are built on first use.
     for (int k : init_depths()) {
-        if (dual_) {
+        if (dual_)
             prepare_dual(k);
-            capture_xgraphs(k);
-        } else {
+        else
             prepare(k);
-        }
     }
     prewarm_graph();
     if (dual_) {
@@ -466,17 +463,13 @@ void HipEngine::first_pass(int kx, int kp, i64 e, bool split) {
             // profiles/strip_split_round5.txt); with later passes the bands follow the interior on the
             // compute stream, whose wait then finds the exchange done.
             const bool bands_comm = e == 0 && !prof;
-            // (a step_pipe interior leaves every CU the registers and LDS RCCL's kernel needs, so it may
-            // be issued first without holding the exchange back; measurement knob GOL_SPLIT_ORDER)
-            const bool int_first = bands_comm && split_int_first_ && pass_kernel(1, kp) == PK_PIPE;
-            if (int_first) launch(1, kp, 0, src, dst, s_comp_);
             wait_pending(s_comm_, ev_ready_);
             if (prof) HIP_CHECK(hipEventRecord(ev_t0_, s_comm_));
             exchange_device(kx, items, cur_, s_comm_);
             if (prof) HIP_CHECK(hipEventRecord(ev_t1_, s_comm_));
             if (!bands_comm) record_halo();
             if (prof) HIP_CHECK(hipEventRecord(ev_t2_, s_comp_));
-            if (!int_first) launch(1, kp, 0, src, dst, s_comp_);
+            launch(1, kp, 0, src, dst, s_comp_);
             if (bands_comm) {
                 launch(2, kp, e, src, dst, s_comm_);
                 post(dst, s_comm_, e);

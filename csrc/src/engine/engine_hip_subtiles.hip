@@ -32,7 +32,6 @@ void HipEngine::setup_dual() {
 // Free the sub-tile buffers, plans and copy lists (the measurement chose one tile).
 void HipEngine::teardown_dual() {
     synchronize();
-    destroy_xgraphs();
     for (auto& kv : sub_plans_) hipFree(kv.second.d);
     sub_plans_.clear();
     for (auto& sb : sub_buf_)
@@ -109,31 +108,20 @@ void HipEngine::dual_superstep(int k) {
     // per superstep.  (Both halves' interiors first, with the exchange between half 0's interior
     // and its band, measured slower everywhere: 13.2-13.7 vs 12.7-12.8 us/gen at 20 generations
     // through the RCCL self-exchange, the exchange and its ~10 us tail then sit on half 0's critical
-    // path; docs/PERFORMANCE.md section 6.)
+    // path; docs/PERFORMANCE.md section 6.  Round 5: the exchange first on the compute stream with half
+    // 1's interior beside it, 12.36-12.52 against 12.30-12.64, and the exchange replayed from a captured
+    // graph, no faster either; both removed, profiles/strip_split_round5.txt.)
     const bool ov = sub_overlap_ == 1 && !self_y();
-    const bool xf = sub_overlap_ == 2 && !self_y();
-    if (xf) {
-        // The exchange first, on the compute stream (issued before any kernel, so its RCCL kernel is
-        // dispatched first); half 1's first pass, but for its band next to the south halo, meanwhile on
-        // the second stream; then half 0's whole first pass after the exchange, and half 1's band after
-        // the exchange's event, which its stream finds complete by then.
-        dual_exchange(p, k, s_comp_);
-        stats_.exchanges += 1;
-        stats_.halo_bytes += (u64)(rows_bytes(0, k) + rows_bytes(1, k));
-        HIP_CHECK(hipEventRecord(ev_sub_x_, s_comp_));
-        wait_pending(s_comm_, ev_sub_a_);  // half 0's previous superstep (the seam rows half 1 reads)
-        launch_half(1, p, k, s_comm_, 0, 1);
-        launch_half(0, p, k, s_comp_, 0);
-        HIP_CHECK(hipStreamWaitEvent(s_comm_, ev_sub_x_, 0));
-        launch_half(1, p, k, s_comm_, 0, 2);
-    } else if (!self_y()) {
+    if (!self_y()) {
         hipStream_t xs = s_comp_;
         if (ov) {
             launch_half(0, p, k, s_comp_, 0, 1);
             wait_pending(s_comm_, ev_sub_a_);  // the exchange sends half 0's edge and writes its halo
             xs = s_comm_;
         }
-        dual_exchange(p, k, xs);
+        std::vector<Message> sends, recvs;
+        dual_messages(p, k, sends, recvs);
+        exchange_rows(sends, recvs, xs);
         stats_.exchanges += 1;
         stats_.halo_bytes += (u64)(rows_bytes(0, k) + rows_bytes(1, k));
         // (full: also implies half 0's previous superstep, which ran on the same stream)
@@ -153,7 +141,7 @@ void HipEngine::dual_superstep(int k) {
     const int np = (int)pass_depths(k).size();
     for (int j = 0; j < np; ++j)
         for (int s = 0; s < 2; ++s) {  // half 0's pass first (half 1 first measured no better: docs/PERFORMANCE.md §6)
-            if (j == 0 && (xf || (ov && s == 0))) continue;
+            if (ov && s == 0 && j == 0) continue;
             if (j == 0 && s == 0) trace::mark("gol.launch0");  // (GOL_ROCTX: host side of the launch latency)
             launch_half(s, p, k, s ? s_comm_ : s_comp_, j);
             if (j == 0 && s == 0) trace::mark("gol.launch0_done");
@@ -185,57 +173,6 @@ void HipEngine::dual_messages(int p, int k, std::vector<Message>& sends, std::ve
     recvs.push_back({g_.nbr[DIR_S], sub_rows(1, p, h1), rows_bytes(1, k)});
     sends.push_back({g_.nbr[DIR_S], sub_rows(1, p, h1 - k), rows_bytes(1, k)});
     recvs.push_back({g_.nbr[DIR_N], sub_rows(0, p, -k), rows_bytes(0, k)});
-}
-
-// The rank's exchange into / out of the halves' buffer p, on stream xs: replayed from a graph captured at
-// init when GOL_SUBTILE_XGRAPH=1 (an eager RCCL group leaves a ~10 us gap before the next kernel on its
-// queue, a captured one none: kernel traces of the 32768^2 and strip cuts, profiles/strip_split_round5.txt).
-void HipEngine::dual_exchange(int p, int k, hipStream_t xs) {
-    auto it = xgraphs_.find(p * 1000 + k);
-    if (it != xgraphs_.end()) {
-        HIP_CHECK(hipGraphLaunch(it->second, xs));
-        return;
-    }
-    std::vector<Message> sends, recvs;
-    dual_messages(p, k, sends, recvs);
-    exchange_rows(sends, recvs, xs);
-}
-
-void HipEngine::capture_xgraphs(int k) {
-    if (!xgraph_wanted_ || !device_transport_ || !t_->graph_capturable() || self_y()) return;
-    for (int p = 0; p < 3; ++p) {
-        const int key = p * 1000 + k;
-        if (xgraphs_.count(key)) continue;
-        hipGraph_t graph = nullptr;
-        hipGraphExec_t exec = nullptr;
-        try {
-            HIP_CHECK(hipStreamBeginCapture(s_comm_, hipStreamCaptureModeRelaxed));
-            std::vector<Message> sends, recvs;
-            dual_messages(p, k, sends, recvs);
-            t_->exchange(sends, recvs, (void*)s_comm_);
-            HIP_CHECK(hipStreamEndCapture(s_comm_, &graph));
-            HIP_CHECK(hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0));
-            HIP_CHECK(hipGraphDestroy(graph));
-            HIP_CHECK(hipGraphUpload(exec, s_comm_));
-        } catch (const Error& e) {
-            hipGraph_t g2 = nullptr;
-            hipStreamEndCapture(s_comm_, &g2);
-            if (g2) hipGraphDestroy(g2);
-            hipGetLastError();
-            xgraph_wanted_ = false;
-            fprintf(stderr, "[gol] sub-tile exchange graph capture disabled: %s\n", e.what());
-            return;
-        }
-        xgraphs_[key] = exec;
-    }
-}
-
-void HipEngine::destroy_xgraphs() {
-    if (xgraphs_.empty()) return;
-    hipStreamSynchronize(s_comm_);
-    hipStreamSynchronize(s_comp_);
-    for (auto& kv : xgraphs_) hipGraphExecDestroy(kv.second);
-    xgraphs_.clear();
 }
 
 // Device transports (RCCL) are stream ordered on `s`.  Host transports are staged through pinned

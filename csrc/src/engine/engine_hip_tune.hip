@@ -170,7 +170,7 @@ void HipEngine::choose_schedule() {
         // the overlapped variant needs the exchange (neighbours, or the self-exchange)
         std::vector<std::string> dc;
         if (cfg_.subtile_overlap <= 0 || self_y()) dc.push_back("subtiles");
-        if (cfg_.subtile_overlap != 0 && !self_y()) dc.push_back(cfg_.subtile_overlap == 2 ? "subtiles+xf" : "subtiles+ov");
+        if (cfg_.subtile_overlap != 0 && !self_y()) dc.push_back("subtiles+ov");
         if (cfg_.subtiles == 2) cands.clear();
         cands.insert(cands.end(), dc.begin(), dc.end());
     }
@@ -230,7 +230,7 @@ void HipEngine::choose_schedule() {
     sched_pick_ = pick;
     split_ = pick == "split";
     dual_ = pick.rfind("subtiles", 0) == 0;
-    sub_overlap_ = pick == "subtiles+ov" ? 1 : (pick == "subtiles+xf" ? 2 : 0);
+    sub_overlap_ = pick == "subtiles+ov" ? 1 : 0;
     graph_rccl_on_ = cfg_.graph_rccl == 1 || pick == "full+graph";
     if (dual_) {
         setup_dual();
@@ -255,27 +255,72 @@ double HipEngine::sample_schedule(const std::string& c, int k, int reps) {
     return t_->allreduce_max(dt) * 1e6 / ((double)reps * k);
 }
 
-// The chosen schedule timed at the end of init the way the hinted runs execute (same superstep depth,
-// graphs or eager launches, pass cuts and kernels, after a device barrier, from an idle GPU): the
-// median of a few samples, reported as stats.predicted_us_per_gen next to what a run then measures.
-// Collective (every rank runs the same samples).  Long samples (big boards) are cut short.
+// The chosen schedule timed at the end of init the way the hinted runs execute it: the real run() path
+// (graph replay or eager supersteps, pass cuts, kernels, progress markers) on a snapshot of the board,
+// each sample bracketed as bench.py brackets its timed run (sample_run), the median of a few samples,
+// reported as stats.predicted_us_per_gen next to what a run then measures.  The board, its parity and
+// the generation count are restored afterwards.  Without memory for the snapshot (agreed over the
+// ranks) the samples run the schedule on scratch state instead (sample_schedule).  Collective.  Long
+// samples (big boards) are cut short.  Skipped with fault injection (the samples would advance the
+// generation count it watches).
 void HipEngine::predict_run() {
-    if (cfg_.run_hint == 0 || cfg_.compat || sched_pick_.empty()) return;
+    if (cfg_.run_hint == 0 || cfg_.compat || sched_pick_.empty() || fault_gen_ >= 0) return;
     const int k = supported_depth((int)std::min<u64>(cfg_.run_hint, (u64)superstep_depth()));
     const int reps = (int)std::min<u64>(kSchedReps, std::max<u64>(1, cfg_.run_hint / (u64)k));
+    const u64 gens = (u64)k * (u64)reps;
     const EngineStats saved = stats_;
     std::vector<double> v;
     const int rounds = reps == 1 ? 9 : 5;
-    if (res_) {
+    sync_canonical();
+    synchronize();
+    size_t fr = 0, tot = 0;
+    double snap_ok = hipMemGetInfo(&fr, &tot) == hipSuccess && fr > alloc_bytes_ + ((size_t)1 << 30) ? 1.0 : 0.0;
+    if (t_->size() > 1) snap_ok = t_->allreduce_min(snap_ok);
+    u64* snap = nullptr;
+    if (snap_ok > 0 && hipMalloc(&snap, alloc_bytes_) != hipSuccess) {
+        hipGetLastError();
+        snap = nullptr;
+    }
+    if (t_->size() > 1) snap_ok = t_->allreduce_min(snap ? 1.0 : 0.0);
+    if (snap_ok <= 0) {
+        if (snap) hipFree(snap);
+        snap = nullptr;
+    }
+    auto over = [&](std::chrono::steady_clock::time_point t0) {  // (agreed: every rank stops together)
+        return t_->allreduce_max(std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count()) > 1.0;
+    };
+    if (snap) {
+        const int cur0 = cur_;
+        const u64 gen0 = gen_;
+        HIP_CHECK(hipMemcpyAsync(snap, buf_[cur0], alloc_bytes_, hipMemcpyDeviceToDevice, s_comp_));
+        synchronize();
+        run(gens);  // warm-up (loads the sub-tile halves, as a warmup run does before a timed one)
+        const auto t0 = std::chrono::steady_clock::now();
+        for (int r = 0; r < rounds; ++r) {
+            device_barrier();
+            const auto ts = std::chrono::steady_clock::now();
+            run(gens);
+            end_sync();
+            const double dt = std::chrono::duration<double>(std::chrono::steady_clock::now() - ts).count();
+            v.push_back(t_->allreduce_max(dt) * 1e6 / (double)gens);
+            if (over(t0)) break;
+        }
+        synchronize();
+        cur_ = cur0;
+        HIP_CHECK(hipMemcpyAsync(buf_[cur0], snap, alloc_bytes_, hipMemcpyDeviceToDevice, s_comp_));
+        synchronize();
+        HIP_CHECK(hipFree(snap));
+        gen_ = gen0;
+        sub_current_ = false;  // the halves hold a later generation: reload them from the board at the next run
+        canon_stale_ = false;
+    } else if (res_) {
         for (int r = 0; r < rounds; ++r) v.push_back((double)time_resident(res_kin_, k) * 1e3);
     } else {
-        sync_canonical();
         time_schedule(sched_pick_, k, reps);  // warm-up (and the candidate's timing graph)
         const auto t0 = std::chrono::steady_clock::now();
         for (int r = 0; r < rounds; ++r) {
             v.push_back(sample_schedule(sched_pick_, k, reps));
-            if (t_->allreduce_max(std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count()) > 1.0)
-                break;  // (agreed: every rank stops after the same sample)
+            if (over(t0)) break;
         }
         synchronize();
         destroy_sched_graphs();
@@ -284,7 +329,7 @@ void HipEngine::predict_run() {
     std::sort(v.begin(), v.end());
     stats_ = saved;  // the samples' exchanges and replays are not part of any run
     stats_.predicted_us_per_gen = v[(v.size() - 1) / 2];
-    stats_.predicted_gens = k * reps;
+    stats_.predicted_gens = (int)gens;
     init_step("init: prediction", sched_pick_.c_str(), k, (float)stats_.predicted_us_per_gen);
 }
 
@@ -295,8 +340,7 @@ void HipEngine::time_schedule(const std::string& c, int k, int reps, bool eager)
         const bool d0 = dual_;
         const int o0 = sub_overlap_;
         dual_ = true;
-        sub_overlap_ = c == "subtiles+ov" ? 1 : (c == "subtiles+xf" ? 2 : 0);
-        capture_xgraphs(k);  // (GOL_SUBTILE_XGRAPH: once per depth, in the untimed warm-up call)
+        sub_overlap_ = c == "subtiles+ov" ? 1 : 0;
         for (int i = 0; i < reps; ++i) dual_superstep(k);
         dual_ = d0;
         sub_overlap_ = o0;
@@ -636,7 +680,7 @@ std::map<std::string, double> HipEngine::phase_probe(int k) {
     // the schedule the runs use, as choose_schedule timed it (graph variants included)
     std::string sched = sched_pick_;
     if (sched.empty())
-        sched = dual_ ? (sub_overlap_ == 2 ? "subtiles+xf" : (sub_overlap_ ? "subtiles+ov" : "subtiles"))
+        sched = dual_ ? (sub_overlap_ ? "subtiles+ov" : "subtiles")
                       : (split_ ? "split" : (halo_items(L_.R).empty() ? "local" : "full"));
     const int reps = 2;
     double best = 1e30;

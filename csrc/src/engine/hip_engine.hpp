@@ -198,7 +198,7 @@ class HipEngine : public Engine {
         for (size_t j = 0; j < ps.size(); ++j)
             for (int s = 0; s < 2; ++s) sub_plan(s, ps[j], ext_after(ps, j));
         if (sub_overlap_ && !self_y())
-            for (int part : {1, 2}) sub_plan(sub_overlap_ == 2 ? 1 : 0, ps[0], ext_after(ps, 0), part);
+            for (int part : {1, 2}) sub_plan(0, ps[0], ext_after(ps, 0), part);
     }
 
     // part: 0 the whole pass; a first pass split around the exchange (sub_overlap_): 1 all output
@@ -244,11 +244,6 @@ class HipEngine : public Engine {
     void dual_superstep(int k);
     void dual_messages(int p, int k, std::vector<Message>& sends, std::vector<Message>& recvs);
     void exchange_rows(const std::vector<Message>& sends, const std::vector<Message>& recvs, hipStream_t s);
-    void dual_exchange(int p, int k, hipStream_t xs);
-    void capture_xgraphs(int k);
-    void destroy_xgraphs();
-    bool xgraph_wanted_ = env_int("GOL_SUBTILE_XGRAPH", 0) != 0;
-    std::map<int, hipGraphExec_t> xgraphs_;  // (start buffer, depth) -> the rank's exchange, captured
 
     void launch_half(int s, int p, int k, hipStream_t st, int only = -1, int part = 0);
 
@@ -584,7 +579,6 @@ class HipEngine : public Engine {
     bool multipass_ = false;
     std::map<int, std::vector<int>> passes_;
     bool split_ = false;   // superstep schedule: interior/boundary split with overlapped exchange
-    bool split_int_first_ = env_str("GOL_SPLIT_ORDER", "") == "interior";
     bool halo_pending_ = false;  // split: the last superstep's bands on the comm stream are not joined (join_halo)
     std::map<std::string, double> sched_us_;  // choose_schedule: us per generation per candidate
     // measure_pass_costs: us per pass by depth, [0] one tile (kind-0 passes), [1] the two sub-tiles
@@ -635,8 +629,7 @@ class HipEngine : public Engine {
     bool dual_ = false;
     // Exchange overlap of the sub-tile superstep (timed candidates): 0 none ("subtiles"); 1 half 0's
     // first pass, but for its band next to the north halo, runs while the exchange is in flight
-    // ("subtiles+ov"); 2 the exchange first on the compute stream, half 1's first pass but for its
-    // south band meanwhile ("subtiles+xf", GOL_SUBTILE_OVERLAP=2)
+    // ("subtiles+ov")
     int sub_overlap_ = 0;
     Layout sub_L_[2];
     i64 sub_r0_[2] = {0, 0};

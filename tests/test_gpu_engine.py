@@ -80,13 +80,12 @@ def test_subtiles_single_rank(gol, N, R):
     assert np.array_equal(s.board(), numpy_step(cells, R + 1))
 
 
-@pytest.mark.parametrize("overlap", [0, 1, 2])
+@pytest.mark.parametrize("overlap", [0, 1])
 @pytest.mark.parametrize("P", [2, 3])
 def test_subtiles_thread_ranks(gol, P, overlap):
     """Sub-tiles with neighbours: each rank's north / south halos go to its two halves through the
     RCCL-semantics transport (thread ranks sharing one GPU).  overlap=1: half 0's first pass runs,
-    but for its band next to the north halo, while the exchange is in flight; 2: the exchange first,
-    half 1's first pass but for its south band meanwhile (GOL_SUBTILE_OVERLAP)."""
+    but for its band next to the north halo, while the exchange is in flight (GOL_SUBTILE_OVERLAP)."""
     import threading
 
     N, gens = 512, 16 * 4 + 5
@@ -98,7 +97,7 @@ def test_subtiles_thread_ranks(gol, P, overlap):
             s = gol.Simulation(N, ts[r], backend="hip", device=0, global_mode=True, halo_depth=16,
                                kernel="temporal", subtiles=2, subtile_overlap=overlap)
             s.init(5, seed=17)
-            assert s.stats()["schedule"].endswith({0: "+subtiles2", 1: "+subtiles2ov", 2: "+subtiles2xf"}[overlap]), s.stats()
+            assert s.stats()["schedule"].endswith({0: "+subtiles2", 1: "+subtiles2ov"}[overlap]), s.stats()
             s.step(gens)
             out[r] = (s.geometry.row0, s.board())
         except Exception as e:  # pragma: no cover - reported below

@@ -54,20 +54,16 @@ def test_rccl_self_auto_schedule(gol, rccl):
     assert np.array_equal(got, numpy_step(initial_board(5, N, 1, True, 5), gens))
 
 
-@pytest.mark.parametrize("xgraph", ["0", "1"])
-@pytest.mark.parametrize("overlap", [0, 1, 2, -1])
+@pytest.mark.parametrize("overlap", [0, 1, -1])
 @pytest.mark.parametrize("R,gens", [(32, 2 * 32 + 20), (16, 5 * 16 + 3)])
-def test_rccl_self_subtiles(gol, rccl, monkeypatch, R, gens, overlap, xgraph):
+def test_rccl_self_subtiles(gol, rccl, R, gens, overlap):
     """Two sub-tiles per rank: the rank's north / south halos go through RCCL straight into the halves;
     the seam between the halves is read in place by each half's first pass.  overlap=1: half 0's
-    first pass (but its band next to the north halo) runs while the RCCL exchange is in flight; 2:
-    the exchange first, half 1's first pass (but its south band) meanwhile; -1: the init-time timing
-    picks one.  GOL_SUBTILE_XGRAPH=1: the exchange replayed from graphs captured per start buffer."""
-    monkeypatch.setenv("GOL_SUBTILE_XGRAPH", xgraph)
+    first pass (but its band next to the north halo) runs while the RCCL exchange is in flight;
+    -1: the init-time timing picks one."""
     N = 1024
     got, st = _run(gol, rccl, N, gens, 9, halo_depth=R, subtiles=2, run_hint=gens, subtile_overlap=overlap)
-    want = {0: ("full+subtiles2",), 1: ("full+subtiles2ov",), 2: ("full+subtiles2xf",),
-            -1: ("full+subtiles2", "full+subtiles2ov")}[overlap]
+    want = {0: ("full+subtiles2",), 1: ("full+subtiles2ov",), -1: ("full+subtiles2", "full+subtiles2ov")}[overlap]
     assert st["schedule"] in want, st
     if overlap == -1:
         assert "sched:subtiles=" in st["tuning"] and "sched:subtiles+ov=" in st["tuning"], st
