@@ -264,7 +264,9 @@ double HipEngine::sample_schedule(const std::string& c, int k, int reps) {
 // samples (big boards) are cut short.  Skipped with fault injection (the samples would advance the
 // generation count it watches).
 void HipEngine::predict_run() {
-    if (cfg_.run_hint == 0 || cfg_.compat || sched_pick_.empty() || fault_gen_ >= 0) return;
+    if (cfg_.run_hint == 0 || cfg_.compat || sched_pick_.empty()) return;
+    // (fault injection is set on the faulting rank only: agreed, since everything below is collective)
+    if (t_->allreduce_max(fault_gen_ >= 0 ? 1.0 : 0.0) > 0) return;
     const int k = supported_depth((int)std::min<u64>(cfg_.run_hint, (u64)superstep_depth()));
     const int reps = (int)std::min<u64>(kSchedReps, std::max<u64>(1, cfg_.run_hint / (u64)k));
     const u64 gens = (u64)k * (u64)reps;
