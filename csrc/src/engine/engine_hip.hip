@@ -315,6 +315,12 @@ void HipEngine::do_init(const PatternSpec& p) {
         // will use (config 3's strip: one step_pipe pass of 20 instead of 7 + 7 + 6 changed the winner)
         kick("init: pass costs");
         measure_pass_costs();
+        // the split first pass's kernels again, at the depth the hinted superstep's cut starts with
+        if (split_used() && !pass_costs().empty()) {
+            const int kh = cfg_.run_hint > 0 && cfg_.run_hint < (u64)L_.R ? supported_depth((int)cfg_.run_hint) : L_.R;
+            const int d0 = pass_depths(kh)[0];
+            if (d0 != kdepth_) tune_split_kinds(d0);
+        }
         kick("init: schedule timing");
         choose_schedule();  // collective when ranks have neighbours
         if (dual_) {

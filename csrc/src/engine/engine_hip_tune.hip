@@ -409,6 +409,60 @@ void HipEngine::time_schedule(const std::string& c, int k, int reps, bool eager)
     split_ = split0;
 }
 
+// The kernels of a split superstep's first pass at depth k: the interior (kind 1) and the bands next to
+// the halos (kind 2), each timed among step_temporal (where instantiated), the LDS tile kernel and, when
+// the full tile runs step_pipe, step_pipe (the bands' passes at the depths of step_pipe passes are
+// latency-bound: 10 stages x 2 generations stream a 60-row segment, where the tile kernel runs 20
+// generations of barriers, 38 us for a 20-row band of config 3's strip; profiles/strip_split_round5.txt).
+void HipEngine::tune_split_kinds(int k) {
+    if (cfg_.kernel != "auto" && cfg_.kernel != "resident") return;
+    std::vector<const char*> cands = {"temporal", "tile"};
+    if (kern_[0] == "pipe") cands.push_back("pipe");
+    hipEvent_t e0, e1;
+    HIP_CHECK(hipEventCreate(&e0));
+    HIP_CHECK(hipEventCreate(&e1));
+    auto usable = [&](int kind, const char* c) {
+        kern_[kind] = c;
+        if (kern_[kind] == "tile") return tile_rows_cap(k) >= 1 && tile_rounds(kind, k, 0) <= kMaxTileRounds;
+        if (kern_[kind] == "temporal") return hipk::step_depth_supported(k);
+        return pipe_geo(k) != nullptr;
+    };
+    for (int kind : {1, 2})  // every plan first (plan building idles the GPU)
+        for (const char* c : cands)
+            if (usable(kind, c)) plan(kind, k, 0);
+    spin_up();
+    for (int kind : {1, 2}) {
+        float bk = 1e30f;
+        const char* pk = "temporal";
+        for (int round = 0; round < 2; ++round)
+            for (const char* c : cands) {
+                if (!usable(kind, c)) continue;
+                launch(kind, k, 0, buf_[cur_], buf_[cur_ ^ 1], s_comp_);  // warm-up
+                HIP_CHECK(hipEventRecord(e0, s_comp_));
+                for (int i = 0; i < 3; ++i) launch(kind, k, 0, buf_[cur_], buf_[cur_ ^ 1], s_comp_);
+                HIP_CHECK(hipEventRecord(e1, s_comp_));
+                HIP_CHECK(hipEventSynchronize(e1));
+                float ms = 0;
+                HIP_CHECK(hipEventElapsedTime(&ms, e0, e1));
+                float per_gen = ms / 3 / (float)k;
+                if (kern_[kind] == "pipe" && hipk::pipe_fault()) per_gen = 1e30f;  // a ring wait timed out
+                init_step("init: split kernels", c, k, per_gen);
+                const std::string key = strprintf("%d:%s@%d", kind, c, k);
+                auto it = tune_ms_.find(key);
+                tune_ms_[key] = it == tune_ms_.end() ? per_gen : std::min(it->second, per_gen);
+                if (per_gen < bk) {
+                    bk = per_gen;
+                    pk = c;
+                }
+            }
+        kern_[kind] = pk;
+    }
+    HIP_CHECK(hipEventDestroy(e0));
+    HIP_CHECK(hipEventDestroy(e1));
+    pipe_used_ = false;  // (the candidates ran on scratch; faults were checked above)
+    passes_.clear();
+}
+
 // GOL_KERNEL=auto: for every plan kind a run uses (full tile; interior + boundary bands when
 // split), time one superstep of each candidate kernel (into the scratch buffer, so the board is
 // untouched) and keep the faster one.  The register pipeline wins on big regions; the
@@ -561,33 +615,9 @@ void HipEngine::autotune_kernel() {
         pipe_k_ = 0;
     }
     passes_.clear();
-    // interior / boundary plans of split supersteps, at the chosen pass depth
-    if (split_used()) {
-        // (the interior and the bands may run step_pipe when the full tile does: the bands' passes at
-        // the depths of step_pipe passes are latency-bound, 10 stages x 2 generations streaming a 60-row
-        // segment, where the tile kernel runs 20 generations of barriers: 38 us for a 20-row band of
-        // config 3's strip, profiles/strip_split_round5.txt)
-        auto kcands = [&](int kind) {
-            std::vector<const char*> v = {"temporal", "tile"};
-            if (kern_[0] == "pipe") v.push_back("pipe");
-            return v;
-        };
-        for (int kind : {1, 2})
-            for (const char* c : kcands(kind)) time_pass(kind, c, kdepth_, true);
-        spin_up();
-        for (int kind : {1, 2}) {
-            float bk = 1e30f;
-            const char* pk = "temporal";
-            for (const char* c : kcands(kind)) {
-                const float t = time_pass(kind, c, kdepth_);
-                if (t < bk) {
-                    bk = t;
-                    pk = c;
-                }
-            }
-            kern_[kind] = pk;
-        }
-    }
+    // interior / boundary plans of split supersteps, at the chosen pass depth (tuned again at the
+    // first-pass depth of the hinted superstep once the pass costs fix the cut: tune_split_kinds)
+    if (split_used()) tune_split_kinds(kdepth_);
     HIP_CHECK(hipEventDestroy(e0));
     HIP_CHECK(hipEventDestroy(e1));
     kernel_ = kern_[0];

@@ -437,6 +437,7 @@ class HipEngine : public Engine {
     }
 
     void autotune_kernel();
+    void tune_split_kinds(int k);
 
     bool can_overlap() const {
         // an interior must exist on EVERY rank (the schedule timing is collective, so the decision
