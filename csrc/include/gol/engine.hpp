@@ -123,6 +123,13 @@ class Engine {
     // transport also a 1-element all-reduce on the compute stream, waited for, so every rank leaves
     // when the collective has completed on the GPUs, not when a host barrier happened to release it.
     virtual void device_barrier() { t_->barrier(); }
+    // The end of a timed region: every GPU stream of this rank drained (HIP: device-wide when the device
+    // is not shared with other ranks of the process, as torch.cuda.synchronize() in bench.py).
+    virtual void device_sync() { synchronize(); }
+    // Collective: `reps` timed runs of `gens` generations on the live board (it advances), each bracketed
+    // as bench.py brackets its timed run (device_barrier, the run, device_sync); us per generation, max
+    // over the ranks.  Used by the HIP engine's init-time prediction and by tools/predict_gap.py.
+    std::vector<double> time_runs(u64 gens, int reps);
     // Collective, untimed: per-phase GPU costs of a k-generation superstep of the schedule in use, in
     // us: "exchange_us" (the halo exchange alone, when there is one) and "superstep_us" (a whole
     // superstep, exchange included), each the best of a few rounds.  Runs on scratch state: the

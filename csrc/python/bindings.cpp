@@ -300,6 +300,7 @@ PYBIND11_MODULE(_gol, m) {
         .def("fingerprint", &Engine::fingerprint, py::call_guard<py::gil_scoped_release>())
         .def("device_barrier", &Engine::device_barrier, py::call_guard<py::gil_scoped_release>())
         .def("phase_probe", &Engine::phase_probe, py::arg("k"), py::call_guard<py::gil_scoped_release>())
+        .def("time_runs", &Engine::time_runs, py::arg("gens"), py::arg("reps"), py::call_guard<py::gil_scoped_release>())
         .def_property_readonly("geometry", &Engine::geometry)
         .def_property_readonly("layout", &Engine::layout)
         .def_property_readonly("generation", &Engine::generation)

@@ -215,6 +215,19 @@ void Engine::run(u64 generations) {
     maybe_inject_fault();
 }
 
+std::vector<double> Engine::time_runs(u64 gens, int reps) {
+    std::vector<double> v;
+    for (int r = 0; r < reps; ++r) {
+        device_barrier();
+        const auto t0 = std::chrono::steady_clock::now();
+        run(gens);
+        device_sync();
+        const double dt = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+        v.push_back(t_->allreduce_max(dt) * 1e6 / (double)std::max<u64>(1, gens));
+    }
+    return v;
+}
+
 u64 Engine::population() { return t_->allreduce_sum(local_reduce().first); }
 u64 Engine::fingerprint() { return t_->allreduce_sum(local_reduce().second); }
 

@@ -299,12 +299,7 @@ void HipEngine::predict_run() {
         run(gens);  // warm-up (loads the sub-tile halves, as a warmup run does before a timed one)
         const auto t0 = std::chrono::steady_clock::now();
         for (int r = 0; r < rounds; ++r) {
-            device_barrier();
-            const auto ts = std::chrono::steady_clock::now();
-            run(gens);
-            end_sync();
-            const double dt = std::chrono::duration<double>(std::chrono::steady_clock::now() - ts).count();
-            v.push_back(t_->allreduce_max(dt) * 1e6 / (double)gens);
+            v.push_back(time_runs(gens, 1)[0]);
             if (over(t0)) break;
         }
         synchronize();
@@ -432,7 +427,7 @@ void HipEngine::tune_split_kinds(int k) {
             if (usable(kind, c)) plan(kind, k, 0);
     spin_up();
     for (int kind : {1, 2}) {
-        float bk = 1e30f;
+        float bk = 1e30f, bpipe = 1e30f;
         const char* pk = "temporal";
         for (int round = 0; round < 2; ++round)
             for (const char* c : cands) {
@@ -450,11 +445,18 @@ void HipEngine::tune_split_kinds(int k) {
                 const std::string key = strprintf("%d:%s@%d", kind, c, k);
                 auto it = tune_ms_.find(key);
                 tune_ms_[key] = it == tune_ms_.end() ? per_gen : std::min(it->second, per_gen);
+                if (kern_[kind] == "pipe") bpipe = std::min(bpipe, per_gen);
                 if (per_gen < bk) {
                     bk = per_gen;
                     pk = c;
                 }
             }
+        // The interior runs beside the exchange: a step_pipe interior (59 VGPRs per wave, 92 KiB of LDS per
+        // workgroup) leaves every CU room for RCCL's kernel and the bands, the tile kernel does not, so
+        // step_pipe is kept within 5% of the fastest alone (config 3's strip: interior tile@20 2.35 vs
+        // pipe@20 2.37 us/gen alone, the split superstep 4.28 vs 3.52-3.58 us/gen with them;
+        // profiles/strip_split_round5.txt)
+        if (kind == 1 && bpipe <= 1.05f * bk) pk = "pipe";
         kern_[kind] = pk;
     }
     HIP_CHECK(hipEventDestroy(e0));

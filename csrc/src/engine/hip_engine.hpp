@@ -335,6 +335,7 @@ class HipEngine : public Engine {
     // The end of a timed sample: bench.py's device-wide synchronisation when this process's engines do not
     // share the device (one rank, or RCCL: one rank per GPU), else the engine's own streams (thread ranks
     // on one GPU: a device-wide wait could wait for a peer's exchange this thread has yet to issue).
+    void device_sync() override { end_sync(); }
     void end_sync() {
         if (t_->size() > 1 && t_->name().rfind("rccl", 0) != 0) return synchronize();
         Armed armed(wd_.get());

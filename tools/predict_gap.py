@@ -7,6 +7,7 @@ run, torch.cuda.synchronize()):
 
   bench      after a `--warmup` run, as bench.py does
   again      right after the previous timed run (no warmup run in between)
+  cxx        the same bracket timed in C++ (Engine::time_runs: what the init-time prediction runs)
   idle<ms>   after sleeping that long with the GPU idle (clock state)
   noop       an empty run (sim.step(0)): the Python + pybind + sync floor
 
@@ -57,11 +58,12 @@ def main():
         torch.cuda.synchronize()
         return (time.perf_counter() - t0) * 1e6
 
-    res = {k: [] for k in ("bench", "again", "idle1", "idle10", "idle100", "noop")}
+    res = {k: [] for k in ("bench", "again", "cxx", "idle1", "idle10", "idle100", "noop")}
     for _ in range(a.reps):
         sim.step(a.warmup)
         res["bench"].append(timed(a.steps) / a.steps)
         res["again"].append(timed(a.steps) / a.steps)
+        res["cxx"].extend(sim.engine.time_runs(a.steps, 1))  # the same bracket in C++ (the prediction's)
         for ms in (1, 10, 100):
             sim.synchronize()
             time.sleep(ms / 1e3)
