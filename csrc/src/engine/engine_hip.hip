@@ -469,15 +469,17 @@ void HipEngine::first_pass(int kx, int kp, i64 e, bool split) {
             // profiles/strip_split_round5.txt); with later passes the bands follow the interior on the
             // compute stream, whose wait then finds the exchange done.
             const bool bands_comm = e == 0 && !prof;
+            const bool int_first = bands_comm && split_int_first_;  // (measurement knob GOL_SPLIT_ORDER)
+            if (int_first) launch(1, kp, 0, src, dst, s_comp_);
             wait_pending(s_comm_, ev_ready_);
             if (prof) HIP_CHECK(hipEventRecord(ev_t0_, s_comm_));
             exchange_device(kx, items, cur_, s_comm_);
             if (prof) HIP_CHECK(hipEventRecord(ev_t1_, s_comm_));
             if (!bands_comm) record_halo();
             if (prof) HIP_CHECK(hipEventRecord(ev_t2_, s_comp_));
-            launch(1, kp, 0, src, dst, s_comp_);
+            if (!int_first) launch(1, kp, 0, src, dst, s_comp_);
             if (bands_comm) {
-                launch(2, kp, e, src, dst, s_comm_);
+                launch(2, kp, e, src, dst, s_comm_, band_prio_ ? hipk::STEP_PRIO : 0u);
                 post(dst, s_comm_, e);
                 record_halo();
                 halo_pending_ = true;
@@ -528,7 +530,7 @@ void HipEngine::do_set_compat_halos(const std::vector<u64>& above, const std::ve
     synchronize();
 }
 
-void HipEngine::launch(int kind, int k, i64 e, const u64* src, u64* dst, hipStream_t s) {
+void HipEngine::launch(int kind, int k, i64 e, const u64* src, u64* dst, hipStream_t s, u32 xflags) {
     if (kernel_ == "lds") {
         // full-row bands only (the LDS variant is never split by columns: can_overlap)
         for (const Region& r : regions(kind, 1))
@@ -536,7 +538,7 @@ void HipEngine::launch(int kind, int k, i64 e, const u64* src, u64* dst, hipStre
     } else {
         const DevPlan& p = plan(kind, k, e);
         if (p.st.out_words == 0) return;
-        hipk::StepParams sp{L_.pitch, (i32)L_.h, (i32)L_.nw, L_.R, step_flags() | p.tflags};
+        hipk::StepParams sp{L_.pitch, (i32)L_.h, (i32)L_.nw, L_.R, step_flags() | p.tflags | xflags};
         const PassKernel pk = pass_kernel(kind, k);
         if (pk == PK_TILE) {
             hipk::launch_step_tile(cfg_.tile_waves, k, src, dst, p.d, p.waves, p.rows, sp, s);

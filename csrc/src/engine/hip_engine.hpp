@@ -453,7 +453,7 @@ class HipEngine : public Engine {
 
     const DevPlan& plan(int kind, int k, i64 e = 0);
 
-    void launch(int kind, int k, i64 e, const u64* src, u64* dst, hipStream_t s);
+    void launch(int kind, int k, i64 e, const u64* src, u64* dst, hipStream_t s, u32 xflags = 0);
 
     // Ghost words for widths that are not a multiple of 64 when the tile is its own E/W neighbour.
     void post(u64* buf, hipStream_t s, i64 rem = 0) {
@@ -581,6 +581,8 @@ class HipEngine : public Engine {
     bool multipass_ = false;
     std::map<int, std::vector<int>> passes_;
     bool split_ = false;   // superstep schedule: interior/boundary split with overlapped exchange
+    bool split_int_first_ = env_str("GOL_SPLIT_ORDER", "") == "interior";  // measurement knobs
+    bool band_prio_ = env_int("GOL_BAND_PRIO", 0) != 0;
     bool halo_pending_ = false;  // split: the last superstep's bands on the comm stream are not joined (join_halo)
     std::map<std::string, double> sched_us_;  // choose_schedule: us per generation per candidate
     // measure_pass_costs: us per pass by depth, [0] one tile (kind-0 passes), [1] the two sub-tiles
