@@ -32,8 +32,6 @@ enum : u32 {
     STEP_TILE_L4 = 1u << 6, // tile kernel: four generations per LDS pass
     STEP_TILE_INPLACE = 1u << 7,  // tile kernel: one tile buffer updated in place (twice the rows)
     STEP_TILE_FOLD = 1u << 8,     // tile kernel: 32-lane tiles folded in half (fold plans, plan.hpp)
-    STEP_PRIO = 1u << 9,    // tile kernel: raise the waves' issue priority (s_setprio): the bands of a
-                            // split superstep running beside the interior kernel on the same CUs
     STEP_SEAM = 1u << 5,    // temporal kernel: rows < 0 are read from StepParams::above, rows >= h
                             // from StepParams::below (sub-tile first pass: the other half's edges)
 };

@@ -469,7 +469,12 @@ void HipEngine::first_pass(int kx, int kp, i64 e, bool split) {
             // profiles/strip_split_round5.txt); with later passes the bands follow the interior on the
             // compute stream, whose wait then finds the exchange done.
             const bool bands_comm = e == 0 && !prof;
-            const bool int_first = bands_comm && split_int_first_;  // (measurement knob GOL_SPLIT_ORDER)
+            // A step_pipe interior (59 VGPRs per wave, 92 KiB of LDS per workgroup) leaves every CU room
+            // for RCCL's kernel (256 VGPRs, 37.6 KiB) and the bands, so it is issued first: the strip's
+            // driver cut 3.46-3.57 against 3.63-3.91 us/gen exchange first (interleaved, one box).  (Raising
+            // the bands' wave priority instead, s_setprio, slowed the interior more than it sped the bands:
+            // 3.90-6.35; profiles/strip_split_round5.txt batch 8.)
+            const bool int_first = bands_comm && pass_kernel(1, kp) == PK_PIPE;
             if (int_first) launch(1, kp, 0, src, dst, s_comp_);
             wait_pending(s_comm_, ev_ready_);
             if (prof) HIP_CHECK(hipEventRecord(ev_t0_, s_comm_));
@@ -479,7 +484,7 @@ void HipEngine::first_pass(int kx, int kp, i64 e, bool split) {
             if (prof) HIP_CHECK(hipEventRecord(ev_t2_, s_comp_));
             if (!int_first) launch(1, kp, 0, src, dst, s_comp_);
             if (bands_comm) {
-                launch(2, kp, e, src, dst, s_comm_, band_prio_ ? hipk::STEP_PRIO : 0u);
+                launch(2, kp, e, src, dst, s_comm_);
                 post(dst, s_comm_, e);
                 record_halo();
                 halo_pending_ = true;

@@ -581,8 +581,6 @@ class HipEngine : public Engine {
     bool multipass_ = false;
     std::map<int, std::vector<int>> passes_;
     bool split_ = false;   // superstep schedule: interior/boundary split with overlapped exchange
-    bool split_int_first_ = env_str("GOL_SPLIT_ORDER", "") == "interior";  // measurement knobs
-    bool band_prio_ = env_int("GOL_BAND_PRIO", 0) != 0;
     bool halo_pending_ = false;  // split: the last superstep's bands on the comm stream are not joined (join_halo)
     std::map<std::string, double> sched_us_;  // choose_schedule: us per generation per candidate
     // measure_pass_costs: us per pass by depth, [0] one tile (kind-0 passes), [1] the two sub-tiles

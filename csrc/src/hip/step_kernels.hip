@@ -72,7 +72,6 @@ __global__ __launch_bounds__(64 * NW) void step_tile(const u64* __restrict__ src
     const LaneDesc d = plan[(i64)blockIdx.x * kWaveLanes + lane];
     const int nrows = __builtin_amdgcn_readfirstlane(d.nrows);
     if (nrows <= 0) return;  // padding tile (uniform over the workgroup)
-    if (p.flags & STEP_PRIO) __builtin_amdgcn_s_setprio(3);
     tile_item<NW, WRAPY, LV, IP>(src, dst, d, nrows, p, K, tile_lds, wv, lane, blockIdx.x);
 }
 
@@ -85,7 +84,6 @@ __global__ __launch_bounds__(64 * NW) void step_tile_fold(const u64* __restrict_
     const LaneDesc d = plan[(i64)blockIdx.x * kWaveLanes + lane];  // lanes 32-63 repeat lanes 0-31
     const int nrows = __builtin_amdgcn_readfirstlane(d.nrows);
     if (nrows <= 0) return;  // padding tile (uniform over the workgroup)
-    if (p.flags & STEP_PRIO) __builtin_amdgcn_s_setprio(3);
     fold_item<NW, WRAPY, LV, IP>(src, dst, d, nrows, p, K, tile_lds, wv, lane, blockIdx.x);
 }
 
