@@ -11,7 +11,7 @@ void HipEngine::prepare(int k) {
     }
     const std::vector<int>& ps = pass_depths(k);
     plan(0, ps[0], ext_after(ps, 0));
-    if (can_overlap()) {
+    if (split_used()) {  // (only split supersteps run the interior / band plans)
         plan(1, ps[0]);
         plan(2, ps[0], ext_after(ps, 0));
     }

@@ -269,10 +269,10 @@ void HipEngine::predict_run() {
     if (t_->allreduce_max(fault_gen_ >= 0 ? 1.0 : 0.0) > 0) return;
     const int k = supported_depth((int)std::min<u64>(cfg_.run_hint, (u64)superstep_depth()));
     const int reps = (int)std::min<u64>(kSchedReps, std::max<u64>(1, cfg_.run_hint / (u64)k));
-    const u64 gens = (u64)k * (u64)reps;
+    u64 gens = (u64)k * (u64)reps;  // (snapshot path: the hinted run itself, when it takes <= ~50 ms)
     const EngineStats saved = stats_;
     std::vector<double> v;
-    const int rounds = reps == 1 ? 9 : 5;
+    int rounds = reps == 1 ? 9 : 5;
     sync_canonical();
     synchronize();
     size_t fr = 0, tot = 0;
@@ -296,7 +296,16 @@ void HipEngine::predict_run() {
         const u64 gen0 = gen_;
         HIP_CHECK(hipMemcpyAsync(snap, buf_[cur0], alloc_bytes_, hipMemcpyDeviceToDevice, s_comp_));
         synchronize();
-        run(gens);  // warm-up (loads the sub-tile halves, as a warmup run does before a timed one)
+        // warm-up (loads the sub-tile halves, as a warmup run does before a timed one), then the samples
+        // run the whole hinted run when it is short enough: a 1000-generation run of 8192^2 is one graph
+        // replay, which samples of 4 supersteps would charge four graph launches per 128 generations
+        const double w = time_runs(gens, 1)[0];
+        const u64 fit = (u64)(0.05e6 / std::max(1e-3, w));
+        gens = std::max<u64>(gens, std::min<u64>(cfg_.run_hint, fit));
+        if (gens > (u64)k * reps) {
+            rounds = 5;
+            run(gens);
+        }
         const auto t0 = std::chrono::steady_clock::now();
         for (int r = 0; r < rounds; ++r) {
             v.push_back(time_runs(gens, 1)[0]);
