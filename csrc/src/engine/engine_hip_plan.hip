@@ -157,8 +157,9 @@ const DevPlan& HipEngine::plan(int kind, int k, i64 e) {
         if (rmax < 1) throw Error(strprintf("GOL_KERNEL=tile: depth %d leaves no LDS rows", k));
         if (!fold && rows > rmax) rows = rmax;
         if (tile_rounds(kind, k, e) > kMaxTileRounds)
-            throw Error(strprintf("GOL_KERNEL=tile: this tile needs %lld rounds of LDS tiles; use the temporal "
-                                  "kernel for boards this large",
+            throw Error(strprintf("LDS tile kernel (plan kind %d, depth %d, tuned kernels %s/%s/%s): this tile needs "
+                                  "%lld rounds of LDS tiles; use the temporal kernel for boards this large",
+                                  kind, k, kern_[0].c_str(), kern_[1].c_str(), kern_[2].c_str(),
                                   (long long)tile_rounds(kind, k, e)));
         if (rows <= 0) {  // (a folded plan has its rows already)
             const i64 rounds = ceil_div(r1, rmax);

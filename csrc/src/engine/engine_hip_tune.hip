@@ -93,6 +93,7 @@ void HipEngine::measure_pass_costs() {
     hipEvent_t e0, e1;
     HIP_CHECK(hipEventCreate(&e0));
     HIP_CHECK(hipEventCreate(&e1));
+    if (!dual_) pipe_geo_.clear();  // (the spin-up runs the tuned kernel at its own depth, not a candidate's)
     spin_up();
     const int reps = 4;
     std::vector<double> best(cs.size(), 1e30);
@@ -450,7 +451,7 @@ void HipEngine::tune_split_kinds(int k) {
                 HIP_CHECK(hipEventElapsedTime(&ms, e0, e1));
                 float per_gen = ms / 3 / (float)k;
                 if (kern_[kind] == "pipe" && hipk::pipe_fault()) per_gen = 1e30f;  // a ring wait timed out
-                init_step("init: split kernels", c, k, per_gen);
+                init_step("init: split kernels", c, k, per_gen * 1e3f);
                 const std::string key = strprintf("%d:%s@%d", kind, c, k);
                 auto it = tune_ms_.find(key);
                 tune_ms_[key] = it == tune_ms_.end() ? per_gen : std::min(it->second, per_gen);
@@ -507,7 +508,7 @@ void HipEngine::autotune_kernel() {
         float ms = 0;
         HIP_CHECK(hipEventElapsedTime(&ms, e0, e1));
         float per_gen = ms / 3 / (float)k;
-        init_step("init: kernel autotune", kern, k, per_gen);
+        init_step("init: kernel autotune", kern, k, per_gen * 1e3f);
         if (pipe && hipk::pipe_fault()) {  // a ring wait timed out: never pick this geometry
             fprintf(stderr, "[gol] step_pipe %dx%d: a ring wait timed out in the kernel autotune; candidate dropped\n",
                     pipe_cur_.nw - 1, pipe_cur_.l);
