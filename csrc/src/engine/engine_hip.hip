@@ -164,6 +164,10 @@ void HipEngine::note_progress() {
     Marker& m = marker_slot();
     HIP_CHECK(hipEventRecord(m.ev[0], s_comp_));
     m.n = 1;
+    if (halo_pending_) {  // a one-pass split superstep left its exchange and bands on the comm stream
+        HIP_CHECK(hipEventRecord(m.ev[1], s_comm_));
+        m.n = 2;
+    }
     publish_marker();
 }
 
@@ -468,12 +472,16 @@ void HipEngine::first_pass(int kx, int kp, i64 e, bool split) {
             // event, more than the ~14 us exchange it would hide (kernel traces of config 3's strip,
             // profiles/strip_split_round5.txt); with later passes the bands follow the interior on the
             // compute stream, whose wait then finds the exchange done.
-            const bool bands_comm = e == 0 && !prof;
+            // (Not when the ghost columns of an unaligned self-wrapped width are refilled after the pass:
+            // post() reads the first and last words of EVERY row, so it must follow both the interior and
+            // the bands on one stream.)
+            const bool bands_comm = e == 0 && !prof && !(self_x() && !L_.aligned());
             // A step_pipe interior (59 VGPRs per wave, 92 KiB of LDS per workgroup) leaves every CU room
             // for RCCL's kernel (256 VGPRs, 37.6 KiB) and the bands, so it is issued first: the strip's
             // driver cut 3.46-3.57 against 3.63-3.91 us/gen exchange first (interleaved, one box).  (Raising
             // the bands' wave priority instead, s_setprio, slowed the interior more than it sped the bands:
             // 3.90-6.35; profiles/strip_split_round5.txt batch 8.)
+            guard_exchange_stream(s_comm_);  // (before any event query or launch of a capture attempt)
             const bool int_first = bands_comm && pass_kernel(1, kp) == PK_PIPE;
             if (int_first) launch(1, kp, 0, src, dst, s_comp_);
             wait_pending(s_comm_, ev_ready_);

@@ -25,7 +25,9 @@ bool HipEngine::graph_shape(int& k, int& m) {
     // Split supersteps with an exchange stay eager: captured (the RCCL group on the capture's origin
     // stream, the interior on a forked one) the exchange kernel started ~140 us into the replay,
     // 5.5 ms per 20-generation strip run against 4.1-4.9 eager (profiles/strip_split_round5.txt).
-    if (!local && split_) return false;
+    // (GOL_GRAPH_SPLIT=1, a test knob, attempts that capture anyway: guard_exchange_stream refuses the
+    // exchange on the comm stream, the capture fails and the supersteps run eagerly)
+    if (!local && split_ && !split_capture_test_) return false;
     return true;
 }
 

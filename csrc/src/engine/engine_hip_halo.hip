@@ -82,6 +82,7 @@ void HipEngine::build_messages(int k, const std::vector<HaloItem>& items, int pa
 
 void HipEngine::exchange_device(int k, const std::vector<HaloItem>& items, int parity, hipStream_t s) {
     trace::Range r("gol.exchange_device");
+    guard_exchange_stream(s);
     const DevCopies& dc = copies(k, parity);
     if (dc.npack) hipk::launch_copy_regions(dc.pack, dc.npack, dc.max_pack, s);
     std::vector<Message> sends, recvs;

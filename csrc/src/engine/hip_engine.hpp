@@ -411,7 +411,9 @@ class HipEngine : public Engine {
     enum PassKernel { PK_TEMPORAL, PK_TILE, PK_PIPE };
     PassKernel pass_kernel(int kind, int k) const {
         if (kern_[kind] == "tile") return PK_TILE;
-        if ((kern_[kind] == "pipe" || (kind == 1 && kern_[0] == "pipe")) && pipe_geo(k)) return PK_PIPE;
+        // (an interior explicitly tuned to step_temporal keeps it: tune_split_kinds times it as such)
+        if ((kern_[kind] == "pipe" || (kind == 1 && kern_[0] == "pipe" && kern_[1] != "temporal")) && pipe_geo(k))
+            return PK_PIPE;
         return hipk::step_depth_supported(k) ? PK_TEMPORAL : PK_TILE;
     }
     bool tile_pass(int kind, int k) const { return pass_kernel(kind, k) == PK_TILE; }
@@ -462,6 +464,18 @@ class HipEngine : public Engine {
     }
 
     // ----- halo exchange -----
+    // A graph capture never gets an exchange on any stream but its origin, the compute stream: an RCCL group
+    // on a stream forked into a capture crashed librccl at capture time (round 5's split+graph superstep;
+    // tools/rccl_capture_probe.cpp, docs/PERFORMANCE.md §17).  Throws instead, before any RCCL call, so a
+    // capture attempt falls back to eager supersteps (graph_for) and a timing candidate is dropped.
+    void guard_exchange_stream(hipStream_t s) const {
+        if (s == s_comp_) return;
+        hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+        HIP_CHECK(hipStreamIsCapturing(s, &cs));
+        if (cs != hipStreamCaptureStatusNone || capturing())
+            throw Error("exchange on a stream other than the capture's origin stream refused (an RCCL group on a "
+                        "stream forked into a graph capture crashes librccl)");
+    }
     const std::vector<HaloItem>& items_for(int k) {
         auto it = items_.find(k);
         if (it != items_.end()) return it->second;
@@ -608,6 +622,7 @@ class HipEngine : public Engine {
     // cut lost its overlapped schedule, 13.5-13.8 vs 12.1-12.2; profiles/event_fence_ab.txt.)
     static constexpr unsigned event_flags() { return hipEventDisableTiming; }
     bool graph_ok_ = true;
+    const bool split_capture_test_ = env_int("GOL_GRAPH_SPLIT", 0) != 0;
     bool graph_rccl_on_ = false;  // one-tile supersteps with an RCCL exchange are captured (choose_schedule)
     // timing graphs of the graphed schedule candidates ("local", "full+graph"), by name
     struct SchedGraph {

@@ -569,3 +569,18 @@ def test_torch_device_sync_covers_engine_streams(gol):
     s.step(1000)  # ~10 ms of GPU work, enqueued in well under that
     torch.cuda.synchronize()
     assert s.engine.gpu_idle()
+
+
+@pytest.mark.parametrize("subtiles", [0, 2])
+def test_prediction_without_snapshot(gol, monkeypatch, subtiles):
+    """predict_run's scratch-state branch (no memory for a board snapshot, as on BASELINE config 5's 2^20-row
+    tile; forced with GOL_PREDICT_SNAPSHOT=0): the prediction is measured and the board stays intact, so
+    the hinted run after init is exact."""
+    monkeypatch.setenv("GOL_PREDICT_SNAPSHOT", "0")
+    N, hint = 2048, 20
+    s = _sim(gol, N, halo_depth=64, kernel="temporal", run_hint=hint, subtiles=subtiles).init(5, seed=31)
+    st = s.stats()
+    assert st["predicted_us_per_gen"] > 0 and st["predicted_gens"] == hint, st
+    s.step(5)
+    s.step(hint)
+    assert np.array_equal(s.board(), numpy_step(initial_board(5, N, 1, True, 31), 5 + hint))

@@ -130,3 +130,35 @@ def test_rccl_self_split_pipe(gol, rccl, monkeypatch, pipe, H, R, gens):
                    halo_depth=R)
     assert st["schedule"] == "split" and st["exchanges"] >= 1 and st["graph_launches"] == 0, st
     assert np.array_equal(got, numpy_step(random_board(H, W, 3), gens))
+
+
+@pytest.mark.parametrize("W", [1000, 4032 + 7])
+def test_rccl_self_split_unaligned_width(gol, rccl, W):
+    """A width that is not a multiple of 64 on a strip that wraps E/W onto itself: after a one-pass split
+    superstep the ghost columns are refilled from the first and last words of every row, so that refill
+    must follow both the interior (compute stream) and the bands (comm stream) -- the bands then run on
+    the compute stream after the exchange instead of beside the interior.  Supersteps of
+    one step_temporal pass (R = K = 8) and a one-pass remainder."""
+    H, R = 1024, 8
+    gens = 3 * R + 5
+    got, st = _run(gol, rccl, H, gens, 4, width=W, schedule="split", kernel="temporal", subtiles=0, halo_depth=R,
+                   run_hint=gens)
+    assert st["schedule"] == "split" and st["exchanges"] >= 3, st
+    assert np.array_equal(got, numpy_step(random_board(H, W, 4), gens))
+
+
+def test_rccl_split_capture_refused(gol, rccl, monkeypatch, capfd):
+    """An exchange is never enqueued on a stream forked into a graph capture (an RCCL group captured that
+    way crashed librccl, docs/PERFORMANCE.md §17): GOL_GRAPH_SPLIT=1 attempts to capture split supersteps,
+    whose exchange runs on the comm stream; the guard refuses it before any RCCL call, the capture is
+    abandoned and the supersteps run eagerly, exact."""
+    monkeypatch.setenv("GOL_GRAPH_SPLIT", "1")
+    monkeypatch.setenv("GOL_GRAPH_RCCL", "1")
+    H, R = 1024, 8
+    gens = 2 * R + 3
+    got, st = _run(gol, rccl, H, gens, 5, schedule="split", kernel="temporal", subtiles=0, halo_depth=R,
+                   run_hint=gens)
+    err = capfd.readouterr().err
+    assert "capture's origin stream refused" in err, err[-2000:]
+    assert st["schedule"] == "split" and st["graph_launches"] == 0, st
+    assert np.array_equal(got, numpy_step(initial_board(5, H, 1, True, 5), gens))
