@@ -53,7 +53,14 @@ struct StepParams {
     // Where lanes that store nothing (halo / idle lanes) write instead: kTrashWaves x 64 words, one
     // word per (wave mod kTrashWaves, lane).  Filled in by the launch functions (ensure_trash).
     u64* trash = nullptr;
+    // Exchange gate (step_temporal, ghost-row sources): a wave whose segment reads ghost rows first waits
+    // until gate[0] >= gate_val (written by the comm stream, hipStreamWriteValue32, once the halo exchange
+    // is done), polling with system-scope loads and bounded by kGateWaitTicks; on timeout it sets gate[1]
+    // (the board is then invalid: the engine checks it at every readout) and proceeds.  nullptr: no gate.
+    u32* gate = nullptr;
+    u32 gate_val = 0;
 };
+constexpr unsigned long long kGateWaitTicks = 200000000ull;  // 2 s of s_memrealtime (100 MHz)
 constexpr int kTrashWaves = 1024;
 // Allocate the current device's trash buffer (call once per device before any launch or capture;
 // thread safe).

@@ -119,6 +119,9 @@ HipEngine::HipEngine(const Geometry& g, const EngineConfig& c, std::shared_ptr<T
         for (auto* e : {&ev_t0_, &ev_t1_, &ev_t2_, &ev_t3_}) HIP_CHECK(hipEventCreate(e));
     }
     HIP_CHECK(hipMalloc(&d_red_, 2 * sizeof(u64)));
+    HIP_CHECK(hipMalloc(&d_gate_, 64));
+    HIP_CHECK(hipMemsetAsync(d_gate_, 0, 64, s_comp_));
+    HIP_CHECK(hipStreamSynchronize(s_comp_));
     HIP_CHECK(hipHostMalloc(&h_red_, 2 * sizeof(u64), hipHostMallocDefault));
     if (wd_)
         for (auto& m : mk_)
@@ -213,6 +216,7 @@ HipEngine::~HipEngine() {
         if (q) hipFree(q);
     for (void* p : deferred_free_) hipFree(p);
     hipFree(d_red_);
+    hipFree(d_gate_);
     hipHostFree(h_red_);
     hipEventDestroy(ev_ready_);
     hipEventDestroy(ev_halo_);
@@ -338,7 +342,7 @@ void HipEngine::do_init(const PatternSpec& p) {
         // schedule (and the forced-split measurement mode).  The full schedule
         // exchanges on the compute stream itself: recording the event there every superstep
         // only idles the GPU (~15 us per record, a release fence).
-        events_needed_ = cfg_.force_split || (split_ && !halo_items(L_.R).empty());
+        events_needed_ = cfg_.force_split || ((split_ || gate_) && !halo_items(L_.R).empty());
     }
     stats_.kernel = split_ ? kern_[1] + "+boundary:" + kern_[2] : (dual_ ? std::string("temporal") : kern_[0]);
     if (!split_ && !dual_ && kern_[0] == "pipe")
@@ -347,7 +351,7 @@ void HipEngine::do_init(const PatternSpec& p) {
         const ResPlan& rp = res_plan(res_kin_);
         stats_.kernel = strprintf("resident@%d(%lld tiles x %d waves x %d rows)", res_kin_, (long long)rp.tiles, rp.nw, rp.B);
     }
-    stats_.schedule = split_ ? "split" : (halo_items(L_.R).empty() ? "local" : "full");
+    stats_.schedule = split_ ? "split" : (halo_items(L_.R).empty() ? "local" : (gate_ ? "full+gate" : "full"));
     if (dual_) stats_.schedule += sub_overlap_ ? "+subtiles2ov" : "+subtiles2";
     stats_.kernel_depth = dual_ ? tdepth_ : kdepth_;
     stats_.tile_waves = cfg_.tile_waves;
@@ -512,6 +516,18 @@ void HipEngine::first_pass(int kx, int kp, i64 e, bool split) {
         launch(2, kp, e, src, dst, s_comp_);
         post(dst, s_comp_, e);
         if (prof) record_profile(true);
+    } else if (gate_ && device_transport_ && pass_kernel(0, kp) == PK_TEMPORAL) {
+        // full+gate: the exchange on the comm stream (after the previous superstep's passes, which wrote what it
+        // sends), then the flag; the whole first pass on the compute stream at once, its ghost-row segments
+        // waiting for the flag inside the kernel.  The comm stream is never waited for by the compute stream:
+        // the first pass cannot complete before the exchange, and everything after it is stream-ordered.
+        const u32 seq = ++gate_seq_;
+        if (gate_order_ == 1) launch(0, kp, e, src, dst, s_comp_, 0, seq);
+        wait_pending(s_comm_, ev_ready_);
+        exchange_device(kx, items, cur_, s_comm_);
+        HIP_CHECK(hipStreamWriteValue32(s_comm_, d_gate_, seq, 0));
+        if (gate_order_ != 1) launch(0, kp, e, src, dst, s_comp_, 0, seq);
+        post(dst, s_comp_, e);
     } else {
         if (prof) HIP_CHECK(hipEventRecord(ev_t0_, s_comp_));
         if (device_transport_)
@@ -543,7 +559,7 @@ void HipEngine::do_set_compat_halos(const std::vector<u64>& above, const std::ve
     synchronize();
 }
 
-void HipEngine::launch(int kind, int k, i64 e, const u64* src, u64* dst, hipStream_t s, u32 xflags) {
+void HipEngine::launch(int kind, int k, i64 e, const u64* src, u64* dst, hipStream_t s, u32 xflags, u32 gate_val) {
     if (kernel_ == "lds") {
         // full-row bands only (the LDS variant is never split by columns: can_overlap)
         for (const Region& r : regions(kind, 1))
@@ -553,6 +569,12 @@ void HipEngine::launch(int kind, int k, i64 e, const u64* src, u64* dst, hipStre
         if (p.st.out_words == 0) return;
         hipk::StepParams sp{L_.pitch, (i32)L_.h, (i32)L_.nw, L_.R, step_flags() | p.tflags | xflags};
         const PassKernel pk = pass_kernel(kind, k);
+        if (gate_val) {
+            if (pk != PK_TEMPORAL) throw Error("full+gate: a gated pass must run step_temporal");
+            sp.gate = d_gate_;
+            sp.gate_val = gate_val;
+            gate_used_ = true;
+        }
         if (pk == PK_TILE) {
             hipk::launch_step_tile(cfg_.tile_waves, k, src, dst, p.d, p.waves, p.rows, sp, s);
         } else if (pk == PK_PIPE) {

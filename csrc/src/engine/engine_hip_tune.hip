@@ -61,11 +61,16 @@ void HipEngine::measure_pass_costs() {
     // geometries reaches (and the superstep allows), so a superstep is cut into the cheapest mix, e.g.
     // the driver's 20-generation run on config 3's 4096 x 32768 strip as ONE step_pipe pass of 20
     // (10 stages x 2) instead of three step_temporal passes of 7 + 7 + 6.
+    // (Round 6: also one generation per stage, and two workgroups per CU -- twice the waves per SIMD to hide
+    // the stage chain's latency, with rings of nw <= 9 waves, whose LDS fits twice in a CU's 160 KiB.)
     if (!dual_ && kern_[0] == "pipe" && pipe_k_ > 0) {
         std::vector<PipeGeo> gs = {pipe_cur_};
-        for (int l : {2, 3})
+        for (int l : {1, 2, 3})
             for (int nw : {5, 7, 9, 11, 13, 16})
                 if (!(l == 3 && (nw == 11 || nw == 16))) gs.push_back({nw, l, 1});
+        for (int l : {1, 2, 3})
+            for (int nw : {5, 7, 9})
+                if (2 * hipk::pipe_lds_bytes(nw) <= 160 * 1024) gs.push_back({nw, l, 2});
         for (const PipeGeo& g : gs) {
             const int d = (g.nw - 1) * g.l;
             if (d > superstep_depth() || !hipk::pipe_supported(g.nw, g.l)) continue;
@@ -168,9 +173,12 @@ void HipEngine::choose_schedule() {
         if (nbrs && device_transport_ && t_->graph_capturable() && cfg_.graph && !cfg_.profile && !cfg_.compat &&
             cfg_.graph_rccl < 0)
             cands.push_back("full+graph");
+        // the one-tile superstep whose first pass starts at once, its ghost-row segments gated on the exchange's flag
+        if (nbrs && cfg_.sched == "auto" && gate_eligible() && env_int("GOL_GATE", -1) != 0) cands.push_back("full+gate");
     }
+    if (cfg_.sched == "gate" && nbrs && gate_eligible()) cands = {"full+gate"};
     graph_rccl_on_ = cfg_.graph_rccl == 1;
-    bool dual_ok = cfg_.subtiles != 0 && cands[0] != "split" && dual_wanted();
+    bool dual_ok = cfg_.subtiles != 0 && cands[0] != "split" && cfg_.sched != "gate" && dual_wanted();
     if (dual_ok) {
         double ok = dual_local_ok() ? 1.0 : 0.0;
         if (t_->size() > 1) ok = t_->allreduce_min(ok);
@@ -239,6 +247,7 @@ void HipEngine::choose_schedule() {
     destroy_sched_graphs();  // (they captured the communicator: destroy them before the comm can go)
     sched_pick_ = pick;
     split_ = pick == "split";
+    gate_ = pick == "full+gate";
     dual_ = pick.rfind("subtiles", 0) == 0;
     sub_overlap_ = pick == "subtiles+ov" ? 1 : 0;
     graph_rccl_on_ = cfg_.graph_rccl == 1 || pick == "full+graph";
@@ -409,8 +418,9 @@ void HipEngine::time_schedule(const std::string& c, int k, int reps, bool eager)
             time_schedule(base, k, reps, true);  // the same exchanges as the peers' replays
         return;
     }
-    const bool split0 = split_;
+    const bool split0 = split_, gate0 = gate_;
     split_ = c == "split";
+    gate_ = c == "full+gate";
     const std::vector<int>& ps = pass_depths(k);
     for (int i = 0; i < reps; ++i) {
         first_pass(k, ps[0], ext_after(ps, 0), split_);
@@ -426,6 +436,7 @@ void HipEngine::time_schedule(const std::string& c, int k, int reps, bool eager)
         if (ps.size() > 1) mark_ready();
     }
     split_ = split0;
+    gate_ = gate0;
 }
 
 // The kernels of a split superstep's first pass at depth k: the interior (kind 1) and the bands next to

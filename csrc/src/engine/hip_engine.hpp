@@ -455,7 +455,8 @@ class HipEngine : public Engine {
 
     const DevPlan& plan(int kind, int k, i64 e = 0);
 
-    void launch(int kind, int k, i64 e, const u64* src, u64* dst, hipStream_t s, u32 xflags = 0);
+    // gate_val != 0: the exchange gate of a full+gate first pass (StepParams::gate)
+    void launch(int kind, int k, i64 e, const u64* src, u64* dst, hipStream_t s, u32 xflags = 0, u32 gate_val = 0);
 
     // Ghost words for widths that are not a multiple of 64 when the tile is its own E/W neighbour.
     void post(u64* buf, hipStream_t s, i64 rem = 0) {
@@ -595,6 +596,26 @@ class HipEngine : public Engine {
     bool multipass_ = false;
     std::map<int, std::vector<int>> passes_;
     bool split_ = false;   // superstep schedule: interior/boundary split with overlapped exchange
+    // full+gate (round 6): the exchange on the comm stream followed by a device flag (hipStreamWriteValue32
+    // of a per-superstep sequence number), the whole first pass on the compute stream at once; only its
+    // segments that read ghost rows wait for the flag, in the kernel (StepParams::gate) -- no cross-queue
+    // event, no interior / band split.  1-D one tile, aligned width, step_temporal first pass.
+    bool gate_ = false;
+    bool gate_used_ = false;  // some pass ran gated (its fault word is checked at readout)
+    u32* d_gate_ = nullptr;   // [0] the flag (the last exchanged sequence number), [1] the fault word
+    u32 gate_seq_ = 0;
+    const int gate_order_ = (int)env_int("GOL_GATE_ORDER", 0);  // 0: exchange enqueued first; 1: the pass first
+    // The compute and comm streams must sit on different hardware queues: a flag write queued behind its
+    // own gated kernel on a shared queue would wait for it (until the wait's bound faults the pass).  One
+    // engine per GPU guarantees that (the two streams' priorities differ: profiles/queue_probe.txt), i.e. an
+    // RCCL transport (RCCL refuses two ranks on one GPU).  Thread ranks sharing a GPU create two streams
+    // each, more than GPU_MAX_HW_QUEUES (4) can separate: only with GOL_GATE=1, for tests run with enough
+    // hardware queues (tests/test_gpu_gate.py: GPU_MAX_HW_QUEUES=32, P = 8).
+    bool gate_eligible() const {
+        const bool queues_ok = t_->name().rfind("rccl", 0) == 0 || env_int("GOL_GATE", -1) == 1;
+        return device_transport_ && queues_ok && !two_d() && L_.aligned() && !cfg_.compat && !cfg_.profile &&
+               !cfg_.force_split && kernel_ != "lds";
+    }
     bool halo_pending_ = false;  // split: the last superstep's bands on the comm stream are not joined (join_halo)
     std::map<std::string, double> sched_us_;  // choose_schedule: us per generation per candidate
     // measure_pass_costs: us per pass by depth, [0] one tile (kind-0 passes), [1] the two sub-tiles

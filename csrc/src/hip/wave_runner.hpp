@@ -48,6 +48,26 @@ constexpr bool pingpong_loop() {
     return K < 32 && (((kPingpongMask >> K) & 1) != 0 || (ROWS == 0 && ((kPingpongGhostMask >> K) & 1) != 0));
 }
 
+// The exchange gate (StepParams::gate): poll the comm stream's flag with system-scope loads (it is written
+// by another queue's packet processor, not by a wave), bounded; then an agent-scope acquire, so this CU's
+// L1 holds no line of the ghost rows older than the exchange.  Wave-uniform.
+__device__ __forceinline__ void gate_wait(u32* gate, u32 val) {
+    u64 t0 = 0;
+    for (int spin = 0;; ++spin) {
+        const u32 v = __builtin_amdgcn_readfirstlane(__hip_atomic_load(gate, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
+        if ((int)(v - val) >= 0) break;
+        if (spin == 0) t0 = __builtin_amdgcn_s_memrealtime();
+        const u32 fault = __builtin_amdgcn_readfirstlane(__hip_atomic_load(gate + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+        if (__builtin_amdgcn_s_memrealtime() - t0 > kGateWaitTicks || fault != 0) {
+            __hip_atomic_store(gate + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // (all lanes, one word)
+            break;
+        }
+        __builtin_amdgcn_s_sleep(4);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
 template <int K, int ROWS>
 struct WaveRunner {
     static constexpr int D = prefetch_rows<K>();
@@ -99,6 +119,11 @@ struct WaveRunner {
         st = out ? reinterpret_cast<uint2*>(dst + (i64)(d.row0 + p.R) * p.pitch + (d.col + 1))
                  : reinterpret_cast<uint2*>(p.trash + ((i64)(wave_id & (kTrashWaves - 1)) * 64 + (threadIdx.x & 63)));
         st_stride = out ? p.pitch : 0;
+        if (ROWS == ROWS_GHOST && p.gate) {
+            // a segment whose input rows include ghost rows waits for the exchange before its first load
+            const bool ghost = d.row0 - K < 0 || d.row0 + nrows + K > p.h;
+            if (__builtin_amdgcn_ballot_w64(ghost) != 0) gate_wait(p.gate, p.gate_val);
+        }
 #pragma unroll
         for (int j = 0; j < D; ++j) {
             ROW_LOAD_INTO(pf[j]);
@@ -126,7 +151,7 @@ struct WaveRunner {
 
     template <int PH, bool GUARD>
     __device__ __forceinline__ void compute_store(u32 lo, u32 hi, int i) {
-        if (!advance<K, PH, GUARD>(P, lo, hi, i)) return;
+        if (!advance<K, PH, GUARD, false>(P, lo, hi, i)) return;  // (rule32: stencil_device.hpp, PAIR)
         *st = make_uint2(lo, hi);
         st += st_stride;
     }

@@ -7,6 +7,10 @@
 //                  a kernel on s0, EndCapture, instantiate, launch x3, check the received bytes.
 //   mode origin    the same group on s0 itself (what the engine's full+graph captures), the kernel on s1.
 //   mode eager     no capture: the group on s1 (sanity check of the communicator).
+//   mode unjoined  as fork, but s1 is never joined back to s0 before EndCapture (which must fail), then
+//                  the communicator is used eagerly and destroyed.
+//   mode query     as fork, with a hipEventQuery of the event recorded inside the capture before the
+//                  fork (what the engine's wait_pending() does before a cross-stream wait).
 //   suffix "+reg"  both buffers registered with the communicator (ncclCommRegister), as the engine
 //                  registers its boards for a one-rank communicator.
 // Every step prints a line (stderr, unbuffered) before it runs; SIGSEGV / SIGABRT print the host
@@ -118,7 +122,28 @@ int main(int argc, char** argv) {
         step("hipStreamBeginCapture(s0)");
         CK(hipStreamBeginCapture(s0, hipStreamCaptureModeRelaxed));
         CK(hipEventRecord(e0, s0));
-        if (mode == "fork") {
+        if (mode == "query") {
+            step("hipEventQuery(e0) inside the capture");
+            const hipError_t q = hipEventQuery(e0);
+            fprintf(stderr, "hipEventQuery -> %s\n", hipGetErrorString(q));
+            hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+            (void)hipStreamIsCapturing(s0, &cs);
+            fprintf(stderr, "capture status after the query: %d\n", (int)cs);
+        }
+        if (mode == "unjoined") {
+            CK(hipStreamWaitEvent(s1, e0, 0));
+            group(s1);
+            step("hipStreamEndCapture (s1 unjoined)");
+            hipGraph_t g2 = nullptr;
+            const hipError_t ec = hipStreamEndCapture(s0, &g2);
+            fprintf(stderr, "hipStreamEndCapture -> %s, graph %p\n", hipGetErrorString(ec), (void*)g2);
+            if (g2) (void)hipGraphDestroy(g2);
+            (void)hipGetLastError();
+            step("eager group on s1 after the failed capture");
+            group(s1);
+            CK(hipStreamSynchronize(s1));
+            CK(hipStreamSynchronize(s0));
+        } else if (mode == "fork" || mode == "query") {
             step("s1 waits e0 (fork)");
             CK(hipStreamWaitEvent(s1, e0, 0));
             hipLaunchKernelGGL(touch, dim3(1), dim3(64), 0, s0, ctr);
@@ -133,21 +158,23 @@ int main(int argc, char** argv) {
             CK(hipEventRecord(e1, s1));
             CK(hipStreamWaitEvent(s0, e1, 0));
         }
-        step("hipStreamEndCapture");
-        CK(hipStreamEndCapture(s0, &g));
-        size_t nn = 0;
-        CK(hipGraphGetNodes(g, nullptr, &nn));
-        fprintf(stderr, "captured graph: %zu nodes\n", nn);
-        step("hipGraphInstantiate");
-        CK(hipGraphInstantiate(&ex, g, nullptr, nullptr, 0));
-        for (int r = 0; r < 3; ++r) {
-            step("hipGraphLaunch");
-            CK(hipGraphLaunch(ex, s0));
+        if (mode != "unjoined") {
+            step("hipStreamEndCapture");
+            CK(hipStreamEndCapture(s0, &g));
+            size_t nn = 0;
+            CK(hipGraphGetNodes(g, nullptr, &nn));
+            fprintf(stderr, "captured graph: %zu nodes\n", nn);
+            step("hipGraphInstantiate");
+            CK(hipGraphInstantiate(&ex, g, nullptr, nullptr, 0));
+            for (int r = 0; r < 3; ++r) {
+                step("hipGraphLaunch");
+                CK(hipGraphLaunch(ex, s0));
+            }
+            step("hipStreamSynchronize");
+            CK(hipStreamSynchronize(s0));
+            CK(hipGraphExecDestroy(ex));
+            CK(hipGraphDestroy(g));
         }
-        step("hipStreamSynchronize");
-        CK(hipStreamSynchronize(s0));
-        CK(hipGraphExecDestroy(ex));
-        CK(hipGraphDestroy(g));
     }
     std::vector<unsigned long long> got(words);
     CK(hipMemcpy(got.data(), rb, words * 8, hipMemcpyDeviceToHost));

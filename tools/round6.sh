@@ -32,6 +32,42 @@ b1)
     fatal $rc && break
   done
   ;;
+b2)
+  # the pair-shared rule (stencil_device.hpp): the whole GPU suite, a kbench A/B of the old rule (r0) against
+  # the pair rule (r1) interleaved, the driver's bench and the per-rank tiles, then two more capture probes
+  timeout -k 10 900 python -u -m pytest tests -x -q -m gpu --timeout 120 --timeout-method thread > $O/pytest_gpu.log 2>&1; rc=$?
+  echo "== pytest -m gpu rc=$rc: $(tail -1 $O/pytest_gpu.log)" >> $S; [ $rc -ne 0 ] && exit $rc
+  kb() {  # kb <label> <env...> -- <args...>
+    local lab=$1; shift; local envs=(); while [ "$1" != "--" ]; do envs+=("$1"); shift; done; shift
+    for v in r0 r1; do
+      r=$(env "${envs[@]}" timeout -k 5 90 build/kbench_$v "$@" 2>&1 | tail -1); rc=$?
+      echo "[kb $lab $v] $(echo "$r" | grep -o '"us_per_gen": [0-9.]*')" >> $S
+      fatal $rc && exit $rc
+    done
+  }
+  for round in 1 2 3; do
+    kb T8 -- 32768 8 1920
+    kb H8 KB_SPLIT2=1 KB_BPC=2 -- 32768 8 1920
+    kb H12 KB_SPLIT2=1 KB_BPC=1 -- 32768 12 1920
+    kb F32 KB_FOLD=1 -- 8192 32 1920 0 0 8 0 4
+    kb P20 KB_W=32768 KB_PIPE=2 -- 4096 20 1920 0 0 11
+    kb P24 KB_PIPE=3 KB_PIPE_WG=2 -- 32768 24 1920 0 0 9
+  done
+  reps 3 "" || exit 1
+  reps 1 "--self-exchange" "--size 4096 --width 32768 --self-exchange" "--size 8192 --steps 1000" || exit 1
+  for m in query unjoined; do
+    timeout -k 10 120 build/rccl_capture_probe $m > $O/capture_$m.log 2>&1; rc=$?
+    echo "== rccl_capture_probe $m rc=$rc: $(tail -1 $O/capture_$m.log)" >> $S
+    fatal $rc && break
+  done
+  ;;
+b3)
+  # full+gate (exchange flag gating the first pass's ghost-row segments), the pair rule in tile/pipe only, the
+  # widened step_pipe pass-cost candidates: tests, then the driver's cut on the weak-scaling rank and the strip
+  pyt gate_tests.log tests/test_gpu_rccl.py tests/test_gpu_gate_p8.py tests/test_gpu_multirank_p8.py tests/test_gpu_pipe.py || exit 1
+  reps 3 "" "--self-exchange" "GOL_SCHEDULE=gate --self-exchange" "GOL_SCHEDULE=gate GOL_GATE_ORDER=1 --self-exchange" "--size 4096 --width 32768 --self-exchange" || exit 1
+  reps 1 "--size 8192 --steps 1000" "--size 32768 --width 16384 --decomp 2d --self-exchange" || exit 1
+  ;;
 *) echo "unknown batch $B"; exit 2 ;;
 esac
 cat $S
