@@ -18,6 +18,8 @@
 
 #include <hip/hip_runtime.h>
 
+#include <vector>
+
 #include "gol/geometry.hpp"
 #include "gol/plan.hpp"
 
@@ -32,6 +34,7 @@ enum : u32 {
     STEP_TILE_L4 = 1u << 6, // tile kernel: four generations per LDS pass
     STEP_TILE_INPLACE = 1u << 7,  // tile kernel: one tile buffer updated in place (twice the rows)
     STEP_TILE_FOLD = 1u << 8,     // tile kernel: 32-lane tiles folded in half (fold plans, plan.hpp)
+    STEP_GATE = 1u << 9,    // temporal kernel: the full+gate first pass (StepParams::gate; launch_step sets it)
     STEP_SEAM = 1u << 5,    // temporal kernel: rows < 0 are read from StepParams::above, rows >= h
                             // from StepParams::below (sub-tile first pass: the other half's edges)
 };
@@ -54,7 +57,7 @@ struct StepParams {
     // word per (wave mod kTrashWaves, lane).  Filled in by the launch functions (ensure_trash).
     u64* trash = nullptr;
     // Exchange gate (step_temporal, ghost-row sources): a wave whose segment reads ghost rows first waits
-    // until gate[0] >= gate_val (written by the comm stream, hipStreamWriteValue32, once the halo exchange
+    // until gate[0] == gate_val (written by the comm stream, hipStreamWriteValue32, once the halo exchange
     // is done), polling with system-scope loads and bounded by kGateWaitTicks; on timeout it sets gate[1]
     // (the board is then invalid: the engine checks it at every readout) and proceeds.  nullptr: no gate.
     u32* gate = nullptr;
@@ -111,6 +114,10 @@ bool pipe_supported(int nw, int L);
 int pipe_blocks_per_cu(int nw, int L, bool wrapy);
 // True (and cleared) when a step_pipe wait timed out since the last call: the board is invalid.
 bool pipe_fault();
+#ifdef GOL_PIPE_STAMPS
+// Diagnostic build: per-wave wait stamps of the last step_pipe launch (pipe_kernel.hip g_pipe_stamps)
+std::vector<u64> pipe_stamps(size_t waves);
+#endif
 void launch_step_pipe(int nw, int L, const u64* src, u64* dst, const LaneDesc* plan, i64 n_tiles, const StepParams& p,
                       hipStream_t s);
 // Single-generation LDS-tiled kernel over output rows [r0, r1) (all words).

@@ -174,7 +174,9 @@ void HipEngine::choose_schedule() {
             cfg_.graph_rccl < 0)
             cands.push_back("full+graph");
         // the one-tile superstep whose first pass starts at once, its ghost-row segments gated on the exchange's flag
-        if (nbrs && cfg_.sched == "auto" && gate_eligible() && env_int("GOL_GATE", -1) != 0) cands.push_back("full+gate");
+        // (not when GOL_GRAPH_RCCL=1 asks for captured RCCL supersteps: gated supersteps run eagerly)
+        if (nbrs && cfg_.sched == "auto" && gate_eligible() && env_int("GOL_GATE", -1) != 0 && cfg_.graph_rccl != 1)
+            cands.push_back("full+gate");
     }
     if (cfg_.sched == "gate" && nbrs && gate_eligible()) cands = {"full+gate"};
     graph_rccl_on_ = cfg_.graph_rccl == 1;
@@ -423,6 +425,10 @@ void HipEngine::time_schedule(const std::string& c, int k, int reps, bool eager)
     gate_ = c == "full+gate";
     const std::vector<int>& ps = pass_depths(k);
     for (int i = 0; i < reps; ++i) {
+        if (gate_ && device_transport_) {  // (its passes replay from captured graphs, on scratch state)
+            gate_superstep(k, true);
+            continue;
+        }
         first_pass(k, ps[0], ext_after(ps, 0), split_);
         for (size_t j = 1; j < ps.size(); ++j) {
             const i64 e = ext_after(ps, j);

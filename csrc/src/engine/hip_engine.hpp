@@ -599,12 +599,16 @@ class HipEngine : public Engine {
     // full+gate (round 6): the exchange on the comm stream followed by a device flag (hipStreamWriteValue32
     // of a per-superstep sequence number), the whole first pass on the compute stream at once; only its
     // segments that read ghost rows wait for the flag, in the kernel (StepParams::gate) -- no cross-queue
-    // event, no interior / band split.  1-D one tile, aligned width, step_temporal first pass.
+    // event, no interior / band split.  1-D one tile, aligned width; any pass kernel (step_temporal's waves,
+    // step_pipe's loader and the tile kernels' staging waves wait).
     bool gate_ = false;
     bool gate_used_ = false;  // some pass ran gated (its fault word is checked at readout)
     u32* d_gate_ = nullptr;   // [0] the flag (the last exchanged sequence number), [1] the fault word
-    u32 gate_seq_ = 0;
-    const int gate_order_ = (int)env_int("GOL_GATE_ORDER", 0);  // 0: exchange enqueued first; 1: the pass first
+    u32 gate_phase_ = 1;      // the flag value of the next gated superstep (1 and 2 alternate)
+    std::map<i64, hipGraphExec_t> gate_graphs_;  // (k, parity, flag value) -> the superstep's captured passes
+    void gate_superstep(int k, bool scratch = false);
+    void gate_passes(int k, u32 v, bool scratch);
+    hipGraphExec_t gate_graph(int k, u32 v, bool scratch = false);
     // The compute and comm streams must sit on different hardware queues: a flag write queued behind its
     // own gated kernel on a shared queue would wait for it (until the wait's bound faults the pass).  One
     // engine per GPU guarantees that (the two streams' priorities differ: profiles/queue_probe.txt), i.e. an
@@ -628,7 +632,9 @@ class HipEngine : public Engine {
     unsigned long long mk_done_ = 0;  // markers retired so far
     std::mutex mk_mu_;
     bool mk_published_ = false;  // this superstep's marker is already published (sub-tile path)
-    u64* buf_[2] = {nullptr, nullptr};
+    u64* buf_[2] = {nullptr, nullptr};      // row -R of each board (inside its allocation, buf_raw_)
+    u64* buf_raw_[2] = {nullptr, nullptr};  // the allocations: kSlackBefore rows, the board, kSlackRows rows
+    static constexpr int kSlackBefore = 8;
     size_t alloc_bytes_ = 0;
     int cur_ = 0;
     hipStream_t s_comp_ = nullptr, s_comm_ = nullptr;

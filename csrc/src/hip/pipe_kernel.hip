@@ -32,6 +32,7 @@
 #include <set>
 #include <type_traits>
 #include <utility>
+#include <vector>
 
 #include "gol/hip_kernels.hpp"
 #include "stencil_device.hpp"
@@ -85,15 +86,32 @@ __device__ __forceinline__ void ctr_store(u32* c, u32 v) {
 
 // Set when a wait gave up (pipe_fault()): the board is invalid then, but every wave still drains.
 __device__ u32 g_pipe_fault;
+
+#ifdef GOL_PIPE_STAMPS
+// Diagnostic build (tools/kbench.cpp KB_PIPE_STAMPS=1, build flag -DGOL_PIPE_STAMPS): per wave, s_memtime
+// cycles of its role [0], spent in its input waits [1] (compute stages: the producer's counter; the loader:
+// s_waitcnt vmcnt for its DMAs), in its output waits [2] (the consumer's counter; the loader: a free ring
+// slot), and the number of waits that found the counter short [3].
+constexpr int kPipeStampWaves = 1 << 16;
+__device__ u64 g_pipe_stamps[kPipeStampWaves * 4];
+#define PIPE_STAMPS 1
+#else
+#define PIPE_STAMPS 0
+#endif
+struct WaitAcc {  // (PIPE_STAMPS only: cycles waited, waits entered)
+    u64 cy = 0, n = 0;
+};
 constexpr u64 kPipeWaitTicks = 200000000ull;  // 2 s of s_memrealtime (100 MHz): no real wait is that long
 
 // wait until *c >= need (the cached value first: counters only grow).  Bounded: after 2 s (or once
 // any wave of the device has given up) the wait returns as if satisfied and records the fault, so a
 // broken pipeline cannot hang the GPU.
 template <bool ASM = false>
-__device__ __forceinline__ void ctr_wait(const u32* c, u32& cached, u32 need) {
+__device__ __forceinline__ void ctr_wait(const u32* c, u32& cached, u32 need, WaitAcc* acc = nullptr) {
     if (cached < need) {
+        const u64 s0 = PIPE_STAMPS && acc ? __builtin_amdgcn_s_memtime() : 0;
         cached = ctr_load<ASM>(c);
+        if (PIPE_STAMPS && acc && cached < need) acc->n += 1;
         if (cached < need) {
             const u64 t0 = __builtin_amdgcn_s_memrealtime();
             for (;;) {
@@ -108,6 +126,7 @@ __device__ __forceinline__ void ctr_wait(const u32* c, u32& cached, u32 need) {
                 }
             }
         }
+        if (PIPE_STAMPS && acc) acc->cy += __builtin_amdgcn_s_memtime() - s0;
     }
     asm volatile("" ::: "memory");  // ring accesses stay after the wait
 }
@@ -119,7 +138,7 @@ __device__ __forceinline__ void ctr_wait(const u32* c, u32& cached, u32 need) {
 // slack rows or the wrap keep them in bounds) and are never published.
 template <bool WRAPY>
 __device__ __forceinline__ void loader(const u64* src, const LaneDesc& d, const StepParams& p, int K, int n, u32* ring,
-                                       u32* prod, const u32* cons) {
+                                       u32* prod, const u32* cons, WaitAcc* acc_in = nullptr, WaitAcc* acc_out = nullptr) {
     int lrow = d.row0 - K;
     if (WRAPY && lrow < 0) lrow += p.h;
     const u32* g = reinterpret_cast<const u32*>(src + (i64)(lrow + p.R) * p.pitch + (d.col + 1));
@@ -127,7 +146,7 @@ __device__ __forceinline__ void loader(const u64* src, const LaneDesc& d, const 
     u32 freed = 0;
     int slot = 0;
     auto issue = [&](int j) {
-        if (j >= kPipeRing0) ctr_wait<true>(cons, freed, (u32)(j + 1 - kPipeRing0));  // slot j % ring free
+        if (j >= kPipeRing0) ctr_wait<true>(cons, freed, (u32)(j + 1 - kPipeRing0), acc_out);  // slot j % ring free
         u32* l = ring + slot * kRowU32;
         __builtin_amdgcn_global_load_lds((glb_void_t*)g, (lds_void_t*)l, 4, 0, 0);
         __builtin_amdgcn_global_load_lds((glb_void_t*)(g + 1), (lds_void_t*)(l + 64), 4, 0, 0);
@@ -143,7 +162,9 @@ __device__ __forceinline__ void loader(const u64* src, const LaneDesc& d, const 
     for (int j = 0; j < kPipeLoadAhead; ++j) issue(j);
     int i = 0;
     for (; i + kPipeLoadAhead < n; ++i) {
+        const u64 s0 = PIPE_STAMPS && acc_in ? __builtin_amdgcn_s_memtime() : 0;
         asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * (kPipeLoadAhead - 1)) : "memory");
+        if (PIPE_STAMPS && acc_in) acc_in->cy += __builtin_amdgcn_s_memtime() - s0;
         ctr_store<true>(prod, (u32)(i + 1));
         issue(i + kPipeLoadAhead);
     }
@@ -171,11 +192,12 @@ struct RingIn {
     u32* cons;        // rows this wave has consumed (their slots are free)
     u32 avail = 0;    // cached *prod
     u32 pv = 0;       // an early read of *prod (peek), used by the next ensure
+    WaitAcc acc;      // (PIPE_STAMPS)
     __device__ __forceinline__ void peek() { pv = __hip_atomic_load(prod, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); }
     // rows < need are published (the peeked value first, then a bounded wait)
     __device__ __forceinline__ void ensure(u32 need, bool peeked = false) {
         if (peeked) avail = max(avail, (u32)__builtin_amdgcn_readfirstlane(pv));
-        ctr_wait(prod, avail, need);
+        ctr_wait(prod, avail, need, PIPE_STAMPS ? &acc : nullptr);
     }
     template <int SLOT>
     __device__ __forceinline__ uint2 read() const {
@@ -193,12 +215,13 @@ struct RingOut {
     const u32* cons;  // the consumer's progress
     u32 freed = 0;    // cached *cons
     u32 cv = 0;       // an early read of *cons
+    WaitAcc acc;      // (PIPE_STAMPS)
     __device__ __forceinline__ void peek() { cv = __hip_atomic_load(cons, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); }
     // slots of rows < end are free (rows < end - kSlots consumed)
     __device__ __forceinline__ void reserve(u32 end, bool peeked = false) {
         if (end <= (u32)kSlots) return;
         if (peeked) freed = max(freed, (u32)__builtin_amdgcn_readfirstlane(cv));
-        ctr_wait(cons, freed, end - kSlots);
+        ctr_wait(cons, freed, end - kSlots, PIPE_STAMPS ? &acc : nullptr);
     }
     template <int SLOT>
     __device__ __forceinline__ void put(u32 lo, u32 hi) {
@@ -210,6 +233,7 @@ struct RingOut {
 
 struct GlobalOut {
     static constexpr int kSlots = 1;
+    WaitAcc acc;  // (never waits)
     uint2* st;
     i64 stride;  // pitch, or 0 for halo/idle lanes (their own trash word)
     __device__ __forceinline__ void peek() {}
@@ -340,8 +364,28 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(5))) vo
     u32* ctr = pipe_lds + (kPipeRing0 + (NW - 2) * kPipeRing) * kRowU32;
     if (threadIdx.x < 2 * NW) ctr[threadIdx.x] = 0;
     __syncthreads();
+#if PIPE_STAMPS
+    const u64 t_start = __builtin_amdgcn_s_memtime();
+    auto stamp = [&](const WaitAcc& a, const WaitAcc& b) {
+        const i64 slot = ((i64)blockIdx.x * NW + wv) * 4;
+        if (lane == 0 && slot + 3 < (i64)kPipeStampWaves * 4) {
+            g_pipe_stamps[slot] = __builtin_amdgcn_s_memtime() - t_start;
+            g_pipe_stamps[slot + 1] = a.cy;
+            g_pipe_stamps[slot + 2] = b.cy;
+            g_pipe_stamps[slot + 3] = a.n + b.n;
+        }
+    };
+#endif
     if (wv == 0) {
+        // (the exchange gate: only the loader reads the source buffer)
+        if (!WRAPY && p.gate && reads_ghost_rows(d.row0, nrows, K, p.h)) gate_wait(p.gate, p.gate_val);
+#if PIPE_STAMPS
+        WaitAcc ai, ao;
+        loader<WRAPY>(src, d, p, K, nrows + 2 * K, ring_of(0), ctr, ctr + NW, &ai, &ao);
+        stamp(ai, ao);
+#else
         loader<WRAPY>(src, d, p, K, nrows + 2 * K, ring_of(0), ctr, ctr + NW);
+#endif
         return;
     }
     const int st = wv - 1;                     // compute stage
@@ -357,12 +401,18 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(5))) vo
                             : reinterpret_cast<uint2*>(p.trash + ((i64)((blockIdx.x * NW + wv) & (kTrashWaves - 1)) * 64 + lane));
             o.stride = out_lane ? p.pitch : 0;
             stage<L>(in, o, n);
+#if PIPE_STAMPS
+            stamp(in.acc, o.acc);
+#endif
         } else {
             RingOut o;
             o.ring = ring_of(wv) + lane;
             o.prod = ctr + wv;
             o.cons = ctr + NW + wv;
             stage<L>(in, o, n);
+#if PIPE_STAMPS
+            stamp(in.acc, o.acc);
+#endif
         }
     };
     if (st == 0)
@@ -416,6 +466,15 @@ const void* pipe_kernel_checked(int nw, int L, bool wrapy) {
 }
 
 }  // namespace
+
+#ifdef GOL_PIPE_STAMPS
+std::vector<u64> pipe_stamps(size_t waves) {
+    std::vector<u64> v(std::min<size_t>(waves, (size_t)kPipeStampWaves) * 4);
+    if (hipMemcpyFromSymbol(v.data(), HIP_SYMBOL(g_pipe_stamps), v.size() * sizeof(u64)) != hipSuccess)
+        throw Error("step_pipe: cannot read the stamps");
+    return v;
+}
+#endif
 
 bool pipe_fault() {
     u32 v = 0, z = 0;

@@ -164,16 +164,16 @@ def test_rccl_split_capture_refused(gol, rccl, monkeypatch, capfd):
     assert np.array_equal(got, numpy_step(initial_board(5, H, 1, True, 5), gens))
 
 
-@pytest.mark.parametrize("order", ["0", "1"])
+@pytest.mark.parametrize("graph", [True, False])
 @pytest.mark.parametrize("R,gens,hint", [(8, 3 * 8 + 5, 0), (32, 2 * 32 + 9, 0), (128, 25, 20)])
-def test_rccl_self_gate(gol, rccl, monkeypatch, order, R, gens, hint):
-    """full+gate: the exchange on the comm stream ends with a device flag, the whole first pass is launched at
-    once and only its segments that read ghost rows wait for the flag inside the kernel (no cross-queue
-    event).  Exchange enqueued first (order 0) or the pass first (order 1); several supersteps, multi-pass
-    supersteps, and the driver's 5 + 20 cut."""
-    monkeypatch.setenv("GOL_GATE_ORDER", order)
+def test_rccl_self_gate(gol, rccl, graph, R, gens, hint):
+    """full+gate: the exchange on the comm stream ends with a device flag (1 and 2 alternating per superstep),
+    the superstep's passes replay from a captured graph (or run eagerly) and only the first pass's segments
+    that read ghost rows wait for the flag, inside the kernel, before their first ghost-row load (segments
+    next to the top halo stream upwards); no cross-queue event.  Several supersteps, multi-pass supersteps,
+    and the driver's 5 + 20 cut."""
     H, W = 2048, 4096
-    kw = dict(width=W, schedule="gate", subtiles=0, halo_depth=R, kernel="temporal")
+    kw = dict(width=W, schedule="gate", subtiles=0, halo_depth=R, kernel="temporal", graph=graph)
     if hint:
         kw["run_hint"] = hint
     s = gol.Simulation(H, rccl, self_exchange=True, backend="hip", device=0, **kw).init(5, seed=R)
@@ -187,7 +187,8 @@ def test_rccl_self_gate(gol, rccl, monkeypatch, order, R, gens, hint):
         s.step(gens)
         total = gens
     got = s.board()
-    assert s.stats()["exchanges"] >= 1
+    st = s.stats()
+    assert st["exchanges"] >= 1 and (st["graph_launches"] >= 1) == graph, st
     assert np.array_equal(got, numpy_step(random_board(H, W, R), total))
 
 

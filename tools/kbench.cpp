@@ -168,6 +168,33 @@ int main(int argc, char** argv) {
         if (ms < best) best = ms;
     }
     CK(hipGetLastError());
+#ifdef GOL_PIPE_STAMPS
+    // KB_PIPE_STAMPS=1 (build with -DGOL_PIPE_STAMPS): one more step_pipe launch, then its per-wave wait stamps
+    // averaged by wave role (0 = loader, 1.. = compute stages): s_memtime cycles of the role, of its input
+    // waits (stages: the producer's counter; loader: its DMA vmcnt waits), of its output waits (the consumer's
+    // counter / a free loader slot), and waits that found the counter short, per workgroup.
+    if (pipe_l > 0 && getenv("KB_PIPE_STAMPS") && atoi(getenv("KB_PIPE_STAMPS"))) {
+        CK(hipDeviceSynchronize());
+        launch(a, b);
+        CK(hipDeviceSynchronize());
+        const std::vector<u64> v = hipk::pipe_stamps((size_t)st.waves * tile_nw);
+        const size_t nwg = v.size() / 4 / tile_nw;
+        printf("stamps: %zu workgroups x %d waves (cycles per wave, mean over workgroups)\n", nwg, tile_nw);
+        for (int w = 0; w < tile_nw; ++w) {
+            double t = 0, wi = 0, wo = 0, nn = 0;
+            size_t cnt = 0;
+            for (size_t g = 0; g < nwg; ++g) {
+                const u64* q = &v[(g * tile_nw + w) * 4];
+                if (q[0] == 0) continue;  // padding workgroup
+                t += (double)q[0], wi += (double)q[1], wo += (double)q[2], nn += (double)q[3];
+                ++cnt;
+            }
+            if (!cnt) continue;
+            printf("  wave %2d %-8s total %9.0f  in-wait %9.0f (%4.1f%%)  out-wait %9.0f (%4.1f%%)  short waits %7.1f\n", w,
+                   w == 0 ? "loader" : "stage", t / cnt, wi / cnt, 100.0 * wi / t, wo / cnt, 100.0 * wo / t, nn / cnt);
+        }
+    }
+#endif
     if (pipe_l > 0 && hipk::pipe_fault()) {
         fprintf(stderr, "step_pipe: a ring wait timed out\n");
         return 3;

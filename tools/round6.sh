@@ -68,6 +68,35 @@ b3)
   reps 3 "" "--self-exchange" "GOL_SCHEDULE=gate --self-exchange" "GOL_SCHEDULE=gate GOL_GATE_ORDER=1 --self-exchange" "--size 4096 --width 32768 --self-exchange" || exit 1
   reps 1 "--size 8192 --steps 1000" "--size 32768 --width 16384 --decomp 2d --self-exchange" || exit 1
   ;;
+b4)
+  # full+gate with upward-streaming top segments and a mid-stream gate (ROWS_GATE); BASELINE config 5 on the
+  # round-6 tree (the 2^20-row tile: its init runs predict_run's no-snapshot branch)
+  pyt gate_tests.log tests/test_gpu_rccl.py tests/test_gpu_gate_p8.py tests/test_gpu_multirank_p8.py -k "gate or p8" || exit 1
+  reps 3 "--self-exchange" "GOL_SCHEDULE=gate --self-exchange" "" || exit 1
+  reps 2 "--size 4096 --width 32768 --self-exchange" "GOL_SCHEDULE=gate --size 4096 --width 32768 --self-exchange" || exit 1
+  GOL_INIT_LOG=1 timeout -k 10 900 python3 bench.py --size 1048576 --steps 16 --warmup 8 > $O/cfg5.json 2> $O/cfg5.err; rc=$?
+  { echo "== config 5 (bench.py --size 1048576 --steps 16 --warmup 8) rc=$rc: init $(grep -c 'init' $O/cfg5.err) timed init steps, last: $(grep 'init' $O/cfg5.err | tail -1)"; grep -h '^{' $O/cfg5.json | python3 tools/bench_line.py cfg5; } >> $S
+  fatal $rc && exit $rc
+  ;;
+b5)
+  # kernel traces of the weak-scaling rank's driver cut through the RCCL self-exchange: full+gate vs full+graph
+  for v in 1 2; do
+    GOL_SCHEDULE=gate GOL_SUBTILES=0 bash tools/trace_run.sh gate$v --self-exchange > /dev/null || exit 1
+    GOL_GATE=0 GOL_SUBTILES=0 bash tools/trace_run.sh graph$v --self-exchange > /dev/null || exit 1
+  done
+  cat gpurun_out/trace_gate1.txt gpurun_out/trace_graph1.txt gpurun_out/trace_gate2.txt gpurun_out/trace_graph2.txt >> $S
+  ;;
+b6)
+  # full+gate, passes replayed from captured graphs (flag values 1/2 alternating), exchange eager on the comm stream
+  pyt gate_tests.log tests/test_gpu_rccl.py tests/test_gpu_gate_p8.py tests/test_gpu_multirank_p8.py -k "gate or p8" || exit 1
+  reps 3 "--self-exchange" "GOL_SCHEDULE=gate --self-exchange" "" || exit 1
+  reps 2 "--size 4096 --width 32768 --self-exchange" "GOL_SCHEDULE=gate --size 4096 --width 32768 --self-exchange" || exit 1
+  GOL_SCHEDULE=gate bash tools/trace_run.sh gate_graph --self-exchange > /dev/null || exit 1
+  cat gpurun_out/trace_gate_graph.txt >> $S
+  # step_pipe wait attribution (diagnostic build -DGOL_PIPE_STAMPS): 32768^2 8 x 3 at 2/CU, the strip's 10 x 2
+  { echo "== kbench_stamps 32768^2 step_pipe<9,3> 2/CU"; KB_PIPE=3 KB_PIPE_WG=2 KB_PIPE_STAMPS=1 timeout -k 5 90 build/kbench_stamps 32768 24 960 0 0 9; } >> $S 2>&1 || exit 1
+  { echo "== kbench_stamps 4096 x 32768 step_pipe<11,2> 1/CU"; KB_W=32768 KB_PIPE=2 KB_PIPE_STAMPS=1 timeout -k 5 90 build/kbench_stamps 4096 20 960 0 0 11; } >> $S 2>&1 || exit 1
+  ;;
 *) echo "unknown batch $B"; exit 2 ;;
 esac
 cat $S
