@@ -34,7 +34,6 @@ enum : u32 {
     STEP_TILE_L4 = 1u << 6, // tile kernel: four generations per LDS pass
     STEP_TILE_INPLACE = 1u << 7,  // tile kernel: one tile buffer updated in place (twice the rows)
     STEP_TILE_FOLD = 1u << 8,     // tile kernel: 32-lane tiles folded in half (fold plans, plan.hpp)
-    STEP_GATE = 1u << 9,    // temporal kernel: the full+gate first pass (StepParams::gate; launch_step sets it)
     STEP_SEAM = 1u << 5,    // temporal kernel: rows < 0 are read from StepParams::above, rows >= h
                             // from StepParams::below (sub-tile first pass: the other half's edges)
 };
@@ -56,14 +55,7 @@ struct StepParams {
     // Where lanes that store nothing (halo / idle lanes) write instead: kTrashWaves x 64 words, one
     // word per (wave mod kTrashWaves, lane).  Filled in by the launch functions (ensure_trash).
     u64* trash = nullptr;
-    // Exchange gate (step_temporal, ghost-row sources): a wave whose segment reads ghost rows first waits
-    // until gate[0] == gate_val (written by the comm stream, hipStreamWriteValue32, once the halo exchange
-    // is done), polling with system-scope loads and bounded by kGateWaitTicks; on timeout it sets gate[1]
-    // (the board is then invalid: the engine checks it at every readout) and proceeds.  nullptr: no gate.
-    u32* gate = nullptr;
-    u32 gate_val = 0;
 };
-constexpr unsigned long long kGateWaitTicks = 200000000ull;  // 2 s of s_memrealtime (100 MHz)
 constexpr int kTrashWaves = 1024;
 // Allocate the current device's trash buffer (call once per device before any launch or capture;
 // thread safe).

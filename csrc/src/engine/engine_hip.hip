@@ -74,14 +74,8 @@ HipEngine::HipEngine(const Geometry& g, const EngineConfig& c, std::shared_ptr<T
     if (R != L_.R) L_ = Layout(L_.h, L_.w, R);
     stats_.depth = R;
     // slack rows: the temporal kernel prefetches 3 (shallow passes: 6) rows past a segment's last input row
-    // (and kSlackBefore rows before row -R: a gated first pass streams its top segments upwards, full+gate,
-    // and prefetches as far past their first row)
     const size_t bytes = (size_t)(L_.words() + hipk::kSlackRows * L_.pitch) * 8;
-    const size_t before = (size_t)kSlackBefore * (size_t)L_.pitch * 8;
-    for (int i = 0; i < 2; ++i) {
-        HIP_CHECK(hipMalloc(&buf_raw_[i], before + bytes));
-        buf_[i] = buf_raw_[i] + (size_t)kSlackBefore * (size_t)L_.pitch;
-    }
+    for (int i = 0; i < 2; ++i) HIP_CHECK(hipMalloc(&buf_[i], bytes));
     alloc_bytes_ = bytes;
     device_transport_ = t_->device_buffers() && cfg_.transport != "host";
     // Register both boards (their ghost and edge rows are what the one-tile exchanges send and receive)
@@ -93,7 +87,7 @@ HipEngine::HipEngine(const Geometry& g, const EngineConfig& c, std::shared_ptr<T
     // halves), off with peers until a multi-GPU run has measured it; GOL_RCCL_REGISTER=0/1 forces.
     const int reg_default = t_->size() == 1 ? 1 : 0;
     if (device_transport_ && env_int("GOL_RCCL_REGISTER", reg_default) != 0 && !halo_items(L_.R).empty()) {
-        for (int i = 0; i < 2; ++i) reg_[i] = t_->register_buffer(buf_raw_[i], before + bytes);
+        for (int i = 0; i < 2; ++i) reg_[i] = t_->register_buffer(buf_[i], bytes);
         stats_registered_ = reg_[0] != nullptr && reg_[1] != nullptr;
     }
     if (cfg_.transport == "device" && !t_->device_buffers())
@@ -116,7 +110,7 @@ HipEngine::HipEngine(const Geometry& g, const EngineConfig& c, std::shared_ptr<T
     // All device memory work is ordered on the engine's own streams.  (They are non-blocking:
     // null-stream calls such as hipMemset, or a pageable hipMemcpy whose DMA may still be in
     // flight when it returns, would NOT be ordered before their kernels.)
-    for (int i = 0; i < 2; ++i) HIP_CHECK(hipMemsetAsync(buf_raw_[i], 0, before + bytes, s_comp_));
+    for (int i = 0; i < 2; ++i) HIP_CHECK(hipMemsetAsync(buf_[i], 0, bytes, s_comp_));
     HIP_CHECK(hipStreamSynchronize(s_comp_));
     // Stream-ordering events (never read by the host for data; event_flags: no system-scope fence)
     HIP_CHECK(hipEventCreateWithFlags(&ev_ready_, event_flags()));
@@ -125,9 +119,6 @@ HipEngine::HipEngine(const Geometry& g, const EngineConfig& c, std::shared_ptr<T
         for (auto* e : {&ev_t0_, &ev_t1_, &ev_t2_, &ev_t3_}) HIP_CHECK(hipEventCreate(e));
     }
     HIP_CHECK(hipMalloc(&d_red_, 2 * sizeof(u64)));
-    HIP_CHECK(hipMalloc(&d_gate_, 64));
-    HIP_CHECK(hipMemsetAsync(d_gate_, 0, 64, s_comp_));
-    HIP_CHECK(hipStreamSynchronize(s_comp_));
     HIP_CHECK(hipHostMalloc(&h_red_, 2 * sizeof(u64), hipHostMallocDefault));
     if (wd_)
         for (auto& m : mk_)
@@ -214,7 +205,7 @@ HipEngine::~HipEngine() {
         for (u64* p : *v) hipHostFree(p);
     for (void* h : reg_)
         if (h) t_->deregister_buffer(h);
-    for (int i = 0; i < 2; ++i) hipFree(buf_raw_[i]);
+    for (int i = 0; i < 2; ++i) hipFree(buf_[i]);
     for (auto& kv : res_plans_)
         for (void* q : {(void*)kv.second.d, (void*)kv.second.nbr_off, (void*)kv.second.nbr, (void*)kv.second.counters})
             if (q) hipFree(q);
@@ -222,9 +213,6 @@ HipEngine::~HipEngine() {
         if (q) hipFree(q);
     for (void* p : deferred_free_) hipFree(p);
     hipFree(d_red_);
-    for (auto& kv : gate_graphs_)
-        if (kv.second) hipGraphExecDestroy(kv.second);
-    hipFree(d_gate_);
     hipHostFree(h_red_);
     hipEventDestroy(ev_ready_);
     hipEventDestroy(ev_halo_);
@@ -350,7 +338,7 @@ void HipEngine::do_init(const PatternSpec& p) {
         // schedule (and the forced-split measurement mode).  The full schedule
         // exchanges on the compute stream itself: recording the event there every superstep
         // only idles the GPU (~15 us per record, a release fence).
-        events_needed_ = cfg_.force_split || ((split_ || gate_) && !halo_items(L_.R).empty());
+        events_needed_ = cfg_.force_split || (split_ && !halo_items(L_.R).empty());
     }
     stats_.kernel = split_ ? kern_[1] + "+boundary:" + kern_[2] : (dual_ ? std::string("temporal") : kern_[0]);
     if (!split_ && !dual_ && kern_[0] == "pipe")
@@ -359,7 +347,7 @@ void HipEngine::do_init(const PatternSpec& p) {
         const ResPlan& rp = res_plan(res_kin_);
         stats_.kernel = strprintf("resident@%d(%lld tiles x %d waves x %d rows)", res_kin_, (long long)rp.tiles, rp.nw, rp.B);
     }
-    stats_.schedule = split_ ? "split" : (halo_items(L_.R).empty() ? "local" : (gate_ ? "full+gate" : "full"));
+    stats_.schedule = split_ ? "split" : (halo_items(L_.R).empty() ? "local" : "full");
     if (dual_) stats_.schedule += sub_overlap_ ? "+subtiles2ov" : "+subtiles2";
     stats_.kernel_depth = dual_ ? tdepth_ : kdepth_;
     stats_.tile_waves = cfg_.tile_waves;
@@ -402,18 +390,6 @@ void HipEngine::do_init(const PatternSpec& p) {
             prepare(k);
     }
     prewarm_graph();
-    if (gate_ && cfg_.graph) {
-        // every (parity, flag value) graph of the superstep depths the runs use, so no timed run captures one
-        const int p0 = cur_;
-        for (int k : init_depths())
-            for (int p = 0; p < 2; ++p)
-                for (u32 v : {1u, 2u}) {
-                    cur_ = p;
-                    gate_graph(k, v);
-                }
-        cur_ = p0;
-        synchronize();
-    }
     if (dual_) {
         // One scratch superstep of each prepared depth (the halves are reloaded from the board at
         // the next run): the first launch of a kernel variant loads its code object, ~20 us that
@@ -444,7 +420,6 @@ void HipEngine::tile_superstep(int k) {
         cur_ ^= 1;
         return;
     }
-    if (gate_ && device_transport_ && !halo_items(L_.R).empty()) return gate_superstep(k);
     const std::vector<int>& ps = pass_depths(k);
     first_pass(k, ps[0], ext_after(ps, 0), split_);
     cur_ ^= 1;
@@ -458,75 +433,6 @@ void HipEngine::tile_superstep(int k) {
         cur_ ^= 1;
     }
     if (ps.size() > 1) mark_ready();  // the next exchange reads what the last pass wrote
-}
-
-// full+gate: the exchange on the comm stream (after the previous superstep's passes, which wrote what it sends)
-// ends by setting the gate flag to this superstep's value (1 and 2 alternate, so the flag never holds the value
-// a superstep waits for before its own exchange is done); the superstep's passes replay from a graph captured
-// at init on the compute stream (one launch, no gap between the passes), the first one gated: its segments
-// wait for the flag in the kernel, before their first ghost-row load (ROWS_GATE: near the end of their
-// streams).  The compute stream never waits for the comm stream: the first pass cannot complete before the
-// exchange, and the rest is stream-ordered after it.  (The exchange is never inside a graph: an RCCL group
-// captured on a forked stream and left unjoined crashes librccl, profiles/rccl_capture_crash_round6.txt.)
-// scratch (the init-time schedule timing): every pass reads the board and writes the other buffer, as the
-// other timed candidates do (time_schedule), so the board is left as it was.
-void HipEngine::gate_superstep(int k, bool scratch) {
-    prepare(k);
-    const u32 v = gate_phase_;
-    gate_phase_ = 3 - gate_phase_;
-    wait_pending(s_comm_, ev_ready_);
-    exchange_device(k, items_for(k), cur_, s_comm_);
-    HIP_CHECK(hipStreamWriteValue32(s_comm_, d_gate_, v, 0));
-    if (hipGraphExec_t g = gate_graph(k, v, scratch)) {
-        HIP_CHECK(hipGraphLaunch(g, s_comp_));
-        if (!scratch) cur_ ^= (int)(pass_depths(k).size() & 1);
-        stats_.graph_launches += 1;
-        gate_used_ = true;
-    } else {
-        gate_passes(k, v, scratch);
-    }
-    mark_ready();
-}
-
-// The passes of a gated superstep on the compute stream (eagerly, or into a capture): buf[cur] -> ...
-void HipEngine::gate_passes(int k, u32 v, bool scratch) {
-    const std::vector<int>& ps = pass_depths(k);
-    for (size_t j = 0; j < ps.size(); ++j) {
-        const i64 e = ext_after(ps, j);
-        launch(0, ps[j], e, buf_[cur_], buf_[cur_ ^ 1], s_comp_, 0, j == 0 ? v : 0u);
-        post(buf_[cur_ ^ 1], s_comp_, e);
-        if (!scratch) cur_ ^= 1;
-    }
-}
-
-// The captured passes of a gated superstep of k generations from the current parity, waiting for flag value v
-// (nullptr: graphs off or the capture failed; the passes then run eagerly).
-hipGraphExec_t HipEngine::gate_graph(int k, u32 v, bool scratch) {
-    if (!cfg_.graph || !graph_ok_) return nullptr;
-    const i64 key = (((i64)k * 2 + cur_) * 4 + v) * 2 + (scratch ? 1 : 0);
-    auto it = gate_graphs_.find(key);
-    if (it != gate_graphs_.end()) return it->second;
-    const int p0 = cur_;
-    hipGraph_t graph = nullptr;
-    hipGraphExec_t exec = nullptr;
-    try {
-        HIP_CHECK(hipStreamBeginCapture(s_comp_, hipStreamCaptureModeRelaxed));
-        gate_passes(k, v, scratch);
-        HIP_CHECK(hipStreamEndCapture(s_comp_, &graph));
-        HIP_CHECK(hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0));
-        HIP_CHECK(hipGraphDestroy(graph));
-        HIP_CHECK(hipGraphUpload(exec, s_comp_));
-    } catch (const Error& e) {
-        hipGraph_t g2 = nullptr;
-        hipStreamEndCapture(s_comp_, &g2);
-        if (g2) hipGraphDestroy(g2);
-        hipGetLastError();
-        exec = nullptr;
-        fprintf(stderr, "[gol] full+gate graph capture failed (eager passes): %s\n", e.what());
-    }
-    cur_ = p0;
-    gate_graphs_[key] = exec;
-    return exec;
 }
 
 // Exchange the kx-deep halo and run the first kernel pass (depth kp, output rows extended by e
@@ -637,7 +543,7 @@ void HipEngine::do_set_compat_halos(const std::vector<u64>& above, const std::ve
     synchronize();
 }
 
-void HipEngine::launch(int kind, int k, i64 e, const u64* src, u64* dst, hipStream_t s, u32 xflags, u32 gate_val) {
+void HipEngine::launch(int kind, int k, i64 e, const u64* src, u64* dst, hipStream_t s, u32 xflags) {
     if (kernel_ == "lds") {
         // full-row bands only (the LDS variant is never split by columns: can_overlap)
         for (const Region& r : regions(kind, 1))
@@ -647,11 +553,6 @@ void HipEngine::launch(int kind, int k, i64 e, const u64* src, u64* dst, hipStre
         if (p.st.out_words == 0) return;
         hipk::StepParams sp{L_.pitch, (i32)L_.h, (i32)L_.nw, L_.R, step_flags() | p.tflags | xflags};
         const PassKernel pk = pass_kernel(kind, k);
-        if (gate_val) {
-            sp.gate = d_gate_;
-            sp.gate_val = gate_val;
-            gate_used_ = true;
-        }
         if (pk == PK_TILE) {
             hipk::launch_step_tile(cfg_.tile_waves, k, src, dst, p.d, p.waves, p.rows, sp, s);
         } else if (pk == PK_PIPE) {

@@ -28,7 +28,6 @@ bool HipEngine::graph_shape(int& k, int& m) {
     // (GOL_GRAPH_SPLIT=1, a test knob, attempts that capture anyway: guard_exchange_stream refuses the
     // exchange on the comm stream, the capture fails and the supersteps run eagerly)
     if (!local && split_ && !split_capture_test_) return false;
-    if (!local && gate_) return false;  // (full+gate supersteps run eagerly: their flag write is a stream op)
     return true;
 }
 

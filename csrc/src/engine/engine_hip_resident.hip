@@ -76,17 +76,9 @@ void HipEngine::res_launch(int G, u64* src, u64* dst, hipStream_t s) {
 void HipEngine::check_res_status() {
     // every launch enqueued so far must be done before its fault words are read (pipe_fault reads its
     // flag with a null-stream copy, which the engine's non-blocking streams do not order)
-    if (pipe_used_ || res_status_ || gate_used_) synchronize();
+    if (pipe_used_ || res_status_) synchronize();
     if (pipe_used_ && hipk::pipe_fault())
         throw Error("step_pipe: a ring wait timed out (a stage never got its rows); the board is invalid");
-    if (gate_used_) {
-        u32 f = 0;
-        HIP_CHECK(hipMemcpyAsync(&f, d_gate_ + 1, sizeof(u32), hipMemcpyDeviceToHost, s_comp_));
-        HIP_CHECK(hipStreamSynchronize(s_comp_));
-        if (f != 0)
-            throw Error("full+gate: a first-pass segment timed out waiting for the halo exchange's flag; the board is "
-                        "invalid");
-    }
     if (!res_status_) return;
     u32 v = 0;
     HIP_CHECK(hipMemcpyAsync(&v, res_status_, sizeof(u32), hipMemcpyDeviceToHost, s_comp_));

@@ -173,14 +173,9 @@ void HipEngine::choose_schedule() {
         if (nbrs && device_transport_ && t_->graph_capturable() && cfg_.graph && !cfg_.profile && !cfg_.compat &&
             cfg_.graph_rccl < 0)
             cands.push_back("full+graph");
-        // the one-tile superstep whose first pass starts at once, its ghost-row segments gated on the exchange's flag
-        // (not when GOL_GRAPH_RCCL=1 asks for captured RCCL supersteps: gated supersteps run eagerly)
-        if (nbrs && cfg_.sched == "auto" && gate_eligible() && env_int("GOL_GATE", -1) != 0 && cfg_.graph_rccl != 1)
-            cands.push_back("full+gate");
     }
-    if (cfg_.sched == "gate" && nbrs && gate_eligible()) cands = {"full+gate"};
     graph_rccl_on_ = cfg_.graph_rccl == 1;
-    bool dual_ok = cfg_.subtiles != 0 && cands[0] != "split" && cfg_.sched != "gate" && dual_wanted();
+    bool dual_ok = cfg_.subtiles != 0 && cands[0] != "split" && dual_wanted();
     if (dual_ok) {
         double ok = dual_local_ok() ? 1.0 : 0.0;
         if (t_->size() > 1) ok = t_->allreduce_min(ok);
@@ -249,7 +244,6 @@ void HipEngine::choose_schedule() {
     destroy_sched_graphs();  // (they captured the communicator: destroy them before the comm can go)
     sched_pick_ = pick;
     split_ = pick == "split";
-    gate_ = pick == "full+gate";
     dual_ = pick.rfind("subtiles", 0) == 0;
     sub_overlap_ = pick == "subtiles+ov" ? 1 : 0;
     graph_rccl_on_ = cfg_.graph_rccl == 1 || pick == "full+graph";
@@ -420,15 +414,10 @@ void HipEngine::time_schedule(const std::string& c, int k, int reps, bool eager)
             time_schedule(base, k, reps, true);  // the same exchanges as the peers' replays
         return;
     }
-    const bool split0 = split_, gate0 = gate_;
+    const bool split0 = split_;
     split_ = c == "split";
-    gate_ = c == "full+gate";
     const std::vector<int>& ps = pass_depths(k);
     for (int i = 0; i < reps; ++i) {
-        if (gate_ && device_transport_) {  // (its passes replay from captured graphs, on scratch state)
-            gate_superstep(k, true);
-            continue;
-        }
         first_pass(k, ps[0], ext_after(ps, 0), split_);
         for (size_t j = 1; j < ps.size(); ++j) {
             const i64 e = ext_after(ps, j);
@@ -442,7 +431,6 @@ void HipEngine::time_schedule(const std::string& c, int k, int reps, bool eager)
         if (ps.size() > 1) mark_ready();
     }
     split_ = split0;
-    gate_ = gate0;
 }
 
 // The kernels of a split superstep's first pass at depth k: the interior (kind 1) and the bands next to

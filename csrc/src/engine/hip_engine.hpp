@@ -455,8 +455,7 @@ class HipEngine : public Engine {
 
     const DevPlan& plan(int kind, int k, i64 e = 0);
 
-    // gate_val != 0: the exchange gate of a full+gate first pass (StepParams::gate)
-    void launch(int kind, int k, i64 e, const u64* src, u64* dst, hipStream_t s, u32 xflags = 0, u32 gate_val = 0);
+    void launch(int kind, int k, i64 e, const u64* src, u64* dst, hipStream_t s, u32 xflags = 0);
 
     // Ghost words for widths that are not a multiple of 64 when the tile is its own E/W neighbour.
     void post(u64* buf, hipStream_t s, i64 rem = 0) {
@@ -596,30 +595,6 @@ class HipEngine : public Engine {
     bool multipass_ = false;
     std::map<int, std::vector<int>> passes_;
     bool split_ = false;   // superstep schedule: interior/boundary split with overlapped exchange
-    // full+gate (round 6): the exchange on the comm stream followed by a device flag (hipStreamWriteValue32
-    // of a per-superstep sequence number), the whole first pass on the compute stream at once; only its
-    // segments that read ghost rows wait for the flag, in the kernel (StepParams::gate) -- no cross-queue
-    // event, no interior / band split.  1-D one tile, aligned width; any pass kernel (step_temporal's waves,
-    // step_pipe's loader and the tile kernels' staging waves wait).
-    bool gate_ = false;
-    bool gate_used_ = false;  // some pass ran gated (its fault word is checked at readout)
-    u32* d_gate_ = nullptr;   // [0] the flag (the last exchanged sequence number), [1] the fault word
-    u32 gate_phase_ = 1;      // the flag value of the next gated superstep (1 and 2 alternate)
-    std::map<i64, hipGraphExec_t> gate_graphs_;  // (k, parity, flag value) -> the superstep's captured passes
-    void gate_superstep(int k, bool scratch = false);
-    void gate_passes(int k, u32 v, bool scratch);
-    hipGraphExec_t gate_graph(int k, u32 v, bool scratch = false);
-    // The compute and comm streams must sit on different hardware queues: a flag write queued behind its
-    // own gated kernel on a shared queue would wait for it (until the wait's bound faults the pass).  One
-    // engine per GPU guarantees that (the two streams' priorities differ: profiles/queue_probe.txt), i.e. an
-    // RCCL transport (RCCL refuses two ranks on one GPU).  Thread ranks sharing a GPU create two streams
-    // each, more than GPU_MAX_HW_QUEUES (4) can separate: only with GOL_GATE=1, for tests run with enough
-    // hardware queues (tests/test_gpu_gate.py: GPU_MAX_HW_QUEUES=32, P = 8).
-    bool gate_eligible() const {
-        const bool queues_ok = t_->name().rfind("rccl", 0) == 0 || env_int("GOL_GATE", -1) == 1;
-        return device_transport_ && queues_ok && !two_d() && L_.aligned() && !cfg_.compat && !cfg_.profile &&
-               !cfg_.force_split && kernel_ != "lds";
-    }
     bool halo_pending_ = false;  // split: the last superstep's bands on the comm stream are not joined (join_halo)
     std::map<std::string, double> sched_us_;  // choose_schedule: us per generation per candidate
     // measure_pass_costs: us per pass by depth, [0] one tile (kind-0 passes), [1] the two sub-tiles
@@ -632,9 +607,7 @@ class HipEngine : public Engine {
     unsigned long long mk_done_ = 0;  // markers retired so far
     std::mutex mk_mu_;
     bool mk_published_ = false;  // this superstep's marker is already published (sub-tile path)
-    u64* buf_[2] = {nullptr, nullptr};      // row -R of each board (inside its allocation, buf_raw_)
-    u64* buf_raw_[2] = {nullptr, nullptr};  // the allocations: kSlackBefore rows, the board, kSlackRows rows
-    static constexpr int kSlackBefore = 8;
+    u64* buf_[2] = {nullptr, nullptr};
     size_t alloc_bytes_ = 0;
     int cur_ = 0;
     hipStream_t s_comp_ = nullptr, s_comm_ = nullptr;

@@ -377,8 +377,6 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(5))) vo
     };
 #endif
     if (wv == 0) {
-        // (the exchange gate: only the loader reads the source buffer)
-        if (!WRAPY && p.gate && reads_ghost_rows(d.row0, nrows, K, p.h)) gate_wait(p.gate, p.gate_val);
 #if PIPE_STAMPS
         WaitAcc ai, ao;
         loader<WRAPY>(src, d, p, K, nrows + 2 * K, ring_of(0), ctr, ctr + NW, &ai, &ao);

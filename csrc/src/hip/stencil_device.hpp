@@ -8,7 +8,6 @@
 #include <hip/hip_runtime.h>
 
 #include "gol/bits.hpp"
-#include "gol/hip_kernels.hpp"
 
 namespace gol {
 namespace hipk {
@@ -148,31 +147,6 @@ __device__ __forceinline__ bool advance(Pipe<K>& P, u32& lo, u32& hi, int i) {
         }
     }
     return true;
-}
-
-// The exchange gate (StepParams::gate): poll the comm stream's flag with system-scope loads (it is written
-// by another queue's packet processor, not by a wave), bounded; then an agent-scope acquire, so this CU's
-// L1 holds no line of the ghost rows older than the exchange.  Wave-uniform.  (step_temporal's waves, step_pipe's loader, the tile kernels' staging waves.)
-__device__ __forceinline__ void gate_wait(u32* gate, u32 val) {
-    u64 t0 = 0;
-    for (int spin = 0;; ++spin) {
-        const u32 v = __builtin_amdgcn_readfirstlane(__hip_atomic_load(gate, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
-        if (v == val) break;
-        if (spin == 0) t0 = __builtin_amdgcn_s_memrealtime();
-        const u32 fault = __builtin_amdgcn_readfirstlane(__hip_atomic_load(gate + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-        if (__builtin_amdgcn_s_memrealtime() - t0 > kGateWaitTicks || fault != 0) {
-            __hip_atomic_store(gate + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // (all lanes, one word)
-            break;
-        }
-        __builtin_amdgcn_s_sleep(4);
-    }
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-}
-
-// Does this wave's segment read ghost rows (input rows [row0 - K, row0 + nrows + K) outside [0, h))?  Any lane.
-__device__ __forceinline__ bool reads_ghost_rows(int row0, int nrows, int K, int h) {
-    return __builtin_amdgcn_ballot_w64(row0 - K < 0 || row0 + nrows + K > h) != 0;
 }
 
 }  // namespace

@@ -59,7 +59,6 @@ __global__ __launch_bounds__(64 * kWavesPerBlock) void step_temporal(const u64* 
 
 template <int K>
 const void* kernel_for(u32 flags) {
-    if (flags & STEP_GATE) return (const void*)step_temporal<K, ROWS_GATE>;
     if (flags & STEP_SEAM) return (const void*)step_temporal<K, ROWS_SEAM>;
     return (flags & STEP_WRAP_Y) ? (const void*)step_temporal<K, ROWS_WRAP> : (const void*)step_temporal<K, ROWS_GHOST>;
 }
@@ -221,7 +220,7 @@ u64* trash_of_current_device() {
 
 void launch_step(int k, const u64* src, u64* dst, const LaneDesc* plan, i64 n_waves, const StepParams& p,
                  hipStream_t s) {
-    const void* f = kernel_of(k, p.flags | (p.gate ? (u32)STEP_GATE : 0u));
+    const void* f = kernel_of(k, p.flags);
     if (!f) throw Error(strprintf("no step kernel instantiated for depth %d", k));
     const dim3 grid((unsigned)(n_waves / kWavesPerBlock)), block(64 * kWavesPerBlock);
     StepParams pp = p;

@@ -223,9 +223,7 @@ __device__ __forceinline__ void tile_item(const u64* __restrict__ src, u64* __re
     u32* B = tile_lds + n_in * kTileRowU32;  // double-buffered: the second tile buffer
     u32* side = tile_lds + n_in * kTileRowU32;  // in place: NW x tile_side_rows(LV) private rows
 
-    // 1. stage rows row0-K .. row0+nrows+K-1 (two 4-byte DMAs per row: lo plane, hi plane); with the exchange
-    //    gate, a tile that reads ghost rows stages only after the flag (every staging wave waits)
-    if (!WRAPY && p.gate && reads_ghost_rows(d.row0, nrows, K, p.h)) gate_wait(p.gate, p.gate_val);
+    // 1. stage rows row0-K .. row0+nrows+K-1 (two 4-byte DMAs per row: lo plane, hi plane)
     for (int i = wv; i < n_in; i += NW) {
         int r = d.row0 - K + i;
         if (WRAPY) r = r < 0 ? r + p.h : (r >= p.h ? r - p.h : r);
@@ -369,8 +367,7 @@ __device__ __forceinline__ void fold_item(const u64* __restrict__ src, u64* __re
     u32* side = tile_lds + nb * kTileRowU32;  // in place: NW x tile_side_rows(LV) private rows
 
     // 1. stage LDS rows 0 .. Th+kFoldMirror+3: row j = tile row j (half 0) / T-1-j (half 1), tile row t
-    //    being board row row0-K+t; two 4-byte DMAs per row (lo plane, hi plane); gated as step_tile
-    if (!WRAPY && p.gate && reads_ghost_rows(d.row0, nrows, K, p.h)) gate_wait(p.gate, p.gate_val);
+    //    being board row row0-K+t; two 4-byte DMAs per row (lo plane, hi plane)
     const int half = lane >> 5;
     for (int i = wv; i < nb; i += NW) {
         const int t = half ? T - 1 - i : i;

@@ -26,22 +26,7 @@ namespace {
 //   ROWS_SEAM   rows < 0 come from p.above, rows >= h from p.below, rows 0..h-1 from the source
 //               buffer: the first pass of a sub-tile superstep reads the neighbouring half's edge rows
 //               in place (and the torus wrap), so no seam copy precedes it
-//   ROWS_GATE   ROWS_GHOST for the first pass of a full+gate superstep (StepParams::gate), whose ghost rows
-//               are being received while it runs.  A segment that reads the top ghost rows streams UPWARDS
-//               (B3/S23 is symmetric: the level pipeline is the same), so that in every segment the ghost
-//               rows come last; the wave waits for the exchange's flag only before its first ghost-row load,
-//               near the end of its stream, by when the exchange has long finished.  (Waiting at the start
-//               of the stream left those waves ~20 us behind the others in a one-round plan, and the pass
-//               ended on them: full+gate then only tied full+graph, profiles/gate_round6.txt.)
-enum { ROWS_GHOST = 0, ROWS_WRAP = 1, ROWS_SEAM = 2, ROWS_GATE = 3 };
-
-// Wave-wide min / max of a lane value (once per wave, at its start).
-__device__ __forceinline__ int wave_min_i32(int v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v = min(v, __shfl_xor(v, o));
-    return __builtin_amdgcn_readfirstlane(v);
-}
-__device__ __forceinline__ int wave_max_i32(int v) { return -wave_min_i32(-v); }
+enum { ROWS_GHOST = 0, ROWS_WRAP = 1, ROWS_SEAM = 2 };
 
 // Prefetch depth in rows.  Deep passes (K >= 5) are VALU bound and keep one row-triple in flight
 // (registers are what limits their occupancy).  Shallow passes are memory bound: a whole-board pass
@@ -75,14 +60,11 @@ struct WaveRunner {
     uint2* st;
     i64 st_stride;  // pitch for output lanes, 0 for halo/idle lanes (they write a trash slot)
     int lrow;       // tile row of the next load (ROWS_WRAP, ROWS_SEAM; wave-uniform)
-    i64 ldstep;     // ROWS_GATE: the load stream's row step (-pitch: streaming upwards)
-    int gate_at;    // ROWS_GATE: input index of the first ghost row (kNoGate: none, or already waited)
-    static constexpr int kNoGate = 1 << 30;
     uint2 pf[D];
     Pipe<K> P;
 
     __device__ __forceinline__ void next_row() {
-        ld += ROWS == ROWS_GATE ? ldstep : p.pitch;
+        ld += p.pitch;
         if (ROWS == ROWS_WRAP) {  // rows are periodic: row h is row 0 (branch-free select)
             ++lrow;
             const bool w = lrow == p.h;
@@ -99,32 +81,6 @@ struct WaveRunner {
                                           i64 wave_id)
         : p(p_), d(d_), n(nrows + 2 * K), hp((i64)p_.h * p_.pitch) {
         lrow = d.row0 - K;
-        bool up = false;
-        ldstep = p.pitch;
-        gate_at = kNoGate;
-        if (ROWS == ROWS_GATE) {
-            // input index of a segment's first ghost row: streaming down, row h at h + K - row0; streaming up
-            // (from row row0 + nrows + K - 1), row -1 at row0 + nrows + K; the wave's earliest lane counts
-            const bool top = __builtin_amdgcn_ballot_w64(d.row0 - K < 0) != 0;
-            const bool bot = __builtin_amdgcn_ballot_w64(d.row0 + nrows + K > p.h) != 0;
-            if (top && !bot) {
-                up = true;
-                gate_at = wave_min_i32(d.row0) + nrows + K;
-            } else if (bot && !top) {
-                gate_at = p.h + K - wave_max_i32(d.row0);
-            } else if (top && bot) {
-                gate_at = 0;  // ghost rows at both ends (a tile of fewer than ~2K rows): wait first
-            }
-            // ghost rows within the fill phase and its prefetch: wait before the first load
-            if (gate_at < ((2 * K + 2) / 3) * 3 + 2 * D + 6) {
-                gate_wait(p.gate, p.gate_val);
-                gate_at = kNoGate;
-            }
-            if (up) {
-                lrow = d.row0 + nrows + K - 1;
-                ldstep = -p.pitch;
-            }
-        }
         if (ROWS == ROWS_WRAP && lrow < 0) lrow += p.h;
         if (ROWS == ROWS_SEAM) {
             own0 = src + (i64)p.R * p.pitch;
@@ -140,9 +96,9 @@ struct WaveRunner {
         // per plan column: thousands of waves storing to the same few words every row, a hot spot
         // that held shallow memory-bound passes at ~55% of the HBM streaming rate.)
         const bool out = d.flags & LANE_STORE;
-        st = out ? reinterpret_cast<uint2*>(dst + (i64)((up ? d.row0 + nrows - 1 : d.row0) + p.R) * p.pitch + (d.col + 1))
+        st = out ? reinterpret_cast<uint2*>(dst + (i64)(d.row0 + p.R) * p.pitch + (d.col + 1))
                  : reinterpret_cast<uint2*>(p.trash + ((i64)(wave_id & (kTrashWaves - 1)) * 64 + (threadIdx.x & 63)));
-        st_stride = out ? (up ? -p.pitch : p.pitch) : 0;
+        st_stride = out ? p.pitch : 0;
 #pragma unroll
         for (int j = 0; j < D; ++j) {
             ROW_LOAD_INTO(pf[j]);
@@ -175,22 +131,9 @@ struct WaveRunner {
         st += st_stride;
     }
 
-    // ROWS_GATE: wait for the exchange before the first load of input row >= gate_at (last_row: the highest
-    // input index the caller is about to load).  A cold branch at the top of a loop iteration; the other
-    // row sources compile it away.
-    __device__ __forceinline__ void gate_point(int last_row) {
-        if constexpr (ROWS == ROWS_GATE) {
-            if (last_row >= gate_at) {
-                gate_wait(p.gate, p.gate_val);
-                gate_at = kNoGate;
-            }
-        }
-    }
-
     template <int PH, bool GUARD>
     __device__ __forceinline__ void body(int i) {
         if (GUARD && i >= n) return;
-        gate_point(i + D);
         u32 lo, hi;
         fetch<PH>(lo, hi);
         compute_store<PH, GUARD>(lo, hi, i);
@@ -215,7 +158,6 @@ struct WaveRunner {
     next_row();                                              \
     __builtin_amdgcn_sched_barrier(0);
             for (; i + 6 <= n; i += 6) {
-                gate_point(i + 11);
                 ROW6_STEP(0) ROW6_STEP(1) ROW6_STEP(2) ROW6_STEP(3) ROW6_STEP(4) ROW6_STEP(5)
             }
 #undef ROW6_STEP
@@ -234,7 +176,6 @@ struct WaveRunner {
                 // issued, s_waitcnt vmcnt(0), and the prefetch is lost.)
                 uint2 q[3];
                 for (; i + 6 <= n; i += 6) {
-                    gate_point(i + 8);
                     ROW_LOAD_INTO(q[0]);
                     next_row();
                     ROW_LOAD_INTO(q[1]);
@@ -258,7 +199,6 @@ struct WaveRunner {
                 }
             }
             for (; i + 3 <= n; i += 3) {
-                gate_point(i + 5);
                 // hoist the whole next triple's loads above this triple's compute
                 const uint2 x0 = pf[0], x1 = pf[1], x2 = pf[2];
                 ROW_LOAD_INTO(pf[0]);

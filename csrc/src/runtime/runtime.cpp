@@ -182,8 +182,8 @@ EngineConfig engine_config(const Options& o, const std::string& backend, int dev
     c.graph_rccl = tri("GOL_GRAPH_RCCL");
     c.plan_xcds = (int)env_int("GOL_PLAN_XCDS", 8);
     c.sched = env_str("GOL_SCHEDULE", "auto");
-    if (c.sched != "auto" && c.sched != "split" && c.sched != "full" && c.sched != "gate")
-        throw Error("GOL_SCHEDULE must be auto, split, full or gate (got " + c.sched + ")");
+    if (c.sched != "auto" && c.sched != "split" && c.sched != "full")
+        throw Error("GOL_SCHEDULE must be auto, split or full (got " + c.sched + ")");
     return c;
 }
 

@@ -162,41 +162,3 @@ def test_rccl_split_capture_refused(gol, rccl, monkeypatch, capfd):
     assert "capture's origin stream refused" in err, err[-2000:]
     assert st["schedule"] == "split" and st["graph_launches"] == 0, st
     assert np.array_equal(got, numpy_step(initial_board(5, H, 1, True, 5), gens))
-
-
-@pytest.mark.parametrize("graph", [True, False])
-@pytest.mark.parametrize("R,gens,hint", [(8, 3 * 8 + 5, 0), (32, 2 * 32 + 9, 0), (128, 25, 20)])
-def test_rccl_self_gate(gol, rccl, graph, R, gens, hint):
-    """full+gate: the exchange on the comm stream ends with a device flag (1 and 2 alternating per superstep),
-    the superstep's passes replay from a captured graph (or run eagerly) and only the first pass's segments
-    that read ghost rows wait for the flag, inside the kernel, before their first ghost-row load (segments
-    next to the top halo stream upwards); no cross-queue event.  Several supersteps, multi-pass supersteps,
-    and the driver's 5 + 20 cut."""
-    H, W = 2048, 4096
-    kw = dict(width=W, schedule="gate", subtiles=0, halo_depth=R, kernel="temporal", graph=graph)
-    if hint:
-        kw["run_hint"] = hint
-    s = gol.Simulation(H, rccl, self_exchange=True, backend="hip", device=0, **kw).init(5, seed=R)
-    st = s.stats()
-    assert st["schedule"] == "full+gate", st
-    if hint:
-        s.step(5)
-        s.step(hint)
-        total = 5 + hint
-    else:
-        s.step(gens)
-        total = gens
-    got = s.board()
-    st = s.stats()
-    assert st["exchanges"] >= 1 and (st["graph_launches"] >= 1) == graph, st
-    assert np.array_equal(got, numpy_step(random_board(H, W, R), total))
-
-
-def test_rccl_self_gate_auto_candidate(gol, rccl):
-    """With neighbours through RCCL, full+gate is a candidate of the init-time schedule timing."""
-    H, W, gens = 2048, 4096, 2 * 32 + 3
-    s = gol.Simulation(H, rccl, self_exchange=True, backend="hip", device=0, width=W, halo_depth=32,
-                       subtiles=0).init(5, seed=77)
-    assert "sched:full+gate=" in s.stats()["tuning"], s.stats()
-    s.step(gens)
-    assert np.array_equal(s.board(), numpy_step(random_board(H, W, 77), gens))
