@@ -138,7 +138,9 @@ void HipEngine::measure_pass_costs() {
                 dropped[i] = 1;
                 best[i] = 1e30;
             }
-            init_step("init: pass costs", cs[i].g.nw ? "pipe pass" : "pass", d, (float)(best[i] / d));
+            const std::string what =
+                cs[i].g.nw ? strprintf("pipe pass %dx%d,%d/CU", cs[i].g.nw - 1, cs[i].g.l, cs[i].g.wg) : std::string("pass");
+            init_step("init: pass costs", what.c_str(), d, (float)(best[i] / d));
         }
     HIP_CHECK(hipEventDestroy(e0));
     HIP_CHECK(hipEventDestroy(e1));

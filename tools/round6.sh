@@ -97,6 +97,22 @@ b6)
   { echo "== kbench_stamps 32768^2 step_pipe<9,3> 2/CU"; KB_PIPE=3 KB_PIPE_WG=2 KB_PIPE_STAMPS=1 timeout -k 5 90 build/kbench_stamps 32768 24 960 0 0 9; } >> $S 2>&1 || exit 1
   { echo "== kbench_stamps 4096 x 32768 step_pipe<11,2> 1/CU"; KB_W=32768 KB_PIPE=2 KB_PIPE_STAMPS=1 timeout -k 5 90 build/kbench_stamps 4096 20 960 0 0 11; } >> $S 2>&1 || exit 1
   ;;
+b7)
+  # the round-6 tree without full+gate: the whole GPU suite; config 3's strip six times in sequence, traced
+  # (the outlier hunt), one with the init log (the widened step_pipe pass-cost sweep); the driver's command;
+  # config 2 through the CLI; the other per-rank tiles
+  timeout -k 10 900 python -u -m pytest tests -x -q -m gpu --timeout 120 --timeout-method thread > $O/pytest_gpu.log 2>&1; rc=$?
+  echo "== pytest -m gpu rc=$rc: $(tail -1 $O/pytest_gpu.log)" >> $S; [ $rc -ne 0 ] && exit $rc
+  for v in 1 2 3 4 5 6; do
+    bash tools/trace_run.sh strip$v --size 4096 --width 32768 --self-exchange > /dev/null || exit 1
+    cat gpurun_out/trace_strip$v.txt >> $S
+  done
+  GOL_INIT_LOG=1 timeout -k 10 300 python3 bench.py --gpus 1 --steps 20 --warmup 5 --size 4096 --width 32768 --self-exchange > $O/strip_initlog.json 2> $O/strip_initlog.err || exit 1
+  grep -h '^{' $O/strip_initlog.json | python3 tools/bench_line.py strip_initlog >> $S
+  reps 3 "" || exit 1
+  for v in 1 2; do timeout -k 10 120 build/gol 5 8192 1000 256 0 > $O/cfg2_cli_$v.log 2>&1 || exit 1; echo "[cfg2 CLI gol 5 8192 1000 256 0] $(grep TOTAL $O/cfg2_cli_$v.log)" >> $S; done
+  reps 1 "--size 8192 --steps 1000" "--size 8192 --width 32768 --self-exchange" "--size 16384 --width 32768 --self-exchange" "--size 32768 --width 16384 --decomp 2d --self-exchange" "--size 32768 --steps 2000 --warmup 200" || exit 1
+  ;;
 *) echo "unknown batch $B"; exit 2 ;;
 esac
 cat $S
