@@ -113,6 +113,27 @@ b7)
   for v in 1 2; do timeout -k 10 120 build/gol 5 8192 1000 256 0 > $O/cfg2_cli_$v.log 2>&1 || exit 1; echo "[cfg2 CLI gol 5 8192 1000 256 0] $(grep TOTAL $O/cfg2_cli_$v.log)" >> $S; done
   reps 1 "--size 8192 --steps 1000" "--size 8192 --width 32768 --self-exchange" "--size 16384 --width 32768 --self-exchange" "--size 32768 --width 16384 --decomp 2d --self-exchange" "--size 32768 --steps 2000 --warmup 200" || exit 1
   ;;
+b8)
+  # evidence: smoke, the driver's command x5, BASELINE configs 1/3/4 (tools/baseline_configs.sh), a rocprofv3
+  # kernel-trace/stats profile of the driver's command, and a PMC A/B of the pair rule (kbench r0 vs r1)
+  timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1; rc=$?
+  echo "== smoke rc=$rc: $(tail -1 $O/smoke.log)" >> $S; fatal $rc && exit $rc
+  reps 5 "" || exit 1
+  bash tools/baseline_configs.sh cfg1 cfg3 cfg4 > $O/configs.log 2>&1; rc=$?
+  { echo "== BASELINE configs rc=$rc"; echo "cfg1: $(grep -h TOTAL gpurun_out/configs/cfg1_cpu_256.log)"; for f in gpurun_out/configs/cfg3_bench_32768.log gpurun_out/configs/cfg4_bench_65536_2d.log; do grep -h '^{' $f | python3 tools/bench_line.py "$(basename $f .log)"; done; } >> $S; fatal $rc && exit $rc
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof -o prof --output-format csv -- python3 bench.py --gpus 1 --steps 20 --warmup 5 > $O/prof.log 2>&1; rc=$?
+  echo "== rocprofv3 --kernel-trace --stats of the driver command rc=$rc: $(grep -h '^{' $O/prof.log | python3 tools/bench_line.py prof)" >> $S; fatal $rc && exit $rc
+  ctr="SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_ANY GRBM_GUI_ACTIVE SQ_WAVE_CYCLES"
+  for v in r0 r1; do
+    KB_FOLD=1 timeout -s KILL 60 rocprofv3 --kernel-trace --pmc $ctr -d $O/pmc_f32_$v -o p --output-format csv -- build/kbench_$v 8192 32 960 0 0 8 0 4 > $O/pmc_f32_$v.log 2>&1 || exit 1
+    KB_W=32768 KB_PIPE=2 timeout -s KILL 60 rocprofv3 --kernel-trace --pmc $ctr -d $O/pmc_p20_$v -o p --output-format csv -- build/kbench_$v 4096 20 960 0 0 11 > $O/pmc_p20_$v.log 2>&1 || exit 1
+  done
+  for f in $(find $O -name "*counter_collection.csv" | sort); do echo "== $f"; python3 tools/pmc_summary.py "$f" | grep -A12 "step_tile_fold\|step_pipe"; done >> $O/pmc_summary.txt 2>&1
+  # 8192^2 folded tiles with the pair rule: 8 vs 16 waves per workgroup (the 16-wave LV = 4 kernel now 101 VGPRs)
+  for round in 1 2; do for nw in 8 16; do for k in 24 32; do
+    echo "[kb fold nw=$nw K=$k] $(KB_FOLD=1 timeout -k 5 90 build/kbench_r1 8192 $k 1920 0 0 $nw 0 4 2>&1 | tail -1 | grep -o '"us_per_gen": [0-9.]*')" >> $S
+  done; done; done
+  ;;
 *) echo "unknown batch $B"; exit 2 ;;
 esac
 cat $S
