@@ -40,7 +40,16 @@ constexpr int prefetch_rows() {
 // (see WaveRunner::run) use the two-triple loop: K = 6, 7 and 12.  Measured at 32768^2, two halves
 // (profiles/pingpong_loop_ab.txt): K=7 12.2 -> 10.9 us/gen, K=12 12.8 -> 10.6, K=6 12.0 -> 11.8;
 // K=5 and 8 do not gain.
-constexpr unsigned kPingpongMask = (1u << 6) | (1u << 7) | (1u << 12);
+// step_temporal's rule: rule32, or (GOL_TEMPORAL_PAIR=1, experiment) the pair-shared rule of stencil_device.hpp
+// with the two-triple loop at K = 8 as well: in the one-triple loop the compiler waits for the fresh prefetch
+// (s_waitcnt vmcnt(0) 60 instructions after the loads, 24% slower: profiles/pair_rule_round6.txt).  With the
+// prefetch kept and 9% fewer instructions per row it still only ties at K = 8 and loses 2-4% at K = 5, 6, 12
+// (profiles/temporal_pair_round6.txt): this streaming kernel is not bound by its gate count.
+#ifndef GOL_TEMPORAL_PAIR
+#define GOL_TEMPORAL_PAIR 0
+#endif
+constexpr bool kTemporalPair = GOL_TEMPORAL_PAIR != 0 && kRulePair;
+constexpr unsigned kPingpongMask = (1u << 6) | (1u << 7) | (1u << 12) | (kTemporalPair ? (1u << 8) : 0u);
 // ... and, for the ghost-row variant only (the sub-tile passes after the first), K = 5
 constexpr unsigned kPingpongGhostMask = 1u << 5;
 template <int K, int ROWS>
@@ -126,7 +135,7 @@ struct WaveRunner {
 
     template <int PH, bool GUARD>
     __device__ __forceinline__ void compute_store(u32 lo, u32 hi, int i) {
-        if (!advance<K, PH, GUARD, false>(P, lo, hi, i)) return;  // (rule32: stencil_device.hpp, PAIR)
+        if (!advance<K, PH, GUARD, kTemporalPair>(P, lo, hi, i)) return;  // (stencil_device.hpp, PAIR)
         *st = make_uint2(lo, hi);
         st += st_stride;
     }

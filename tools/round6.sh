@@ -61,6 +61,21 @@ b2)
     fatal $rc && break
   done
   ;;
+b9)
+  # step_temporal with the pair rule and the two-triple loop at K = 8 (tp, GOL_TEMPORAL_PAIR=1) against the
+  # default build (r1: rule32 in step_temporal), interleaved
+  for round in 1 2 3; do
+    for cfg in "T8 -- 32768 8 1920" "H8 KB_SPLIT2=1 KB_BPC=2 -- 32768 8 1920" "H12 KB_SPLIT2=1 KB_BPC=1 -- 32768 12 1920" \
+               "T6 -- 32768 6 1920" "T5 -- 32768 5 1920"; do
+      set -- $cfg; lab=$1; shift; envs=(); while [ "$1" != "--" ]; do envs+=("$1"); shift; done; shift
+      for v in r1 tp; do
+        r=$(env "${envs[@]}" timeout -k 5 90 build/kbench_$v "$@" 2>&1 | tail -1); rc=$?
+        echo "[kb $lab $v] $(echo "$r" | grep -o '"us_per_gen": [0-9.]*')" >> $S
+        fatal $rc && exit $rc
+      done
+    done
+  done
+  ;;
 b3)
   # full+gate (exchange flag gating the first pass's ghost-row segments), the pair rule in tile/pipe only, the
   # widened step_pipe pass-cost candidates: tests, then the driver's cut on the weak-scaling rank and the strip
