@@ -76,6 +76,35 @@ b9)
     done
   done
   ;;
+b10)
+  # (GOL_COMM_CUS and its layout / plan-size knobs were removed after b10-b13: profiles/comm_cus_round6.txt)
+  # VERDICT round 5 item 1's CU-reserved comm stream (GOL_COMM_CUS): the compute cost of the mask on the local
+  # tile (both layouts), then the weak-scaling rank's cut through the self-exchange, split and auto, 8 and 16 CUs,
+  # the 2-D tile and the strip; one kernel trace of the masked split
+  pyt cu_tests.log tests/test_gpu_rccl.py -k "comm_cus or split" || exit 1
+  reps 2 "" "GOL_COMM_CUS=8" "GOL_COMM_CUS=8 GOL_COMM_CU_LAYOUT=1" || exit 1
+  reps 2 "--self-exchange" "GOL_COMM_CUS=8 --self-exchange" "GOL_COMM_CUS=8 GOL_SCHEDULE=split --self-exchange" \
+    "GOL_COMM_CUS=16 GOL_SCHEDULE=split --self-exchange" "GOL_COMM_CUS=8 GOL_COMM_CU_LAYOUT=1 GOL_SCHEDULE=split --self-exchange" || exit 1
+  reps 2 "--size 32768 --width 16384 --decomp 2d --self-exchange" "GOL_COMM_CUS=8 --size 32768 --width 16384 --decomp 2d --self-exchange" \
+    "--size 4096 --width 32768 --self-exchange" "GOL_COMM_CUS=8 --size 4096 --width 32768 --self-exchange" || exit 1
+  GOL_COMM_CUS=8 GOL_SCHEDULE=split bash tools/trace_run.sh cu8_split --self-exchange > /dev/null || exit 1
+  cat gpurun_out/trace_cu8_split.txt >> $S
+  ;;
+b11)
+  # GOL_COMM_CUS sweep: 2 and 4 reserved CUs (8 and 16 in b10), local and the self-exchange cut
+  reps 2 "GOL_COMM_CUS=2" "GOL_COMM_CUS=4" "GOL_COMM_CUS=2 --self-exchange" "GOL_COMM_CUS=4 --self-exchange" \
+    "GOL_COMM_CUS=4 GOL_SCHEDULE=split --self-exchange" "GOL_SUBTILES=0" || exit 1
+  ;;
+b12)
+  # is it the masked queue? the compute stream's mask with every CU (layout 2), local
+  reps 2 "GOL_COMM_CUS=8 GOL_COMM_CU_LAYOUT=2" "GOL_SUBTILES=0" "GOL_COMM_CUS=8 GOL_COMM_CU_LAYOUT=2 GOL_KERNEL=temporal" "GOL_SUBTILES=0 GOL_KERNEL=temporal" || exit 1
+  ;;
+b13)
+  # 8 CUs masked off the compute stream (layout 0), plans sized for 256 / 248 / 240 / 224 / 192 CUs, step_temporal
+  reps 1 "GOL_SUBTILES=0 GOL_KERNEL=temporal" || exit 1
+  for pc in 256 248 240 224 192; do reps 1 "GOL_COMM_CUS=8 GOL_PLAN_CUS=$pc GOL_KERNEL=temporal" || exit 1; done
+  for pc in 256 224; do reps 1 "GOL_COMM_CUS=8 GOL_COMM_CU_LAYOUT=1 GOL_PLAN_CUS=$pc GOL_KERNEL=temporal" || exit 1; done
+  ;;
 b3)
   # full+gate (exchange flag gating the first pass's ghost-row segments), the pair rule in tile/pipe only, the
   # widened step_pipe pass-cost candidates: tests, then the driver's cut on the weak-scaling rank and the strip
