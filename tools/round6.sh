@@ -105,6 +105,11 @@ b13)
   for pc in 256 248 240 224 192; do reps 1 "GOL_COMM_CUS=8 GOL_PLAN_CUS=$pc GOL_KERNEL=temporal" || exit 1; done
   for pc in 256 224; do reps 1 "GOL_COMM_CUS=8 GOL_COMM_CU_LAYOUT=1 GOL_PLAN_CUS=$pc GOL_KERNEL=temporal" || exit 1; done
   ;;
+b14)
+  # HIP runtime knobs against the driver command's fixed cost (launch to first kernel, last kernel to sync)
+  reps 3 "" "ROC_ACTIVE_WAIT_TIMEOUT=1000" "ROC_ACTIVE_WAIT_TIMEOUT=0" "ROC_CPU_WAIT_FOR_SIGNAL=0" "HIP_FORCE_DEV_KERNARG=0" \
+    "HIP_FORCE_DEV_KERNARG=1" "DEBUG_CLR_GRAPH_PACKET_CAPTURE=0" "DEBUG_CLR_GRAPH_PACKET_CAPTURE=1" "ROC_SKIP_KERNEL_ARG_COPY=1" || exit 1
+  ;;
 b3)
   # full+gate (exchange flag gating the first pass's ghost-row segments), the pair rule in tile/pipe only, the
   # widened step_pipe pass-cost candidates: tests, then the driver's cut on the weak-scaling rank and the strip
