@@ -326,20 +326,18 @@ void HipEngine::do_init(const PatternSpec& p) {
             if (d0 != kdepth_) tune_split_kinds(d0);
         }
         kick("init: schedule timing");
+        pass_us_[1].clear();  // (the halves' pass costs are measured when a sub-tile schedule is applied)
         choose_schedule();  // collective when ranks have neighbours
-        if (dual_) {
-            kick("init: pass costs");
-            measure_pass_costs();  // the two halves' (the sub-tile candidates ran the default cuts)
-        }
         kick("init: plans and graphs");
         tuned_ = true;
-        passes_.clear();  // the pass cuts may depend on the tuned kernel (pass_depths)
-        // The comm stream waits on the compute stream's ready event only in the split
-        // schedule (and the forced-split measurement mode).  The full schedule
-        // exchanges on the compute stream itself: recording the event there every superstep
-        // only idles the GPU (~15 us per record, a release fence).
-        events_needed_ = cfg_.force_split || (split_ && !halo_items(L_.R).empty());
+        finish_init();
+        if (!sched_runner_up_.empty()) confirm_schedule();
+        return;
     }
+    finish_init();
+}
+
+void HipEngine::finish_init() {
     stats_.kernel = split_ ? kern_[1] + "+boundary:" + kern_[2] : (dual_ ? std::string("temporal") : kern_[0]);
     if (!split_ && !dual_ && kern_[0] == "pipe")
         stats_.kernel = strprintf("pipe@%d(%dx%d,%d/CU)", pipe_k_, pipe_cur_.nw - 1, pipe_cur_.l, pipe_cur_.wg);
@@ -378,7 +376,7 @@ void HipEngine::do_init(const PatternSpec& p) {
                                 : ((p0.tflags & hipk::STEP_TILE_INPLACE) ? "inplace" : "double"),
                         (long long)p0.rows, (long long)p0.waves);
     }
-    stats_.tuning = tn;
+    stats_.tuning = tn + confirm_note_;
     stats_.registered = stats_registered_;
     // Build the plans of the supersteps the runs will use now (the full superstep and the
     // remainder of the hinted run length), so neither graph capture nor a hinted timed loop

@@ -239,11 +239,31 @@ void HipEngine::choose_schedule() {
                 if (cands[c] != "split" && (b2 == cands.size() || best[c] < best[b2])) b2 = c;
             pick = cands[b2];
         }
+        // the runner-up, when it timed within kConfirmMargin of the pick (identical on every rank: the
+        // timings are maxima over the ranks)
+        size_t ru = cands.size();
+        for (size_t c = 0; c < cands.size(); ++c)
+            if (cands[c] != pick && best[c] < 1e29 && (ru == cands.size() || best[c] < best[ru])) ru = c;
+        // (GOL_SCHED_CONFIRM=2, a test knob: confirm whatever the margin)
+        const int confirm = env_int("GOL_SCHED_CONFIRM", 1);
+        if (ru < cands.size() && cfg_.run_hint > 0 && confirm != 0 &&
+            (confirm == 2 || best[ru] <= (1.0 + kConfirmMargin) * sched_us_[pick]))
+            sched_runner_up_ = cands[ru];
         stats_.exchanges = 0;  // the timing exchanges and replays are not part of the run
         stats_.halo_bytes = 0;
         stats_.graph_launches = 0;
     }
     destroy_sched_graphs();  // (they captured the communicator: destroy them before the comm can go)
+    apply_schedule(pick);
+}
+
+// Make `pick` the schedule of the runs (choose_schedule, confirm_schedule).  The board is canonical
+// (buf_[cur_]) whenever this runs: at the end of the timing, or after predict_run.
+void HipEngine::apply_schedule(const std::string& pick) {
+    synchronize();
+    // the run graphs were captured for the previous schedule (their keys do not name it)
+    for (auto& kv : graphs_) HIP_CHECK(hipGraphExecDestroy(kv.second));
+    graphs_.clear();
     sched_pick_ = pick;
     split_ = pick == "split";
     dual_ = pick.rfind("subtiles", 0) == 0;
@@ -252,10 +272,39 @@ void HipEngine::choose_schedule() {
     if (dual_) {
         setup_dual();
         sub_current_ = false;  // the halves hold timing scratch: load the board at the next run
+        if (pass_us_[1].empty()) measure_pass_costs();  // the two halves' (the candidates ran the default cuts)
     } else if (sub_buf_[0][0]) {
         teardown_dual();
     }
-    passes_.clear();
+    passes_.clear();  // the pass cuts depend on the schedule (pass_costs) and the tuned kernels
+    // The comm stream waits on the compute stream's ready event only in the split schedule (and the
+    // forced-split measurement mode).  The full schedule exchanges on the compute stream itself:
+    // recording the event there every superstep only idles the GPU (~15 us per record, a release fence).
+    events_needed_ = cfg_.force_split || (split_ && !halo_items(L_.R).empty());
+}
+
+// The close call of choose_schedule settled on the real run() path: the runner-up set up in full and
+// predicted like the pick was (finish_init -> predict_run: the hinted run on a snapshot of the board,
+// bracketed as bench.py brackets it, max over the ranks); the faster prediction is kept.  Collective:
+// both predictions are identical on every rank, so is the decision.
+void HipEngine::confirm_schedule() {
+    const std::string first = sched_pick_, second = sched_runner_up_;
+    sched_runner_up_.clear();
+    const double p1 = stats_.predicted_us_per_gen;
+    if (p1 <= 0 || second.empty()) return;  // (no prediction: no hinted run, or fault injection)
+    if (wd_) wd_->kick("init: schedule confirm");
+    apply_schedule(second);
+    finish_init();
+    const double p2 = stats_.predicted_us_per_gen;
+    const bool keep = p2 > 0 && p2 < p1;
+    init_step("init: schedule confirm", (keep ? second : first).c_str(), 0, (float)(keep ? p2 : p1));
+    confirm_note_ = strprintf(" confirm:%s=%.3fus/gen,%s=%.3fus/gen", first.c_str(), p1, second.c_str(), p2);
+    if (!keep) {
+        apply_schedule(first);
+        finish_init();
+    } else {
+        stats_.tuning += confirm_note_;
+    }
 }
 
 // One timed sample of `reps` supersteps of k generations of schedule `c`, bracketed as bench.py

@@ -162,3 +162,19 @@ def test_rccl_split_capture_refused(gol, rccl, monkeypatch, capfd):
     assert "capture's origin stream refused" in err, err[-2000:]
     assert st["schedule"] == "split" and st["graph_launches"] == 0, st
     assert np.array_equal(got, numpy_step(initial_board(5, H, 1, True, 5), gens))
+
+
+@pytest.mark.parametrize("decomp,subtiles", [("1d", -1), ("2d", 0)])
+def test_rccl_schedule_confirm(gol, rccl, monkeypatch, decomp, subtiles):
+    """The close call of the schedule timing settled on the real run() path (confirm_schedule): the runner-up
+    is set up in full (sub-tile halves allocated or freed, graphs re-captured) and predicted on a snapshot of
+    the board, then kept or undone.  GOL_SCHED_CONFIRM=2 confirms whatever the margin.  The board must
+    survive both switches: exact against numpy after the run."""
+    monkeypatch.setenv("GOL_SCHED_CONFIRM", "2")
+    N, R = 1024, 32
+    gens = R + 9
+    kw = {} if subtiles < 0 else {"subtiles": subtiles}
+    got, st = _run(gol, rccl, N, gens, 12, halo_depth=R, decomp=decomp, run_hint=gens, **kw)
+    assert " confirm:" in st["tuning"], st
+    assert st["predicted_us_per_gen"] > 0, st
+    assert np.array_equal(got, numpy_step(initial_board(5, N, 1, True, 12), gens))

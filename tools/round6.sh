@@ -110,6 +110,12 @@ b14)
   reps 3 "" "ROC_ACTIVE_WAIT_TIMEOUT=1000" "ROC_ACTIVE_WAIT_TIMEOUT=0" "ROC_CPU_WAIT_FOR_SIGNAL=0" "HIP_FORCE_DEV_KERNARG=0" \
     "HIP_FORCE_DEV_KERNARG=1" "DEBUG_CLR_GRAPH_PACKET_CAPTURE=0" "DEBUG_CLR_GRAPH_PACKET_CAPTURE=1" "ROC_SKIP_KERNEL_ARG_COPY=1" || exit 1
   ;;
+b15)
+  # confirm_schedule: close calls of the schedule timing settled on the real run() path; the RCCL, engine and
+  # P = 8 thread-rank tests, then the per-rank tiles whose candidates time within a few % of each other
+  pyt confirm_tests.log tests/test_gpu_rccl.py tests/test_gpu_multirank_p8.py tests/test_gpu_engine.py || exit 1
+  reps 3 "--size 32768 --width 16384 --decomp 2d --self-exchange" "--self-exchange" "" "--size 4096 --width 32768 --self-exchange" || exit 1
+  ;;
 b3)
   # full+gate (exchange flag gating the first pass's ghost-row segments), the pair rule in tile/pipe only, the
   # widened step_pipe pass-cost candidates: tests, then the driver's cut on the weak-scaling rank and the strip
