@@ -116,6 +116,21 @@ b15)
   pyt confirm_tests.log tests/test_gpu_rccl.py tests/test_gpu_multirank_p8.py tests/test_gpu_engine.py || exit 1
   reps 3 "--size 32768 --width 16384 --decomp 2d --self-exchange" "--self-exchange" "" "--size 4096 --width 32768 --self-exchange" || exit 1
   ;;
+b16)
+  # step_pipe as two halves on two streams (KB_SPLIT2 with KB_PIPE) against the headline's two step_temporal halves
+  # and the one-tile step_pipe, 32768^2, 2 rounds
+  for round in 1 2; do
+    for cfg in "H8t KB_SPLIT2=1 KB_BPC=2 -- 32768 8 1920" "P24 KB_PIPE=3 KB_PIPE_WG=2 -- 32768 24 1920 0 0 9" \
+               "HP24w1 KB_SPLIT2=1 KB_PIPE=3 KB_PIPE_WG=1 -- 32768 24 1920 0 0 9" "HP24w2 KB_SPLIT2=1 KB_PIPE=3 KB_PIPE_WG=2 -- 32768 24 1920 0 0 9" \
+               "P36 KB_PIPE=3 -- 32768 36 1920 0 0 13" "HP36 KB_SPLIT2=1 KB_PIPE=3 -- 32768 36 1920 0 0 13" \
+               "HP16 KB_SPLIT2=1 KB_PIPE=2 -- 32768 16 1920 0 0 9" "HP20 KB_SPLIT2=1 KB_PIPE=2 -- 32768 20 1920 0 0 11"; do
+      set -- $cfg; lab=$1; shift; envs=(); while [ "$1" != "--" ]; do envs+=("$1"); shift; done; shift
+      r=$(env "${envs[@]}" timeout -k 5 90 build/kbench_r1 "$@" 2>&1 | tail -1); rc=$?
+      echo "[kb $lab] $(echo "$r" | grep -o '"us_per_gen": [0-9.]*')" >> $S
+      fatal $rc && exit $rc
+    done
+  done
+  ;;
 b3)
   # full+gate (exchange flag gating the first pass's ghost-row segments), the pair rule in tile/pipe only, the
   # widened step_pipe pass-cost candidates: tests, then the driver's cut on the weak-scaling rank and the strip
