@@ -68,3 +68,41 @@ def test_p8_bench_cut(gol, monkeypatch, name, kw, want):
         board[r0 : r0 + H] = b
     want_board = numpy_step(random_board(P * H, W, SEED), 25)
     assert np.array_equal(board, want_board), f"{int((board != want_board).sum())} cells differ"
+
+
+def test_p8_schedule_confirm(gol, monkeypatch):
+    """The init-time schedule timing's close call settled collectively on the run path (confirm_schedule,
+    forced with GOL_SCHED_CONFIRM=2): every rank sets up the runner-up, predicts it, and keeps or undoes it
+    on the max-over-ranks predictions, so all ranks end on ONE schedule; then the 5 + 20 cut is exact."""
+    monkeypatch.setenv("GOL_GRAPH_RCCL", "0")
+    monkeypatch.setenv("GOL_SPINUP_MS", "0")
+    monkeypatch.setenv("GOL_SCHED_CONFIRM", "2")
+    ts = gol.parallel.p2p_thread_transports(P)
+    out, errs = [None] * P, []
+
+    def rank_main(r):
+        try:
+            s = gol.Simulation(P * H, ts[r], backend="hip", device=0, global_mode=True, width=W, halo_depth=32,
+                               run_hint=20, kernel="temporal")
+            s.init(5, seed=SEED)
+            s.step(5)
+            s.step(20)
+            out[r] = (s.geometry.row0, s.board(), s.stats())
+        except Exception as e:  # pragma: no cover - reported below
+            errs.append(f"rank {r}: {e!r}")
+
+    th = [threading.Thread(target=rank_main, args=(r,)) for r in range(P)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=300)
+    assert not errs, errs
+    assert all(o is not None for o in out)
+    scheds = {o[2]["schedule"] for o in out}
+    assert len(scheds) == 1, scheds
+    assert all(" confirm:" in o[2]["tuning"] for o in out), out[0][2]["tuning"]
+    board = np.zeros((P * H, W), dtype=np.uint8)
+    for r0, b, st in out:
+        board[r0 : r0 + H] = b
+    want_board = numpy_step(random_board(P * H, W, SEED), 25)
+    assert np.array_equal(board, want_board), f"{int((board != want_board).sum())} cells differ"
