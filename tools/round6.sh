@@ -131,6 +131,24 @@ b16)
     done
   done
   ;;
+b18)
+  # the round-6 final tree (1/2): the whole GPU suite, smoke, the driver's command x5
+  timeout -k 10 900 python -u -m pytest tests -x -q -m gpu --timeout 200 --timeout-method thread > $O/pytest_gpu.log 2>&1; rc=$?
+  echo "== pytest -m gpu rc=$rc: $(tail -1 $O/pytest_gpu.log)" >> $S; [ $rc -ne 0 ] && exit $rc
+  timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1; rc=$?
+  echo "== smoke rc=$rc: $(tail -1 $O/smoke.log)" >> $S; fatal $rc && exit $rc
+  reps 5 "" || exit 1
+  ;;
+b19)
+  # the round-6 final tree (2/2): the per-rank tiles through RCCL, BASELINE configs 1/3/4, the 8-process torchrun
+  # rehearsal of the driver's multi-GPU launch (host-staged halos: 8 ranks share the one GPU)
+  reps 2 "--self-exchange" "--size 32768 --width 16384 --decomp 2d --self-exchange" "--size 4096 --width 32768 --self-exchange" || exit 1
+  bash tools/baseline_configs.sh cfg1 cfg3 cfg4 > $O/configs.log 2>&1; rc=$?
+  { echo "== BASELINE configs rc=$rc"; echo "cfg1: $(grep -h TOTAL gpurun_out/configs/cfg1_cpu_256.log)"; for f in gpurun_out/configs/cfg3_bench_32768.log gpurun_out/configs/cfg4_bench_65536_2d.log; do grep -h '^{' $f | python3 tools/bench_line.py "$(basename $f .log)"; done; } >> $S; fatal $rc && exit $rc
+  rm -f gpurun_out/rehearse/summary.txt
+  bash tools/rehearse_torchrun.sh > $O/rehearse.log 2>&1; rc=$?
+  echo "== tools/rehearse_torchrun.sh rc=$rc" >> $S; cat gpurun_out/rehearse/summary.txt >> $S
+  ;;
 b3)
   # full+gate (exchange flag gating the first pass's ghost-row segments), the pair rule in tile/pipe only, the
   # widened step_pipe pass-cost candidates: tests, then the driver's cut on the weak-scaling rank and the strip
