@@ -474,13 +474,15 @@ void HipEngine::first_pass(int kx, int kp, i64 e, bool split) {
             // post() reads the first and last words of EVERY row, so it must follow both the interior and
             // the bands on one stream.)
             const bool bands_comm = e == 0 && !prof && !(self_x() && !L_.aligned());
-            // A step_pipe interior (59 VGPRs per wave, 92 KiB of LDS per workgroup) leaves every CU room
-            // for RCCL's kernel (256 VGPRs, 37.6 KiB) and the bands, so it is issued first: the strip's
-            // driver cut 3.46-3.57 against 3.63-3.91 us/gen exchange first (interleaved, one box).  (Raising
-            // the bands' wave priority instead, s_setprio, slowed the interior more than it sped the bands:
-            // 3.90-6.35; profiles/strip_split_round5.txt batch 8.)
+            // The interior is issued first, before the exchange's host-side RCCL group launch: the interior
+            // then starts ~17 us after run() instead of ~46, and the exchange still runs beside it (its kernel
+            // stretches, 37.8 -> 43.6 us, the interior does not).  Config 4's 2-D tile 7.94 against 8.55-8.70
+            // us/gen, the weak rank's split 12.43-12.87 against 12.90-13.02 (profiles/split_order_round6.txt);
+            // the strip's step_pipe interior: 3.46-3.57 against 3.63-3.91 (profiles/strip_split_round5.txt).
+            // GOL_SPLIT_INT_FIRST=0 restores the exchange-first order.  (Raising the bands' wave priority
+            // instead, s_setprio, slowed the interior more than it sped the bands: 3.90-6.35, round 5.)
             guard_exchange_stream(s_comm_);  // (before any event query or launch of a capture attempt)
-            const bool int_first = bands_comm && pass_kernel(1, kp) == PK_PIPE;
+            const bool int_first = split_int_first_;
             if (int_first) launch(1, kp, 0, src, dst, s_comp_);
             wait_pending(s_comm_, ev_ready_);
             if (prof) HIP_CHECK(hipEventRecord(ev_t0_, s_comm_));

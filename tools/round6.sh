@@ -149,6 +149,22 @@ b19)
   bash tools/rehearse_torchrun.sh > $O/rehearse.log 2>&1; rc=$?
   echo "== tools/rehearse_torchrun.sh rc=$rc" >> $S; cat gpurun_out/rehearse/summary.txt >> $S
   ;;
+b20)
+  # the split superstep's interior issued before the exchange for every interior kernel (GOL_SPLIT_INT_FIRST=1; by
+  # default only a step_pipe interior of a one-pass superstep goes first): config 4's 2-D tile, the weak rank, the strip
+  reps 3 "GOL_SCHEDULE=split --size 32768 --width 16384 --decomp 2d --self-exchange" "GOL_SPLIT_INT_FIRST=1 GOL_SCHEDULE=split --size 32768 --width 16384 --decomp 2d --self-exchange" \
+    "GOL_SCHEDULE=split --self-exchange" "GOL_SPLIT_INT_FIRST=1 GOL_SCHEDULE=split --self-exchange" || exit 1
+  GOL_SPLIT_INT_FIRST=1 GOL_SCHEDULE=split bash tools/trace_run.sh t2d_intfirst --size 32768 --width 16384 --decomp 2d --self-exchange > /dev/null || exit 1
+  GOL_SCHEDULE=split bash tools/trace_run.sh t2d_split --size 32768 --width 16384 --decomp 2d --self-exchange > /dev/null || exit 1
+  cat gpurun_out/trace_t2d_intfirst.txt gpurun_out/trace_t2d_split.txt >> $S
+  ;;
+b21)
+  # interior-first as the split default: the split / RCCL / thread-rank / pipe tests, then the per-rank tiles through
+  # the auto schedule timing, new order against the old (GOL_SPLIT_INT_FIRST=0), interleaved
+  pyt split_tests.log tests/test_gpu_rccl.py tests/test_gpu_multirank_p8.py tests/test_gpu_pipe.py tests/test_gpu_engine.py -k "split or rccl or p8 or pipe" || exit 1
+  reps 3 "--size 32768 --width 16384 --decomp 2d --self-exchange" "GOL_SPLIT_INT_FIRST=0 --size 32768 --width 16384 --decomp 2d --self-exchange" \
+    "--self-exchange" "GOL_SPLIT_INT_FIRST=0 --self-exchange" "--size 4096 --width 32768 --self-exchange" "GOL_SPLIT_INT_FIRST=0 --size 4096 --width 32768 --self-exchange" || exit 1
+  ;;
 b3)
   # full+gate (exchange flag gating the first pass's ghost-row segments), the pair rule in tile/pipe only, the
   # widened step_pipe pass-cost candidates: tests, then the driver's cut on the weak-scaling rank and the strip
