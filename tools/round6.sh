@@ -165,6 +165,10 @@ b21)
   reps 3 "--size 32768 --width 16384 --decomp 2d --self-exchange" "GOL_SPLIT_INT_FIRST=0 --size 32768 --width 16384 --decomp 2d --self-exchange" \
     "--self-exchange" "GOL_SPLIT_INT_FIRST=0 --self-exchange" "--size 4096 --width 32768 --self-exchange" "GOL_SPLIT_INT_FIRST=0 --size 4096 --width 32768 --self-exchange" || exit 1
   ;;
+b22)
+  # config 4's 2-D tile: forced split against the auto schedule timing (which picks split), same box, interleaved
+  reps 3 "GOL_SCHEDULE=split --size 32768 --width 16384 --decomp 2d --self-exchange" "--size 32768 --width 16384 --decomp 2d --self-exchange" || exit 1
+  ;;
 b3)
   # full+gate (exchange flag gating the first pass's ghost-row segments), the pair rule in tile/pipe only, the
   # widened step_pipe pass-cost candidates: tests, then the driver's cut on the weak-scaling rank and the strip
