@@ -526,7 +526,11 @@ void HipEngine::first_pass(int kx, int kp, i64 e, bool split) {
         post(dst, s_comp_, e);
         if (prof) record_profile(true);
     }
-    mark_ready();
+    // The ready event marks the end of the superstep, for the next exchange: with later passes to come the
+    // caller records it after the last one (tile_superstep, time_schedule), and a record here would only put
+    // a release barrier between this pass and the next (a ~5.7 us gap on the compute queue: config 4's 2-D
+    // tile trace, profiles/split_order_round6.txt).  GOL_FIRST_PASS_MARK=1 restores it (A/B knob).
+    if (pass_depths(kx).size() == 1 || first_pass_mark_) mark_ready();
 }
 
 void HipEngine::do_set_compat_halos(const std::vector<u64>& above, const std::vector<u64>& below) {

@@ -169,6 +169,15 @@ b22)
   # config 4's 2-D tile: forced split against the auto schedule timing (which picks split), same box, interleaved
   reps 3 "GOL_SCHEDULE=split --size 32768 --width 16384 --decomp 2d --self-exchange" "--size 32768 --width 16384 --decomp 2d --self-exchange" || exit 1
   ;;
+b23)
+  # no ready-event record between a superstep's first and second pass (GOL_FIRST_PASS_MARK=1: the old record): tests,
+  # then config 4's 2-D tile, the forced-split weak rank, the strip, interleaved; a trace of the 2-D tile
+  pyt mark_tests.log tests/test_gpu_rccl.py tests/test_gpu_multirank_p8.py tests/test_gpu_engine.py tests/test_gpu_pipe.py || exit 1
+  reps 3 "--size 32768 --width 16384 --decomp 2d --self-exchange" "GOL_FIRST_PASS_MARK=1 --size 32768 --width 16384 --decomp 2d --self-exchange" \
+    "GOL_SCHEDULE=split --self-exchange" "GOL_FIRST_PASS_MARK=1 GOL_SCHEDULE=split --self-exchange" "--size 4096 --width 32768 --self-exchange" || exit 1
+  bash tools/trace_run.sh t2d_nomark --size 32768 --width 16384 --decomp 2d --self-exchange > /dev/null || exit 1
+  cat gpurun_out/trace_t2d_nomark.txt >> $S
+  ;;
 b3)
   # full+gate (exchange flag gating the first pass's ghost-row segments), the pair rule in tile/pipe only, the
   # widened step_pipe pass-cost candidates: tests, then the driver's cut on the weak-scaling rank and the strip
