@@ -178,6 +178,12 @@ b23)
   bash tools/trace_run.sh t2d_nomark --size 32768 --width 16384 --decomp 2d --self-exchange > /dev/null || exit 1
   cat gpurun_out/trace_t2d_nomark.txt >> $S
   ;;
+b24)
+  # (GOL_EXP_NO_END_RECORD was an experiment-only knob, removed after this batch: profiles/end_record_round6.txt)
+  # the headline's end-of-superstep event records: default (watchdog markers), --watchdog 0 (plain records), --watchdog 0
+  # with no end records (experiment knob, valid only because bench.py synchronises before the timed run), interleaved
+  reps 4 "" "--watchdog 0" "GOL_EXP_NO_END_RECORD=1 --watchdog 0" || exit 1
+  ;;
 b3)
   # full+gate (exchange flag gating the first pass's ghost-row segments), the pair rule in tile/pipe only, the
   # widened step_pipe pass-cost candidates: tests, then the driver's cut on the weak-scaling rank and the strip
