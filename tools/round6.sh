@@ -184,6 +184,16 @@ b24)
   # with no end records (experiment knob, valid only because bench.py synchronises before the timed run), interleaved
   reps 4 "" "--watchdog 0" "GOL_EXP_NO_END_RECORD=1 --watchdog 0" || exit 1
   ;;
+b26)
+  # (GOL_SPLIT_SWAP was removed after this batch: profiles/split_order_round6.txt, b26)
+  # GOL_SPLIT_SWAP=1: a split superstep's interior on the comm stream, exchange + bands + later passes on the compute
+  # stream; the split tests with it, then config 4's 2-D tile and the forced-split weak rank, interleaved; a trace
+  GOL_SPLIT_SWAP=1 pyt swap_tests.log tests/test_gpu_rccl.py tests/test_gpu_multirank_p8.py -k "split or 2d or p8 or confirm" || exit 1
+  reps 3 "--size 32768 --width 16384 --decomp 2d --self-exchange" "GOL_SPLIT_SWAP=1 --size 32768 --width 16384 --decomp 2d --self-exchange" \
+    "GOL_SCHEDULE=split --self-exchange" "GOL_SPLIT_SWAP=1 GOL_SCHEDULE=split --self-exchange" || exit 1
+  GOL_SPLIT_SWAP=1 bash tools/trace_run.sh t2d_swap --size 32768 --width 16384 --decomp 2d --self-exchange > /dev/null || exit 1
+  cat gpurun_out/trace_t2d_swap.txt >> $S
+  ;;
 b3)
   # full+gate (exchange flag gating the first pass's ghost-row segments), the pair rule in tile/pipe only, the
   # widened step_pipe pass-cost candidates: tests, then the driver's cut on the weak-scaling rank and the strip
