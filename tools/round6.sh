@@ -194,6 +194,19 @@ b26)
   GOL_SPLIT_SWAP=1 bash tools/trace_run.sh t2d_swap --size 32768 --width 16384 --decomp 2d --self-exchange > /dev/null || exit 1
   cat gpurun_out/trace_t2d_swap.txt >> $S
   ;;
+b27)
+  # n row bands of 32768^2 on n streams, step_temporal (kbench KB_SPLIT2=n), plans sized for KB_BPC waves per SIMD
+  for round in 1 2; do
+    for cfg in "n2b2 KB_SPLIT2=2 KB_BPC=2 -- 32768 8 1920" "n3b1 KB_SPLIT2=3 KB_BPC=1 -- 32768 8 1920" "n3b2 KB_SPLIT2=3 KB_BPC=2 -- 32768 8 1920" \
+               "n4b1 KB_SPLIT2=4 KB_BPC=1 -- 32768 8 1920" "n4b2 KB_SPLIT2=4 KB_BPC=2 -- 32768 8 1920" "n2k12 KB_SPLIT2=2 KB_BPC=1 -- 32768 12 1920" \
+               "n3k12 KB_SPLIT2=3 KB_BPC=1 -- 32768 12 1920" "n4k12 KB_SPLIT2=4 KB_BPC=1 -- 32768 12 1920"; do
+      set -- $cfg; lab=$1; shift; envs=(); while [ "$1" != "--" ]; do envs+=("$1"); shift; done; shift
+      r=$(env "${envs[@]}" timeout -k 5 90 build/kbench_r1 "$@" 2>&1 | tail -1); rc=$?
+      echo "[kb $lab] $(echo "$r" | grep -o '"us_per_gen": [0-9.]*')" >> $S
+      fatal $rc && exit $rc
+    done
+  done
+  ;;
 b3)
   # full+gate (exchange flag gating the first pass's ghost-row segments), the pair rule in tile/pipe only, the
   # widened step_pipe pass-cost candidates: tests, then the driver's cut on the weak-scaling rank and the strip
