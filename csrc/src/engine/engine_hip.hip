@@ -331,7 +331,7 @@ void HipEngine::do_init(const PatternSpec& p) {
         kick("init: plans and graphs");
         tuned_ = true;
         finish_init();
-        if (!sched_runner_up_.empty()) confirm_schedule();
+        if (!sched_runners_up_.empty()) confirm_schedule();
         return;
     }
     finish_init();

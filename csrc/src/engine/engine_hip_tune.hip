@@ -239,16 +239,18 @@ void HipEngine::choose_schedule() {
                 if (cands[c] != "split" && (b2 == cands.size() || best[c] < best[b2])) b2 = c;
             pick = cands[b2];
         }
-        // the runner-up, when it timed within kConfirmMargin of the pick (identical on every rank: the
-        // timings are maxima over the ranks)
-        size_t ru = cands.size();
-        for (size_t c = 0; c < cands.size(); ++c)
-            if (cands[c] != pick && best[c] < 1e29 && (ru == cands.size() || best[c] < best[ru])) ru = c;
+        // the runners-up (at most kMaxConfirm, fastest first) that timed within kConfirmMargin of the pick
+        // (identical on every rank: the timings are maxima over the ranks)
         // (GOL_SCHED_CONFIRM=2, a test knob: confirm whatever the margin)
         const int confirm = env_int("GOL_SCHED_CONFIRM", 1);
-        if (ru < cands.size() && cfg_.run_hint > 0 && confirm != 0 &&
-            (confirm == 2 || best[ru] <= (1.0 + kConfirmMargin) * sched_us_[pick]))
-            sched_runner_up_ = cands[ru];
+        std::vector<size_t> order;
+        for (size_t c = 0; c < cands.size(); ++c)
+            if (cands[c] != pick && best[c] < 1e29) order.push_back(c);
+        std::stable_sort(order.begin(), order.end(), [&](size_t a, size_t b) { return best[a] < best[b]; });
+        for (size_t c : order)
+            if (cfg_.run_hint > 0 && confirm != 0 && (int)sched_runners_up_.size() < kMaxConfirm &&
+                (confirm == 2 || best[c] <= (1.0 + kConfirmMargin) * sched_us_[pick]))
+                sched_runners_up_.push_back(cands[c]);
         stats_.exchanges = 0;  // the timing exchanges and replays are not part of the run
         stats_.halo_bytes = 0;
         stats_.graph_launches = 0;
@@ -283,25 +285,35 @@ void HipEngine::apply_schedule(const std::string& pick) {
     events_needed_ = cfg_.force_split || (split_ && !halo_items(L_.R).empty());
 }
 
-// The close call of choose_schedule settled on the real run() path: the runner-up set up in full and
+// The close call of choose_schedule settled on the real run() path: each runner-up set up in full and
 // predicted like the pick was (finish_init -> predict_run: the hinted run on a snapshot of the board,
-// bracketed as bench.py brackets it, max over the ranks); the faster prediction is kept.  Collective:
-// both predictions are identical on every rank, so is the decision.
+// bracketed as bench.py brackets it, max over the ranks); the fastest prediction is kept.  Collective:
+// the predictions are identical on every rank, so is the decision.
 void HipEngine::confirm_schedule() {
-    const std::string first = sched_pick_, second = sched_runner_up_;
-    sched_runner_up_.clear();
-    const double p1 = stats_.predicted_us_per_gen;
-    if (p1 <= 0 || second.empty()) return;  // (no prediction: no hinted run, or fault injection)
-    if (wd_) wd_->kick("init: schedule confirm");
-    apply_schedule(second);
-    finish_init();
-    const double p2 = stats_.predicted_us_per_gen;
-    const bool keep = p2 > 0 && p2 < p1;
-    init_step("init: schedule confirm", (keep ? second : first).c_str(), 0, (float)(keep ? p2 : p1));
-    confirm_note_ = strprintf(" confirm:%s=%.3fus/gen,%s=%.3fus/gen", first.c_str(), p1, second.c_str(), p2);
-    if (!keep) {
-        apply_schedule(first);
+    const std::vector<std::string> runners = sched_runners_up_;
+    sched_runners_up_.clear();
+    std::string best = sched_pick_;
+    double pbest = stats_.predicted_us_per_gen;
+    if (pbest <= 0 || runners.empty()) return;  // (no prediction: no hinted run, or fault injection)
+    std::string note = strprintf(" confirm:%s=%.3fus/gen", best.c_str(), pbest);
+    std::string current = best;
+    for (const std::string& c : runners) {
+        if (wd_) wd_->kick("init: schedule confirm");
+        apply_schedule(c);
         finish_init();
+        current = c;
+        const double p = stats_.predicted_us_per_gen;
+        note += strprintf(",%s=%.3fus/gen", c.c_str(), p);
+        if (p > 0 && p < pbest) {
+            best = c;
+            pbest = p;
+        }
+    }
+    init_step("init: schedule confirm", best.c_str(), 0, (float)pbest);
+    confirm_note_ = note;
+    if (best != current) {
+        apply_schedule(best);
+        finish_init();  // (appends confirm_note_ to stats.tuning)
     } else {
         stats_.tuning += confirm_note_;
     }

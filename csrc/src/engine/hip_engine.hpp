@@ -327,14 +327,15 @@ class HipEngine : public Engine {
     // generation wins.
     static constexpr int kSchedReps = 4;
     void choose_schedule();
-    // Close calls are settled on the real run() path: when the runner-up of the timing is within
-    // kConfirmMargin of the pick, both are set up in full and predicted (predict_run), and the faster
-    // prediction is kept (confirm_schedule; GOL_SCHED_CONFIRM=0 turns it off).  The timing runs one
+    // Close calls are settled on the real run() path: the runners-up of the timing within kConfirmMargin of
+    // the pick are set up in full and predicted (predict_run) like the pick, and the fastest prediction is
+    // kept (confirm_schedule; GOL_SCHED_CONFIRM=0 turns it off).  The timing runs one
     // superstep per sample on scratch state; the 2-D tile's split and full+graph timed within 1-2% of each
     // other and picked full+graph in half the inits, whose runs then measured 9.1-9.35 against split's 8.5
     // us/gen (docs/PERFORMANCE.md section 17).
     static constexpr double kConfirmMargin = 0.05;
-    std::string sched_runner_up_;  // set by choose_schedule when the call is close
+    static constexpr int kMaxConfirm = 2;        // runners-up predicted at most (the weak rank has three close schedules)
+    std::vector<std::string> sched_runners_up_;  // set by choose_schedule when the call is close
     std::string confirm_note_;     // the two predictions, appended to stats.tuning
     void apply_schedule(const std::string& pick);
     void finish_init();  // labels, plans, graphs, spin-up and the prediction of the current schedule

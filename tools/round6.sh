@@ -207,6 +207,12 @@ b27)
     done
   done
   ;;
+b28)
+  # confirm_schedule over up to two runners-up: the RCCL / thread-rank / engine tests, then the weak rank and the 2-D
+  # tile through the auto timing
+  pyt confirm3_tests.log tests/test_gpu_rccl.py tests/test_gpu_multirank_p8.py tests/test_gpu_engine.py || exit 1
+  reps 3 "--self-exchange" "--size 32768 --width 16384 --decomp 2d --self-exchange" || exit 1
+  ;;
 b3)
   # full+gate (exchange flag gating the first pass's ghost-row segments), the pair rule in tile/pipe only, the
   # widened step_pipe pass-cost candidates: tests, then the driver's cut on the weak-scaling rank and the strip
