@@ -455,6 +455,7 @@ void HipEngine::first_pass(int kx, int kp, i64 e, bool split) {
             stats_.t_compute_ms += ms;
         }
     } else if (split) {
+        bool bands_multi = false;  // the bands ran on the comm stream (a superstep with later passes)
         if (items.empty()) {
             // GOL_FORCE_SPLIT on a rank without neighbours: the multi-GPU stream structure
             // with an empty exchange (measures the split schedule's own cost on one GPU)
@@ -474,6 +475,14 @@ void HipEngine::first_pass(int kx, int kp, i64 e, bool split) {
             // post() reads the first and last words of EVERY row, so it must follow both the interior and
             // the bands on one stream.)
             const bool bands_comm = e == 0 && !prof && !(self_x() && !L_.aligned());
+            // With later passes too, the bands run on the comm stream right after the exchange, beside the
+            // interior's tail, and the compute stream waits for them before the next pass.  The bands read the
+            // old board and the fresh ghost rows and write rows the interior does not, so they need only the
+            // exchange; on the compute stream they waited for the interior as well and added their whole pass
+            // to the critical path.  Weak rank 11.75-12.17 against 12.32-12.54 us/gen, config 4's 2-D tile
+            // 7.72-7.80 against 7.88-7.99 (profiles/split_order_round6.txt, b30); GOL_SPLIT_BANDS_COMM=0
+            // restores the bands on the compute stream.
+            bands_multi = split_bands_comm_ && e > 0 && !prof && !(self_x() && !L_.aligned());
             // The interior is issued first, before the exchange's host-side RCCL group launch: the interior
             // then starts ~17 us after run() instead of ~46, and the exchange still runs beside it (its kernel
             // stretches, 37.8 -> 43.6 us, the interior does not).  Config 4's 2-D tile 7.94 against 8.55-8.70
@@ -488,7 +497,7 @@ void HipEngine::first_pass(int kx, int kp, i64 e, bool split) {
             if (prof) HIP_CHECK(hipEventRecord(ev_t0_, s_comm_));
             exchange_device(kx, items, cur_, s_comm_);
             if (prof) HIP_CHECK(hipEventRecord(ev_t1_, s_comm_));
-            if (!bands_comm) record_halo();
+            if (!bands_comm && !bands_multi) record_halo();
             if (prof) HIP_CHECK(hipEventRecord(ev_t2_, s_comp_));
             if (!int_first) launch(1, kp, 0, src, dst, s_comp_);
             if (bands_comm) {
@@ -498,6 +507,10 @@ void HipEngine::first_pass(int kx, int kp, i64 e, bool split) {
                 halo_pending_ = true;
                 mark_ready();
                 return;
+            }
+            if (bands_multi) {
+                launch(2, kp, e, src, dst, s_comm_);
+                record_halo();
             }
         } else {
             if (prof) HIP_CHECK(hipEventRecord(ev_t2_, s_comp_));
@@ -509,7 +522,7 @@ void HipEngine::first_pass(int kx, int kp, i64 e, bool split) {
             HIP_CHECK(hipEventRecord(ev_halo_, s_comm_));
         }
         HIP_CHECK(hipStreamWaitEvent(s_comp_, ev_halo_, 0));
-        launch(2, kp, e, src, dst, s_comp_);
+        if (!bands_multi) launch(2, kp, e, src, dst, s_comp_);
         post(dst, s_comp_, e);
         if (prof) record_profile(true);
     } else {

@@ -213,6 +213,29 @@ b28)
   pyt confirm3_tests.log tests/test_gpu_rccl.py tests/test_gpu_multirank_p8.py tests/test_gpu_engine.py || exit 1
   reps 3 "--self-exchange" "--size 32768 --width 16384 --decomp 2d --self-exchange" || exit 1
   ;;
+b29)
+  # kernel traces of the weak rank's split superstep (the confirmed schedule) and of the local headline
+  GOL_SCHEDULE=split bash tools/trace_run.sh selfx_split --self-exchange > /dev/null || exit 1
+  bash tools/trace_run.sh local_head > /dev/null || exit 1
+  cat gpurun_out/trace_selfx_split.txt gpurun_out/trace_local_head.txt >> $S
+  ;;
+b30)
+  # GOL_SPLIT_BANDS_COMM=1: a multi-pass split superstep's bands on the comm stream right after the exchange, beside the
+  # interior; the split tests with it, then the forced-split weak rank and config 4's 2-D tile, interleaved; traces
+  GOL_SPLIT_BANDS_COMM=1 pyt bandscomm_tests.log tests/test_gpu_rccl.py tests/test_gpu_multirank_p8.py -k "split or 2d or p8 or confirm" || exit 1
+  reps 3 "GOL_SCHEDULE=split --self-exchange" "GOL_SPLIT_BANDS_COMM=1 GOL_SCHEDULE=split --self-exchange" \
+    "GOL_SCHEDULE=split --size 32768 --width 16384 --decomp 2d --self-exchange" "GOL_SPLIT_BANDS_COMM=1 GOL_SCHEDULE=split --size 32768 --width 16384 --decomp 2d --self-exchange" || exit 1
+  GOL_SPLIT_BANDS_COMM=1 GOL_SCHEDULE=split bash tools/trace_run.sh selfx_bandscomm --self-exchange > /dev/null || exit 1
+  GOL_SPLIT_BANDS_COMM=1 GOL_SCHEDULE=split bash tools/trace_run.sh t2d_bandscomm --size 32768 --width 16384 --decomp 2d --self-exchange > /dev/null || exit 1
+  cat gpurun_out/trace_selfx_bandscomm.txt gpurun_out/trace_t2d_bandscomm.txt >> $S
+  ;;
+b31)
+  # the split bands beside the interior as the default: the whole GPU suite, then the per-rank tiles through the auto
+  # schedule timing (weak rank, config 4's 2-D tile, config 3's strip) and the driver's command
+  timeout -k 10 900 python -u -m pytest tests -x -q -m gpu --timeout 200 --timeout-method thread > $O/pytest_gpu.log 2>&1; rc=$?
+  echo "== pytest -m gpu rc=$rc: $(tail -1 $O/pytest_gpu.log)" >> $S; [ $rc -ne 0 ] && exit $rc
+  reps 3 "--self-exchange" "--size 32768 --width 16384 --decomp 2d --self-exchange" "--size 4096 --width 32768 --self-exchange" "" || exit 1
+  ;;
 b3)
   # full+gate (exchange flag gating the first pass's ghost-row segments), the pair rule in tile/pipe only, the
   # widened step_pipe pass-cost candidates: tests, then the driver's cut on the weak-scaling rank and the strip
