@@ -236,6 +236,17 @@ b31)
   echo "== pytest -m gpu rc=$rc: $(tail -1 $O/pytest_gpu.log)" >> $S; [ $rc -ne 0 ] && exit $rc
   reps 3 "--self-exchange" "--size 32768 --width 16384 --decomp 2d --self-exchange" "--size 4096 --width 32768 --self-exchange" "" || exit 1
   ;;
+b32)
+  # (GOL_SPLIT_RESERVE was removed after this batch: profiles/split_order_round6.txt, b32)
+  # GOL_SPLIT_RESERVE=n: the split interior's one-round plan leaves n workgroup slots free for the exchange's kernels;
+  # forced split, weak rank and config 4's 2-D tile, n = 0 / 8 / 16 / 32 interleaved; a trace of the 2-D tile at n = 16
+  reps 2 "GOL_SCHEDULE=split --self-exchange" "GOL_SPLIT_RESERVE=8 GOL_SCHEDULE=split --self-exchange" "GOL_SPLIT_RESERVE=16 GOL_SCHEDULE=split --self-exchange" "GOL_SPLIT_RESERVE=32 GOL_SCHEDULE=split --self-exchange" || exit 1
+  reps 2 "GOL_SCHEDULE=split --size 32768 --width 16384 --decomp 2d --self-exchange" "GOL_SPLIT_RESERVE=8 GOL_SCHEDULE=split --size 32768 --width 16384 --decomp 2d --self-exchange" \
+    "GOL_SPLIT_RESERVE=16 GOL_SCHEDULE=split --size 32768 --width 16384 --decomp 2d --self-exchange" "GOL_SPLIT_RESERVE=32 GOL_SCHEDULE=split --size 32768 --width 16384 --decomp 2d --self-exchange" || exit 1
+  GOL_SPLIT_RESERVE=16 GOL_SCHEDULE=split bash tools/trace_run.sh t2d_res16 --size 32768 --width 16384 --decomp 2d --self-exchange > /dev/null || exit 1
+  GOL_SPLIT_RESERVE=16 GOL_SCHEDULE=split bash tools/trace_run.sh selfx_res16 --self-exchange > /dev/null || exit 1
+  cat gpurun_out/trace_t2d_res16.txt gpurun_out/trace_selfx_res16.txt >> $S
+  ;;
 b3)
   # full+gate (exchange flag gating the first pass's ghost-row segments), the pair rule in tile/pipe only, the
   # widened step_pipe pass-cost candidates: tests, then the driver's cut on the weak-scaling rank and the strip
