@@ -216,6 +216,7 @@ HipEngine::~HipEngine() {
     hipHostFree(h_red_);
     hipEventDestroy(ev_ready_);
     hipEventDestroy(ev_halo_);
+    if (d_seq_) hipFree(d_seq_);
     for (auto& m : mk_)
         for (auto e : m.ev)
             if (e) hipEventDestroy(e);
@@ -510,6 +511,22 @@ void HipEngine::first_pass(int kx, int kp, i64 e, bool split) {
             }
             if (bands_multi) {
                 launch(2, kp, e, src, dst, s_comm_);
+                if (split_value_wait_) {
+                    // The compute stream waits for the bands with a stream memory op on a value written after
+                    // them, not with the event: the runtime polls it from a one-workgroup kernel queued right
+                    // behind the interior, and the next pass follows that kernel with no gap, where the event
+                    // wait cost the compute queue ~10-20 us.  Config 4's 2-D tile 7.41-7.48 against 7.70-8.02
+                    // us/gen, the weak rank's split 11.68-11.96 against 11.97-12.19 (profiles/split_order_round6.txt,
+                    // b33).  The write is always enqueued before the wait (no deadlock on a shared hardware queue),
+                    // and the next write only after the wait has passed (the next exchange waits for the superstep's
+                    // end), so waiting for equality is exact and immune to wrap-around.  GOL_SPLIT_VALUE_WAIT=0: the event.
+                    if (!d_seq_) {
+                        HIP_CHECK(hipMalloc(&d_seq_, sizeof(u32)));
+                        HIP_CHECK(hipMemsetAsync(d_seq_, 0, sizeof(u32), s_comm_));
+                    }
+                    ++seq_;
+                    HIP_CHECK(hipStreamWriteValue32(s_comm_, d_seq_, seq_, 0));
+                }
                 record_halo();
             }
         } else {
@@ -521,7 +538,10 @@ void HipEngine::first_pass(int kx, int kp, i64 e, bool split) {
             if (prof) HIP_CHECK(hipEventRecord(ev_t1_, s_comm_));
             HIP_CHECK(hipEventRecord(ev_halo_, s_comm_));
         }
-        HIP_CHECK(hipStreamWaitEvent(s_comp_, ev_halo_, 0));
+        if (bands_multi && split_value_wait_)
+            HIP_CHECK(hipStreamWaitValue32(s_comp_, d_seq_, seq_, hipStreamWaitValueEq, 0xFFFFFFFFu));
+        else
+            HIP_CHECK(hipStreamWaitEvent(s_comp_, ev_halo_, 0));
         if (!bands_multi) launch(2, kp, e, src, dst, s_comp_);
         post(dst, s_comp_, e);
         if (prof) record_profile(true);

@@ -180,17 +180,20 @@ def test_rccl_schedule_confirm(gol, rccl, monkeypatch, decomp, subtiles):
     assert np.array_equal(got, numpy_step(initial_board(5, N, 1, True, 12), gens))
 
 
-@pytest.mark.parametrize("int_first,mark,bands", [("0", "0", "1"), ("1", "1", "1"), ("0", "1", "0"), ("1", "0", "0")])
+@pytest.mark.parametrize("int_first,mark,bands,vwait", [("0", "0", "1", "1"), ("1", "1", "1", "0"), ("0", "1", "0", "1"),
+                                                       ("1", "0", "0", "0")])
 @pytest.mark.parametrize("decomp", ["1d", "2d"])
-def test_rccl_split_order_knobs(gol, rccl, monkeypatch, int_first, mark, bands, decomp):
+def test_rccl_split_order_knobs(gol, rccl, monkeypatch, int_first, mark, bands, vwait, decomp):
     """The split superstep's host order, ready-event record and band stream as knobs (the defaults -- interior
     first, no record between the first two passes, the bands on the comm stream beside the interior -- run in
     every split test above): the exchange enqueued before the interior (GOL_SPLIT_INT_FIRST=0), the record
-    after every first pass (GOL_FIRST_PASS_MARK=1) and the bands on the compute stream (GOL_SPLIT_BANDS_COMM=0),
+    after every first pass (GOL_FIRST_PASS_MARK=1), the bands on the compute stream (GOL_SPLIT_BANDS_COMM=0) and
+    the compute stream waiting for the comm stream's bands by event instead of by value (GOL_SPLIT_VALUE_WAIT=0),
     in 1-D and 2-D, supersteps of two passes and a remainder -- exact either way."""
     monkeypatch.setenv("GOL_SPLIT_INT_FIRST", int_first)
     monkeypatch.setenv("GOL_FIRST_PASS_MARK", mark)
     monkeypatch.setenv("GOL_SPLIT_BANDS_COMM", bands)
+    monkeypatch.setenv("GOL_SPLIT_VALUE_WAIT", vwait)
     N, R = 768, 24
     gens = 2 * R + 7
     got, st = _run(gol, rccl, N, gens, 21, halo_depth=R, kernel_depth=12, decomp=decomp, schedule="split",

@@ -247,6 +247,25 @@ b32)
   GOL_SPLIT_RESERVE=16 GOL_SCHEDULE=split bash tools/trace_run.sh selfx_res16 --self-exchange > /dev/null || exit 1
   cat gpurun_out/trace_t2d_res16.txt gpurun_out/trace_selfx_res16.txt >> $S
   ;;
+b33)
+  # GOL_SPLIT_VALUE_WAIT=1: the compute stream waits for the split bands with hipStreamWaitValue32 on a value the comm stream
+  # writes after them, instead of an event; tests, then forced split on the weak rank and config 4's 2-D tile; traces
+  GOL_SPLIT_VALUE_WAIT=1 pyt valuewait_tests.log tests/test_gpu_rccl.py tests/test_gpu_multirank_p8.py -k "split or 2d or p8 or confirm" || exit 1
+  reps 3 "GOL_SCHEDULE=split --self-exchange" "GOL_SPLIT_VALUE_WAIT=1 GOL_SCHEDULE=split --self-exchange" \
+    "GOL_SCHEDULE=split --size 32768 --width 16384 --decomp 2d --self-exchange" "GOL_SPLIT_VALUE_WAIT=1 GOL_SCHEDULE=split --size 32768 --width 16384 --decomp 2d --self-exchange" || exit 1
+  GOL_SPLIT_VALUE_WAIT=1 GOL_SCHEDULE=split bash tools/trace_run.sh selfx_vw --self-exchange > /dev/null || exit 1
+  GOL_SPLIT_VALUE_WAIT=1 GOL_SCHEDULE=split bash tools/trace_run.sh t2d_vw --size 32768 --width 16384 --decomp 2d --self-exchange > /dev/null || exit 1
+  cat gpurun_out/trace_selfx_vw.txt gpurun_out/trace_t2d_vw.txt >> $S
+  ;;
+b34)
+  # the value wait as the default: the whole GPU suite, then the per-rank tiles through the auto schedule timing and the
+  # driver's command
+  timeout -k 10 900 python -u -m pytest tests -x -q -m gpu --timeout 200 --timeout-method thread > $O/pytest_gpu.log 2>&1; rc=$?
+  echo "== pytest -m gpu rc=$rc: $(tail -1 $O/pytest_gpu.log)" >> $S; [ $rc -ne 0 ] && exit $rc
+  timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1; rc=$?
+  echo "== smoke rc=$rc: $(tail -1 $O/smoke.log)" >> $S; fatal $rc && exit $rc
+  reps 3 "--self-exchange" "--size 32768 --width 16384 --decomp 2d --self-exchange" "--size 4096 --width 32768 --self-exchange" "" || exit 1
+  ;;
 b3)
   # full+gate (exchange flag gating the first pass's ghost-row segments), the pair rule in tile/pipe only, the
   # widened step_pipe pass-cost candidates: tests, then the driver's cut on the weak-scaling rank and the strip
