@@ -266,6 +266,19 @@ b34)
   echo "== smoke rc=$rc: $(tail -1 $O/smoke.log)" >> $S; fatal $rc && exit $rc
   reps 3 "--self-exchange" "--size 32768 --width 16384 --decomp 2d --self-exchange" "--size 4096 --width 32768 --self-exchange" "" || exit 1
   ;;
+b35)
+  # (GOL_SPLIT_KERNEL_SIGNAL and the tile kernels' signal_done epilogue were removed after this batch: profiles/split_order_round6.txt, b35)
+  # the split bands' tile kernel publishes the stream value itself (last workgroup, GOL_SPLIT_KERNEL_SIGNAL=1): one small
+  # test under a short limit first, then the split tests, then the A/B against the runtime's write and traces
+  timeout -k 10 150 python -u -m pytest -x -v --timeout 60 --timeout-method thread 'tests/test_gpu_rccl.py::test_rccl_split_order_knobs[1d-0-0-1-1]' > $O/first.log 2>&1; rc=$?
+  echo "== first test rc=$rc: $(tail -1 $O/first.log)" >> $S; [ $rc -ne 0 ] && exit $rc
+  pyt ksig_tests.log tests/test_gpu_rccl.py tests/test_gpu_multirank_p8.py -k "split or 2d or p8 or confirm" || exit 1
+  reps 3 "--self-exchange" "GOL_SPLIT_KERNEL_SIGNAL=0 --self-exchange" \
+    "--size 32768 --width 16384 --decomp 2d --self-exchange" "GOL_SPLIT_KERNEL_SIGNAL=0 --size 32768 --width 16384 --decomp 2d --self-exchange" || exit 1
+  GOL_SCHEDULE=split bash tools/trace_run.sh selfx_ksig --self-exchange > /dev/null || exit 1
+  GOL_SCHEDULE=split bash tools/trace_run.sh t2d_ksig --size 32768 --width 16384 --decomp 2d --self-exchange > /dev/null || exit 1
+  cat gpurun_out/trace_selfx_ksig.txt gpurun_out/trace_t2d_ksig.txt >> $S
+  ;;
 b3)
   # full+gate (exchange flag gating the first pass's ghost-row segments), the pair rule in tile/pipe only, the
   # widened step_pipe pass-cost candidates: tests, then the driver's cut on the weak-scaling rank and the strip
