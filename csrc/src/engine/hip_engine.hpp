@@ -637,11 +637,11 @@ class HipEngine : public Engine {
     bool graph_ok_ = true;
     const bool split_capture_test_ = env_int("GOL_GRAPH_SPLIT", 0) != 0;
     const bool split_int_first_ = env_int("GOL_SPLIT_INT_FIRST", 1) != 0;  // split: interior issued before the exchange
-    const bool first_pass_mark_ = env_int("GOL_FIRST_PASS_MARK", 0) != 0;
+    const bool first_pass_mark_ = env_int("GOL_FIRST_PASS_MARK", 0) != 0;  // (A/B: the ready event after every first pass)
     const bool split_bands_comm_ = env_int("GOL_SPLIT_BANDS_COMM", 1) != 0;  // split bands beside the interior (first_pass)
     const bool split_value_wait_ = env_int("GOL_SPLIT_VALUE_WAIT", 1) != 0;  // the compute stream waits for the bands by value
     u32* d_seq_ = nullptr;  // its flag (device memory) and the last value written
-    u32 seq_ = 0;  // (A/B: the ready event after every first pass)
+    u32 seq_ = 0;
     bool graph_rccl_on_ = false;  // one-tile supersteps with an RCCL exchange are captured (choose_schedule)
     // timing graphs of the graphed schedule candidates ("local", "full+graph"), by name
     struct SchedGraph {
