@@ -279,6 +279,12 @@ b35)
   GOL_SCHEDULE=split bash tools/trace_run.sh t2d_ksig --size 32768 --width 16384 --decomp 2d --self-exchange > /dev/null || exit 1
   cat gpurun_out/trace_selfx_ksig.txt gpurun_out/trace_t2d_ksig.txt >> $S
   ;;
+b36)
+  # config 3's strip: the auto cut (one step_pipe pass of 20) against forced pass depths, now that a multi-pass split
+  # superstep runs its bands beside the interior; 2 interleaved rounds
+  reps 2 "--size 4096 --width 32768 --self-exchange" "--kernel-depth 12 --size 4096 --width 32768 --self-exchange" \
+    "--kernel-depth 10 --size 4096 --width 32768 --self-exchange" "--kernel-depth 8 --size 4096 --width 32768 --self-exchange" || exit 1
+  ;;
 b3)
   # full+gate (exchange flag gating the first pass's ghost-row segments), the pair rule in tile/pipe only, the
   # widened step_pipe pass-cost candidates: tests, then the driver's cut on the weak-scaling rank and the strip
